@@ -1,0 +1,150 @@
+/* g2048.h -- C ABI of the MI355X-native batched 2048 environment + replay ring.
+ *
+ * The drop-in boundary for the reference's hot path (ribal-aladeeb/reinforcement-learning-2048).
+ * The reference has no FFI: its seams are Python callables operating on ONE Board2048 at a
+ * time.  Each entry point below cites the reference interface it replaces; the Python mirror
+ * (reinforcement-learning-2048_amd/g2048/dqn_lib.py) binds these through ctypes with the
+ * reference's own function names.  See INTEGRATION.md for the bindings.
+ *
+ * Conventions
+ *  - Boards are 16 log2 exponents (u8, 0 = empty), row-major: cell(r, c) = 4r + c.  This is
+ *    exactly Board2048.log_scale() (src/board.py:224-231) of the reference's int64 values.
+ *  - Actions: 0 = up, 1 = down, 2 = left, 3 = right (src/board.py:191, :129).
+ *  - Legal masks: bit a set iff move a changes the board (src/board.py:128-135).
+ *  - Every call returns 0 (G2048_OK) or a negative g2048_status; nothing throws across the ABI;
+ *    g2048_last_error() returns a thread-local message for the last failure.
+ *  - Every pointer named *dev* / every buffer argument is DEVICE memory on the env's device,
+ *    owned by the caller unless the object was made by *_create (library-owned).
+ *  - All step / sample calls are stream-ordered and asynchronous (no host sync, no allocation),
+ *    so they may be captured into a hipGraph.  `stream` is a hipStream_t (NULL = default).
+ *  - One env per stream; distinct envs are thread-safe, concurrent calls on one env are not.
+ *  - Randomness is counter-based Philox4x32-10.  Board g (global id = board_offset + i) owns
+ *    rocRAND philox4x32_10 subsequence g: its step draw at step t is the 4-word block
+ *    rocrand_init(seed, g, 4t) would return first (domain bits 30-31 of the subsequence word
+ *    select step / auto-reset / explicit-reset / sampler draws).  No per-lane state in HBM
+ *    beyond the per-board step counter.
+ */
+#ifndef G2048_H
+#define G2048_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define G2048_ABI_VERSION 1
+
+#ifndef G2048_API
+#define G2048_API __attribute__((visibility("default")))
+#endif
+
+typedef enum {
+    G2048_OK = 0,
+    G2048_EINVAL = -1,   /* bad argument (size, null, dtype) */
+    G2048_EHIP = -2,     /* HIP runtime error */
+    G2048_ENOMEM = -3,
+    G2048_EBADINPUT = -4 /* device-side input errors were counted (see g2048_env_error_count) */
+} g2048_status;
+
+typedef enum {
+    G2048_P4_10 = 1u,         /* spawn a 4 with p = 0.1 (default: p = 0.5, src/board.py:12,49) */
+    G2048_EGREEDY_FIXED = 2u, /* greedy over legal moves only / explore among legal moves;
+                                 default reproduces src/dqn_lib.py:25-29 bit-for-bit (F5) */
+    G2048_NO_AUTORESET = 4u   /* leave terminal boards in place (tests) */
+} g2048_flags;
+
+typedef enum { G2048_F32 = 0, G2048_F64 = 1 } g2048_dtype;
+
+typedef struct g2048_env g2048_env;
+typedef struct g2048_replay g2048_replay;
+
+/* ---- environment -------------------------------------------------------------------------
+ * State per board i: board u8[16]; meta u32[4] = {score, moves, steps_lo, steps_hi} (score =
+ * Board2048._mergescore, moves = len(_action_history) of the running episode, steps = RNG
+ * step counter); ep u32[4] = {episodes finished, last score, last moves, last max exponent}
+ * (the Experiment.add_episode fields, src/experiments.py:112-122). */
+
+/* Replaces `Board2048()` x n_boards (src/board.py:10-20): allocates and resets n boards. */
+G2048_API int g2048_env_create(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,
+                     int device_id, uint32_t flags, void* stream);
+/* Same, over caller-owned device buffers board u8[n][16], meta u32[n][4], ep u32[n][4]
+ * (16-byte aligned).  If reset != 0 the boards are reset (2 spawns each), else left as given. */
+G2048_API int g2048_env_wrap(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,
+                   int device_id, uint32_t flags, uint8_t* board_dev, uint32_t* meta_dev,
+                   uint32_t* ep_dev, int reset, void* stream);
+G2048_API void g2048_env_destroy(g2048_env* env);
+/* Device views of the env state (library-owned or wrapped). */
+G2048_API int g2048_env_views(g2048_env* env, uint8_t** board_dev, uint32_t** meta_dev, uint32_t** ep_dev);
+G2048_API int64_t g2048_env_size(const g2048_env* env);
+
+/* Re-deal fresh boards (2 spawns, src/board.py:18-20) where reset_mask_dev[i] != 0 (all if NULL). */
+G2048_API int g2048_env_reset(g2048_env* env, const uint8_t* reset_mask_dev, void* stream);
+
+/* One env step of every board.  Replaces Board2048.peek_action (src/board.py:185-202) +
+ * available_moves_as_torch_unit_vector (:128-135) + reward_func_merge_score
+ * (src/dqn_lib.py:87-88) + the done test (src/dqn_lib.py:17-18).
+ *  actions_dev  u8[n] (0..3) or NULL = uniform random action per board (np.random.randint(4)).
+ *  reward_dev   i32[n] merge-score gain (0 for invalid / terminal moves), or NULL
+ *  done_dev     u8[n]  1 iff the board had no legal move BEFORE this step, or NULL
+ *  legal_dev    u8[n]  legal mask of the board before this step, or NULL
+ *  rb           replay ring to append (s, a, r, s', done) to, or NULL (src/dqn_lib.py:106)
+ * A terminal board records the self-transition (s, a, 0, s, 1) (F6) and is then re-dealt unless
+ * G2048_NO_AUTORESET.  An action > 3 is counted as a device-side input error and is a no-op. */
+G2048_API int g2048_env_step(g2048_env* env, const uint8_t* actions_dev, int32_t* reward_dev,
+                   uint8_t* done_dev, uint8_t* legal_dev, g2048_replay* rb, void* stream);
+
+/* Fused epsilon-greedy select + step + replay append: replaces play_one_step
+ * (src/dqn_lib.py:91-107) with epsilon_greedy_policy (:16-30) for every board at once.
+ *  q_dev      Q-values [n][4] of the current boards, dtype q_dtype (f32 or f64)
+ *  eps_dev    f64 scalar on device (read at kernel time, graph-safe), or NULL -> use eps
+ *  action_dev u8[n] chosen actions out, or NULL */
+G2048_API int g2048_env_step_egreedy(g2048_env* env, const void* q_dev, int q_dtype, const double* eps_dev,
+                           double eps, int32_t* reward_dev, uint8_t* done_dev,
+                           uint8_t* action_dev, g2048_replay* rb, void* stream);
+
+/* Test entry: actions + injected spawns (cell index -1..15, exponent) instead of Philox draws,
+ * so trajectories recorded from the reference replay bit-for-bit. */
+G2048_API int g2048_env_step_inject(g2048_env* env, const uint8_t* actions_dev, const int8_t* spawn_idx_dev,
+                          const uint8_t* spawn_exp_dev, int32_t* reward_dev, uint8_t* done_dev,
+                          uint8_t* legal_dev, void* stream);
+
+/* k_steps random-policy env steps per launch with the board held in registers (replay pre-fill,
+ * env-only throughput).  Identical results to k_steps calls of g2048_env_step(actions=NULL).
+ * reward_sum_dev (i64[n], accumulated, or NULL). */
+G2048_API int g2048_env_rollout(g2048_env* env, int32_t k_steps, g2048_replay* rb, int64_t* reward_sum_dev,
+                      void* stream);
+
+/* Device-side input errors counted since the last call (synchronises `stream`). */
+G2048_API int g2048_env_error_count(g2048_env* env, int64_t* count_out, void* stream);
+
+/* ---- replay ring (replaces the deque of (Board, a, r, Board, done), src/dqn_lib.py:172) ----
+ * SoA in HBM: s u8[C][16], s2 u8[C][16], a u8[C], r i32[C], d u8[C], count u64 (valid rows).
+ * The env appends board i of step t at row (t mod (C/n)) * n + i, so C must be a multiple of the
+ * appending env's n. */
+G2048_API int g2048_replay_create(g2048_replay** out, int64_t capacity, int device_id, void* stream);
+G2048_API int g2048_replay_wrap(g2048_replay** out, int64_t capacity, int device_id, uint8_t* s_dev,
+                      uint8_t* s2_dev, uint8_t* a_dev, int32_t* r_dev, uint8_t* d_dev,
+                      uint64_t* count_dev);
+G2048_API void g2048_replay_destroy(g2048_replay* rb);
+G2048_API int g2048_replay_views(g2048_replay* rb, uint8_t** s_dev, uint8_t** s2_dev, uint8_t** a_dev,
+                       int32_t** r_dev, uint8_t** d_dev, uint64_t** count_dev);
+
+/* sample_experiences + extract_samples_conv/_dense (src/dqn_lib.py:33-84) for a whole batch:
+ * gather rows idx_dev[b] (i64[B]; NULL -> uniform with replacement over [0, count) from Philox
+ * (seed, epoch, b)) and encode them.  s_out/s2_out: [B][16] of `dtype` (f32/f64; the conv view
+ * [B,1,4,4] is the same memory), a_out i64[B], r_out/d_out [B] of `dtype`, idx_out i64[B] or
+ * NULL.  Any of the outputs may be NULL. */
+G2048_API int g2048_replay_sample_encode(g2048_replay* rb, const int64_t* idx_dev, int64_t batch,
+                               uint64_t seed, uint64_t epoch, int dtype, void* s_out,
+                               void* s2_out, int64_t* a_out, void* r_out, void* d_out,
+                               int64_t* idx_out, void* stream);
+
+/* ---- misc ---- */
+G2048_API const char* g2048_last_error(void);
+G2048_API int g2048_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* G2048_H */

@@ -1,0 +1,328 @@
+/* oracle2048.c -- TEST INFRASTRUCTURE ONLY (see oracle2048.h).
+ *
+ * A deliberately plain, loop-by-loop restatement.  It shares no code with the HIP kernels in
+ * reinforcement-learning-2048_amd/csrc/: the kernels use packed-byte (SWAR) arithmetic and
+ * v_perm_b32 transposes; this file walks cells one at a time the way src/board.py does.
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).
+ */
+#include "oracle2048.h"
+
+#include <string.h>
+
+/* ------------------------------------------------------------------ slide / score */
+
+/* src/board.py:92-126, restated on tile VALUES (2^e) exactly as the reference loop runs:
+ * a `current` cursor, the first non-zero strictly right of it, and four cases
+ * (fill the hole / merge + score / adjacent stop / pull next to current). */
+uint32_t o2048_slide_row(const uint8_t in[4], uint8_t out[4]) {
+    int64_t v[4];
+    uint32_t score = 0;
+    for (int i = 0; i < 4; ++i) v[i] = in[i] ? ((int64_t)1 << in[i]) : 0;
+    int current = 0;
+    while (current < 3) {
+        int last_nz = -1;
+        for (int i = 0; i < 4; ++i)
+            if (v[i] != 0) last_nz = i;
+        if (last_nz < 0 || last_nz <= current) break;               /* board.py:100-101 */
+        int j = -1;
+        for (int i = current + 1; i < 4; ++i)
+            if (v[i] != 0) { j = i; break; }                        /* board.py:103 */
+        if (j < 0) break;
+        if (v[current] == 0) {                                      /* board.py:107-110 */
+            v[current] += v[j];
+            v[j] = 0;
+        } else if (v[current] == v[j]) {                            /* board.py:111-116 */
+            v[current] += v[j];
+            score += (uint32_t)v[current];                          /* board.py:114 */
+            v[j] = 0;
+            current += 1;
+        } else if (current + 1 == j) {                              /* board.py:117-119 */
+            current += 1;
+        } else {                                                    /* board.py:120-124 */
+            v[current + 1] = v[j];
+            v[j] = 0;
+            current += 1;
+        }
+    }
+    for (int i = 0; i < 4; ++i) {
+        uint8_t e = 0;
+        while (v[i] > 1) { v[i] >>= 1; ++e; }
+        out[i] = e;
+    }
+    return score;
+}
+
+/* src/board.py:147-183.  up: each column read top->bottom slides toward row 0 (state.T rows);
+ * down: the reversed column; left: each row toward column 0; right: the reversed row. */
+uint32_t o2048_move(const uint8_t in[16], int action, uint8_t out[16]) {
+    uint32_t score = 0;
+    for (int line = 0; line < 4; ++line) {
+        int cells[4];
+        for (int k = 0; k < 4; ++k) {
+            switch (action) {
+                case 0: cells[k] = k * 4 + line; break;        /* up    */
+                case 1: cells[k] = (3 - k) * 4 + line; break;  /* down  */
+                case 2: cells[k] = line * 4 + k; break;        /* left  */
+                default: cells[k] = line * 4 + (3 - k); break; /* right */
+            }
+        }
+        uint8_t vin[4], vout[4];
+        for (int k = 0; k < 4; ++k) vin[k] = in[cells[k]];
+        score += o2048_slide_row(vin, vout);
+        for (int k = 0; k < 4; ++k) out[cells[k]] = vout[k];
+    }
+    return score;
+}
+
+/* src/board.py:128-135: a move is available iff peeking it changes the state. */
+uint8_t o2048_legal_mask(const uint8_t b[16]) {
+    uint8_t mask = 0;
+    for (int a = 0; a < 4; ++a) {
+        uint8_t t[16];
+        o2048_move(b, a, t);
+        if (memcmp(t, b, 16) != 0) mask |= (uint8_t)(1u << a);
+    }
+    return mask;
+}
+
+/* ------------------------------------------------------------------ Philox4x32-10 */
+void o2048_philox(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int round = 0; round < 10; ++round) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+static void draw(uint64_t seed, uint64_t gid, uint32_t domain, uint64_t t, uint32_t out[4]) {
+    uint32_t ctr[4] = {(uint32_t)t, (uint32_t)(t >> 32), (uint32_t)gid,
+                       (uint32_t)(gid >> 32) | (domain << 30)};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    o2048_philox(ctr, key, out);
+}
+
+/* ------------------------------------------------------------------ policy */
+
+/* src/dqn_lib.py:25-29.  compat: Qn = Q - min(Q)*max(Q) - min(Q); argmax(avail * Qn), first
+ * index on ties (torch.argmax).  fixed: argmax of Q over legal moves only, 0 if none. */
+int o2048_greedy_f64(const double q[4], uint8_t legal, int fixed) {
+    int best = 0;
+    if (fixed) {
+        int found = 0;
+        for (int j = 0; j < 4; ++j) {
+            if (!((legal >> j) & 1)) continue;
+            if (!found || q[j] > q[best]) { best = j; found = 1; }
+        }
+        return best;
+    }
+    double mn = q[0], mx = q[0];
+    for (int j = 1; j < 4; ++j) { if (q[j] < mn) mn = q[j]; if (q[j] > mx) mx = q[j]; }
+    double prod = mn * mx;
+    double bestv = 0;
+    for (int j = 0; j < 4; ++j) {
+        double qn = (q[j] - prod) - mn;
+        double v = (double)(float)((legal >> j) & 1) * qn;
+        if (j == 0 || v > bestv) { best = j; bestv = v; }
+    }
+    return best;
+}
+
+int o2048_greedy_f32(const float q[4], uint8_t legal, int fixed) {
+    int best = 0;
+    if (fixed) {
+        int found = 0;
+        for (int j = 0; j < 4; ++j) {
+            if (!((legal >> j) & 1)) continue;
+            if (!found || q[j] > q[best]) { best = j; found = 1; }
+        }
+        return best;
+    }
+    float mn = q[0], mx = q[0];
+    for (int j = 1; j < 4; ++j) { if (q[j] < mn) mn = q[j]; if (q[j] > mx) mx = q[j]; }
+    float prod = mn * mx;
+    float bestv = 0;
+    for (int j = 0; j < 4; ++j) {
+        float qn = (q[j] - prod) - mn;
+        float v = (float)((legal >> j) & 1) * qn;
+        if (j == 0 || v > bestv) { best = j; bestv = v; }
+    }
+    return best;
+}
+
+/* ------------------------------------------------------------------ spawn */
+
+/* src/board.py:41-51 distribution: a uniformly chosen empty cell in row-major order,
+ * value 4 with probability p4 (0.5 in the reference, board.py:12 + np.random.choice).
+ * Our draw: k = floor(u_cell * n / 2^32); the k-th empty cell; 4 iff u_val < p4 * 2^32. */
+static void spawn(uint8_t b[16], uint32_t u_cell, uint32_t u_val, uint32_t flags) {
+    int n = 0;
+    for (int i = 0; i < 16; ++i) n += (b[i] == 0);
+    if (n == 0) return;
+    uint32_t k = (uint32_t)(((uint64_t)u_cell * (uint64_t)n) >> 32);
+    uint64_t thresh = (flags & 1u) ? 429496730ull : 2147483648ull;  /* G2048_P4_10 */
+    uint8_t e = ((uint64_t)u_val < thresh) ? 2 : 1;
+    for (int i = 0; i < 16; ++i) {
+        if (b[i] != 0) continue;
+        if (k == 0) { b[i] = e; return; }
+        --k;
+    }
+}
+
+static void fresh_board(uint8_t b[16], const uint32_t u[4], uint32_t flags) {
+    memset(b, 0, 16);
+    spawn(b, u[0], u[1], flags);   /* board.py:18-20: two spawns on an empty board */
+    spawn(b, u[2], u[3], flags);
+}
+
+void o2048_env_reset(o2048_env* e, const uint8_t* mask, uint32_t epoch) {
+    for (int64_t i = 0; i < e->n; ++i) {
+        if (mask && !mask[i]) continue;
+        uint32_t u[4];
+        draw(e->seed, e->board_offset + (uint64_t)i, 2u, epoch, u);
+        fresh_board(e->board + 16 * i, u, e->flags);
+        uint32_t* m = e->meta + 4 * i;
+        m[0] = 0; m[1] = 0;  /* score, moves; the step counter keeps running */
+    }
+}
+
+/* One transition per board: the contract of include/g2048.h g2048_env_step*. */
+int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const void* q, double eps,
+                       const int8_t* spawn_idx, const uint8_t* spawn_exp,
+                       int32_t* reward, uint8_t* done_out, uint8_t* legal_out,
+                       uint8_t* action_out, o2048_replay* rb) {
+    const int fixed = (e->flags & 2u) != 0;     /* G2048_EGREEDY_FIXED */
+    const int autoreset = (e->flags & 4u) == 0; /* G2048_NO_AUTORESET */
+    int64_t bad = 0;
+    for (int64_t i = 0; i < e->n; ++i) {
+        uint8_t* b = e->board + 16 * i;
+        uint32_t* m = e->meta + 4 * i;
+        const uint64_t gid = e->board_offset + (uint64_t)i;
+        const uint64_t t = (uint64_t)m[2] | ((uint64_t)m[3] << 32);
+        uint32_t u[4];
+        draw(e->seed, gid, 0u, t, u);
+
+        const uint8_t legal = o2048_legal_mask(b);   /* dqn_lib.py:17 */
+        const int done = legal == 0;                 /* dqn_lib.py:18 */
+        int a;
+        if (mode == 0 || mode == 4) {
+            a = actions[i];
+        } else if (mode == 1) {
+            a = (int)(u[0] >> 30);
+        } else {
+            const int explore = (double)u[1] * (1.0 / 4294967296.0) < eps;  /* dqn_lib.py:20 */
+            if (explore) {
+                int nl = 0;
+                for (int j = 0; j < 4; ++j) nl += (legal >> j) & 1;
+                if (fixed && nl > 0) {
+                    uint32_t k = (uint32_t)(((uint64_t)u[0] * (uint64_t)nl) >> 32);
+                    a = 0;
+                    for (int j = 0; j < 4; ++j) {
+                        if (!((legal >> j) & 1)) continue;
+                        if (k == 0) { a = j; break; }
+                        --k;
+                    }
+                } else {
+                    a = (int)(u[0] >> 30);               /* np.random.randint(4) */
+                }
+            } else if (mode == 2) {
+                a = o2048_greedy_f32((const float*)q + 4 * i, legal, fixed);
+            } else {
+                a = o2048_greedy_f64((const double*)q + 4 * i, legal, fixed);
+            }
+        }
+
+        uint8_t s_old[16];
+        memcpy(s_old, b, 16);
+        int32_t r = 0;
+        if (a < 0 || a > 3) {
+            ++bad;                                   /* board.py:192 IndexError -> no-op */
+        } else if (!done) {
+            uint8_t nb[16];
+            uint32_t gain = o2048_move(b, a, nb);
+            if (memcmp(nb, b, 16) != 0) {            /* board.py:151-153 */
+                if (mode == 4) {
+                    int si = spawn_idx[i];
+                    if (si >= 0 && si < 16 && nb[si] == 0) nb[si] = spawn_exp[i];
+                    else ++bad;
+                } else {
+                    spawn(nb, u[2], u[3], e->flags);
+                }
+                memcpy(b, nb, 16);
+                r = (int32_t)gain;                   /* dqn_lib.py:87-88 */
+            }
+        }
+        m[0] += (uint32_t)r;
+        m[1] += 1;
+        if (rb) {
+            const int64_t rows = rb->capacity / e->n;
+            const int64_t slot = (int64_t)(t % (uint64_t)rows) * e->n + i;
+            memcpy(rb->s + 16 * slot, s_old, 16);
+            memcpy(rb->s2 + 16 * slot, b, 16);       /* terminal: (s, a, 0, s, 1) */
+            rb->a[slot] = (uint8_t)a;
+            rb->r[slot] = r;
+            rb->d[slot] = (uint8_t)done;
+            uint64_t c = (t + 1) * (uint64_t)e->n;
+            if (c > (uint64_t)rb->capacity) c = (uint64_t)rb->capacity;
+            if (c > *rb->count) *rb->count = c;
+        }
+        if (reward) reward[i] = r;
+        if (done_out) done_out[i] = (uint8_t)done;
+        if (legal_out) legal_out[i] = legal;
+        if (action_out) action_out[i] = (uint8_t)a;
+        if (done) {
+            uint32_t* ep = e->ep + 4 * i;
+            uint8_t mx = 0;
+            for (int k = 0; k < 16; ++k) if (b[k] > mx) mx = b[k];
+            ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;
+            if (autoreset) {
+                uint32_t ur[4];
+                draw(e->seed, gid, 1u, t, ur);
+                fresh_board(b, ur, e->flags);
+                m[0] = 0; m[1] = 0;
+            }
+        }
+        const uint64_t t1 = t + 1;
+        m[2] = (uint32_t)t1;
+        m[3] = (uint32_t)(t1 >> 32);
+    }
+    return bad;
+}
+
+/* src/dqn_lib.py:67-84 + :33-64: uniform-with-replacement indices, log2 encoding (the stored
+ * exponent itself, board.py:224-231), actions/rewards/dones as tensors. */
+void o2048_replay_sample_f64(const o2048_replay* rb, const int64_t* idx, int64_t B,
+                             uint64_t seed, uint64_t epoch, int64_t* idx_out,
+                             double* s, double* s2, int64_t* a, double* r, double* d) {
+    const uint64_t count = *rb->count;
+    for (int64_t b = 0; b < B; ++b) {
+        int64_t j;
+        if (idx) {
+            j = idx[b];
+        } else {
+            uint32_t u[4];
+            uint32_t ctr[4] = {(uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)epoch,
+                               (uint32_t)(epoch >> 32) | (3u << 30)};
+            uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+            o2048_philox(ctr, key, u);
+            uint64_t x = ((uint64_t)u[1] << 32) | u[0];
+            j = (int64_t)(((unsigned __int128)x * count) >> 64);
+        }
+        if (idx_out) idx_out[b] = j;
+        for (int k = 0; k < 16; ++k) {
+            s[16 * b + k] = (double)rb->s[16 * j + k];
+            s2[16 * b + k] = (double)rb->s2[16 * j + k];
+        }
+        a[b] = rb->a[j];
+        r[b] = (double)rb->r[j];
+        d[b] = (double)rb->d[j];
+    }
+}

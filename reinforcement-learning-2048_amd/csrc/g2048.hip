@@ -1,0 +1,700 @@
+// g2048.hip -- batched 2048 env step / rollout / reset and replay sample-encode kernels for
+// gfx950, plus the extern "C" ABI declared in include/g2048.h.
+//
+// HBM layout (one env = one shard of boards, SoA, 16-byte records so every lane moves whole
+// dwordx4s):
+//   board u8[N][16]   exponents                       (one uint4 per board)
+//   meta  u32[N][4]   {score, moves, steps_lo, steps_hi}
+//   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (touched on done only)
+// Replay ring (capacity C): s u8[C][16], s2 u8[C][16], a u8[C], r i32[C], d u8[C], count u64.
+//
+// One lane owns one board for the whole launch: load board + meta (2 x dwordx4), do the
+// legal-mask / select / slide / spawn / reset arithmetic in VGPRs (g2048_board.hpp), store them
+// back.  Consecutive blocks own consecutive board ranges, so a board's lines stay in the same
+// XCD L2 from one step to the next (blocks are dealt round-robin over the 8 XCDs).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/g2048.h"
+#include "g2048_board.hpp"
+
+using namespace g2048;
+
+namespace {
+
+constexpr int kBlock = 256;
+enum : int { MODE_ACTIONS = 0, MODE_RANDOM = 1, MODE_EG_F32 = 2, MODE_EG_F64 = 3, MODE_INJECT = 4 };
+
+struct ReplayDev {
+    uint4* s;
+    uint4* s2;
+    uint8_t* a;
+    int32_t* r;
+    uint8_t* d;
+    unsigned long long* count;
+    int64_t capacity;
+    int64_t rows;  // capacity / n  (0 = no replay)
+};
+
+struct StepArgs {
+    uint4* board;
+    uint4* meta;
+    uint4* ep;
+    int64_t n;
+    uint64_t board_offset;
+    uint32_t seed_lo, seed_hi;
+    uint32_t p4_thresh;
+    uint32_t flags;
+    const uint8_t* actions;
+    const void* q;
+    const double* eps_dev;
+    double eps;
+    const int8_t* spawn_idx;
+    const uint8_t* spawn_exp;
+    int32_t* reward;
+    uint8_t* done;
+    uint8_t* legal_out;
+    uint8_t* action_out;
+    unsigned long long* err;
+    ReplayDev rb;
+    int k_steps;
+    long long* reward_sum;
+};
+
+__device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v.y, v.z, v.w}; }
+
+// One transition of board i (global id gid).  Mirrors o2048_env_step (oracle/oracle2048.c),
+// which restates src/dqn_lib.py:91-107 + src/board.py.
+template <int MODE>
+__device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, Board& b,
+                                         uint4& m, double eps, int32_t& rew_out,
+                                         uint32_t& done_out, uint32_t& legal_out,
+                                         uint32_t& act_out) {
+    const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
+    const uint4 u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
+    const uint32_t legal = legal_mask(b);
+    const bool done = legal == 0u;
+
+    uint32_t act;
+    if constexpr (MODE == MODE_ACTIONS || MODE == MODE_INJECT) {
+        act = A.actions[i];
+    } else if constexpr (MODE == MODE_RANDOM) {
+        act = u.x >> 30;
+    } else {
+        const bool explore = (double)u.y * (1.0 / 4294967296.0) < eps;
+        const bool fixed = (A.flags & G2048_EGREEDY_FIXED) != 0u;
+        if (explore) {
+            const uint32_t nl = __popc(legal);
+            act = (fixed && nl) ? kth_bit16(legal, __umulhi(u.x, nl)) : (u.x >> 30);
+        } else if constexpr (MODE == MODE_EG_F32) {
+            const float4 q = reinterpret_cast<const float4*>(A.q)[i];
+            act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
+                        : greedy_compat(q.x, q.y, q.z, q.w, legal);
+        } else {
+            const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
+            const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
+            act = fixed ? greedy_fixed(q01.x, q01.y, q23.x, q23.y, legal)
+                        : greedy_compat(q01.x, q01.y, q23.x, q23.y, legal);
+        }
+    }
+
+    const Board s_old = b;
+    uint32_t r = 0;
+    if (act > 3u) {
+        atomicAdd(A.err, 1ull);  // src/board.py:192 IndexError -> counted, no-op here
+    } else if (!done && ((legal >> act) & 1u)) {
+        r = apply_move(b, act);
+        if constexpr (MODE == MODE_INJECT) {
+            const int si = A.spawn_idx[i];
+            const uint32_t Z = empty_mask(b);
+            if (si >= 0 && si < 16 && ((Z >> si) & 1u)) set_cell(b, (uint32_t)si, A.spawn_exp[i]);
+            else atomicAdd(A.err, 1ull);
+        } else {
+            spawn(b, u.z, u.w, A.p4_thresh);
+        }
+    }
+    m.x += r;
+    m.y += 1u;
+
+    if (A.rb.rows) {
+        const uint64_t row = (t >> 32) ? (t % (uint64_t)A.rb.rows)
+                                       : (uint64_t)((uint32_t)t % (uint32_t)A.rb.rows);
+        const int64_t slot = (int64_t)row * A.n + i;
+        A.rb.s[slot] = make_uint4(s_old.r0, s_old.r1, s_old.r2, s_old.r3);
+        A.rb.s2[slot] = make_uint4(b.r0, b.r1, b.r2, b.r3);  // terminal: s' = s (F6)
+        A.rb.a[slot] = (uint8_t)act;
+        A.rb.r[slot] = (int32_t)r;
+        A.rb.d[slot] = (uint8_t)done;
+    }
+
+    if (done) {
+        A.ep[i] = make_uint4(A.ep[i].x + 1u, m.x, m.y, max_exp(b));
+        if (!(A.flags & G2048_NO_AUTORESET)) {
+            b = fresh_board(draw(A.seed_lo, A.seed_hi, gid, DOMAIN_AUTORESET, t), A.p4_thresh);
+            m.x = 0u;
+            m.y = 0u;
+        }
+    }
+    const uint64_t t1 = t + 1u;
+    m.z = (uint32_t)t1;
+    m.w = (uint32_t)(t1 >> 32);
+    rew_out = (int32_t)r;
+    done_out = done;
+    legal_out = legal;
+    act_out = act;
+}
+
+__device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
+    uint64_t c = t_next * (uint64_t)A.n;
+    if (c > (uint64_t)A.rb.capacity) c = (uint64_t)A.rb.capacity;
+    atomicMax(A.rb.count, (unsigned long long)c);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.n) return;
+    Board b = load_board(A.board[i]);
+    uint4 m = A.meta[i];
+    double eps = 0.0;
+    if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) eps = A.eps_dev ? *A.eps_dev : A.eps;
+    int32_t rew;
+    uint32_t done, legal, act;
+    step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, rew, done, legal, act);
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (A.reward) A.reward[i] = rew;
+    if (A.done) A.done[i] = (uint8_t)done;
+    if (A.legal_out) A.legal_out[i] = (uint8_t)legal;
+    if (A.action_out) A.action_out[i] = (uint8_t)act;
+    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+}
+
+// k_steps random-policy steps with the board resident in VGPRs.
+__global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.n) return;
+    Board b = load_board(A.board[i]);
+    uint4 m = A.meta[i];
+    const uint64_t gid = A.board_offset + (uint64_t)i;
+    long long rsum = 0;
+    for (int s = 0; s < A.k_steps; ++s) {
+        int32_t rew;
+        uint32_t done, legal, act;
+        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, rew, done, legal, act);
+        rsum += rew;
+    }
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (A.reward_sum) A.reward_sum[i] += rsum;
+    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint4* meta, int64_t n,
+                                                  uint64_t board_offset, uint32_t seed_lo,
+                                                  uint32_t seed_hi, uint32_t p4_thresh,
+                                                  uint32_t epoch, const uint8_t* mask) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+    const Board b = fresh_board(
+        draw(seed_lo, seed_hi, board_offset + (uint64_t)i, DOMAIN_RESET, epoch), p4_thresh);
+    board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    uint4 m = meta[i];
+    m.x = 0u;
+    m.y = 0u;
+    meta[i] = m;
+}
+
+struct SampleArgs {
+    const uint4* s;
+    const uint4* s2;
+    const uint8_t* a;
+    const int32_t* r;
+    const uint8_t* d;
+    const unsigned long long* count;
+    int64_t capacity;
+    const int64_t* idx;
+    int64_t batch;
+    uint32_t seed_lo, seed_hi;
+    uint64_t epoch;
+    void* s_out;
+    void* s2_out;
+    int64_t* a_out;
+    void* r_out;
+    void* d_out;
+    int64_t* idx_out;
+    unsigned long long* err;
+};
+
+template <typename T>
+__device__ __forceinline__ void store_exps(T* dst, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    if constexpr (sizeof(T) == 4) {
+        float4* o = reinterpret_cast<float4*>(dst);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            o[k] = make_float4((float)(w[k] & 0xFFu), (float)((w[k] >> 8) & 0xFFu),
+                               (float)((w[k] >> 16) & 0xFFu), (float)(w[k] >> 24));
+    } else {
+        double2* o = reinterpret_cast<double2*>(dst);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            o[2 * k] = make_double2((double)(w[k] & 0xFFu), (double)((w[k] >> 8) & 0xFFu));
+            o[2 * k + 1] = make_double2((double)((w[k] >> 16) & 0xFFu), (double)(w[k] >> 24));
+        }
+    }
+}
+
+// sample_experiences + extract_samples_* (src/dqn_lib.py:33-84) for B rows at once.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_sample(SampleArgs S) {
+    const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (b >= S.batch) return;
+    int64_t j;
+    if (S.idx) {
+        j = S.idx[b];
+    } else {
+        const uint4 u = philox10(make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32),
+                                            (uint32_t)S.epoch,
+                                            (uint32_t)(S.epoch >> 32) | (DOMAIN_SAMPLE << 30)),
+                                 S.seed_lo, S.seed_hi);
+        const unsigned long long x = ((unsigned long long)u.y << 32) | u.x;
+        j = (int64_t)__umul64hi(x, *S.count);
+    }
+    if (j < 0 || j >= S.capacity) {  // np.random.randint never leaves range; a bad idx is counted
+        atomicAdd(S.err, 1ull);
+        j = 0;
+    }
+    if (S.idx_out) S.idx_out[b] = j;
+    if (S.s_out) store_exps(reinterpret_cast<T*>(S.s_out) + 16 * b, S.s[j]);
+    if (S.s2_out) store_exps(reinterpret_cast<T*>(S.s2_out) + 16 * b, S.s2[j]);
+    if (S.a_out) S.a_out[b] = S.a[j];
+    if (S.r_out) reinterpret_cast<T*>(S.r_out)[b] = (T)S.r[j];
+    if (S.d_out) reinterpret_cast<T*>(S.d_out)[b] = (T)S.d[j];
+}
+
+// ------------------------------------------------------------------ host side
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define G_HIP(expr)                                                                        \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(G2048_EHIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                         \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) (void)hipSetDevice(dev);
+        else prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+struct g2048_env {
+    int64_t n = 0;
+    uint64_t seed = 0, board_offset = 0;
+    int device = 0;
+    uint32_t flags = 0;
+    uint8_t* board = nullptr;
+    uint32_t* meta = nullptr;
+    uint32_t* ep = nullptr;
+    unsigned long long* err = nullptr;
+    bool owns = false;
+    uint32_t epoch = 0;
+};
+
+struct g2048_replay {
+    int64_t capacity = 0;
+    int device = 0;
+    uint8_t* s = nullptr;
+    uint8_t* s2 = nullptr;
+    uint8_t* a = nullptr;
+    int32_t* r = nullptr;
+    uint8_t* d = nullptr;
+    unsigned long long* count = nullptr;
+    unsigned long long* err = nullptr;
+    bool owns = false;
+};
+
+namespace {
+
+inline uint32_t p4_thresh(uint32_t flags) {
+    return (flags & G2048_P4_10) ? 429496730u : 2147483648u;  // round(p * 2^32)
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
+    DeviceGuard g(e->device);
+    hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), 0, st,
+                       reinterpret_cast<uint4*>(e->board), reinterpret_cast<uint4*>(e->meta), e->n,
+                       e->board_offset, (uint32_t)e->seed, (uint32_t)(e->seed >> 32),
+                       p4_thresh(e->flags), e->epoch, mask);
+    G_HIP(hipGetLastError());
+    e->epoch += 1;
+    return G2048_OK;
+}
+
+int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
+    std::memset(&A, 0, sizeof(A));
+    A.board = reinterpret_cast<uint4*>(e->board);
+    A.meta = reinterpret_cast<uint4*>(e->meta);
+    A.ep = reinterpret_cast<uint4*>(e->ep);
+    A.n = e->n;
+    A.board_offset = e->board_offset;
+    A.seed_lo = (uint32_t)e->seed;
+    A.seed_hi = (uint32_t)(e->seed >> 32);
+    A.p4_thresh = p4_thresh(e->flags);
+    A.flags = e->flags;
+    A.err = e->err;
+    if (rb) {
+        if (rb->device != e->device)
+            return fail(G2048_EINVAL, "replay on device %d, env on device %d", rb->device, e->device);
+        if (rb->capacity < e->n || rb->capacity % e->n != 0)
+            return fail(G2048_EINVAL, "replay capacity %lld must be a positive multiple of n=%lld",
+                        (long long)rb->capacity, (long long)e->n);
+        A.rb.s = reinterpret_cast<uint4*>(rb->s);
+        A.rb.s2 = reinterpret_cast<uint4*>(rb->s2);
+        A.rb.a = rb->a;
+        A.rb.r = rb->r;
+        A.rb.d = rb->d;
+        A.rb.count = rb->count;
+        A.rb.capacity = rb->capacity;
+        A.rb.rows = rb->capacity / e->n;
+    }
+    return G2048_OK;
+}
+
+template <int MODE>
+int launch_step(g2048_env* e, const StepArgs& A, void* stream) {
+    DeviceGuard g(e->device);
+    hipLaunchKernelGGL(k_step<MODE>, dim3(grid_for(e->n)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), A);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ extern "C" ABI
+extern "C" {
+
+const char* g2048_last_error(void) { return g_err.c_str(); }
+int g2048_abi_version(void) { return G2048_ABI_VERSION; }
+
+int g2048_env_wrap(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_offset, int device_id,
+                   uint32_t flags, uint8_t* board, uint32_t* meta, uint32_t* ep, int reset,
+                   void* stream) {
+    if (!out || n <= 0) return fail(G2048_EINVAL, "env_wrap: need out != NULL and n > 0");
+    if (!board || !meta || !ep || !aligned16(board) || !aligned16(meta) || !aligned16(ep))
+        return fail(G2048_EINVAL, "env_wrap: board/meta/ep must be non-NULL and 16-byte aligned");
+    if (flags & ~(uint32_t)(G2048_P4_10 | G2048_EGREEDY_FIXED | G2048_NO_AUTORESET))
+        return fail(G2048_EINVAL, "env_wrap: unknown flags 0x%x", flags);
+    DeviceGuard g(device_id);
+    auto* e = new (std::nothrow) g2048_env;
+    if (!e) return fail(G2048_ENOMEM, "env_wrap: host allocation failed");
+    e->n = n;
+    e->seed = seed;
+    e->board_offset = board_offset;
+    e->device = device_id;
+    e->flags = flags;
+    e->board = board;
+    e->meta = meta;
+    e->ep = ep;
+    hipError_t he = hipMalloc(&e->err, sizeof(unsigned long long));
+    if (he != hipSuccess) {
+        delete e;
+        return fail(G2048_ENOMEM, "env_wrap: hipMalloc(err): %s", hipGetErrorString(he));
+    }
+    he = hipMemsetAsync(e->err, 0, sizeof(unsigned long long), (hipStream_t)stream);
+    if (he != hipSuccess) {
+        g2048_env_destroy(e);
+        return fail(G2048_EHIP, "env_wrap: %s", hipGetErrorString(he));
+    }
+    if (reset) {
+        int rc = launch_reset(e, nullptr, (hipStream_t)stream);
+        if (rc) {
+            g2048_env_destroy(e);
+            return rc;
+        }
+    }
+    *out = e;
+    return G2048_OK;
+}
+
+int g2048_env_create(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_offset,
+                     int device_id, uint32_t flags, void* stream) {
+    if (!out || n <= 0) return fail(G2048_EINVAL, "env_create: need out != NULL and n > 0");
+    DeviceGuard g(device_id);
+    uint8_t* board = nullptr;
+    uint32_t *meta = nullptr, *ep = nullptr;
+    if (hipMalloc(&board, 16 * n) != hipSuccess || hipMalloc(&meta, 16 * n) != hipSuccess ||
+        hipMalloc(&ep, 16 * n) != hipSuccess) {
+        (void)hipFree(board);
+        (void)hipFree(meta);
+        (void)hipFree(ep);
+        return fail(G2048_ENOMEM, "env_create: hipMalloc of %lld boards failed", (long long)n);
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(meta, 0, 16 * n, st) != hipSuccess ||
+        hipMemsetAsync(ep, 0, 16 * n, st) != hipSuccess) {
+        (void)hipFree(board);
+        (void)hipFree(meta);
+        (void)hipFree(ep);
+        return fail(G2048_EHIP, "env_create: hipMemsetAsync failed");
+    }
+    int rc = g2048_env_wrap(out, n, seed, board_offset, device_id, flags, board, meta, ep, 1,
+                            stream);
+    if (rc) {
+        (void)hipFree(board);
+        (void)hipFree(meta);
+        (void)hipFree(ep);
+        return rc;
+    }
+    (*out)->owns = true;
+    return G2048_OK;
+}
+
+void g2048_env_destroy(g2048_env* e) {
+    if (!e) return;
+    DeviceGuard g(e->device);
+    if (e->owns) {
+        (void)hipFree(e->board);
+        (void)hipFree(e->meta);
+        (void)hipFree(e->ep);
+    }
+    (void)hipFree(e->err);
+    delete e;
+}
+
+int g2048_env_views(g2048_env* e, uint8_t** board, uint32_t** meta, uint32_t** ep) {
+    if (!e) return fail(G2048_EINVAL, "env_views: NULL env");
+    if (board) *board = e->board;
+    if (meta) *meta = e->meta;
+    if (ep) *ep = e->ep;
+    return G2048_OK;
+}
+
+int64_t g2048_env_size(const g2048_env* e) { return e ? e->n : 0; }
+
+int g2048_env_reset(g2048_env* e, const uint8_t* mask, void* stream) {
+    if (!e) return fail(G2048_EINVAL, "env_reset: NULL env");
+    return launch_reset(e, mask, (hipStream_t)stream);
+}
+
+int g2048_env_step(g2048_env* e, const uint8_t* actions, int32_t* reward, uint8_t* done,
+                   uint8_t* legal, g2048_replay* rb, void* stream) {
+    if (!e) return fail(G2048_EINVAL, "env_step: NULL env");
+    StepArgs A;
+    int rc = make_args(e, rb, A);
+    if (rc) return rc;
+    A.actions = actions;
+    A.reward = reward;
+    A.done = done;
+    A.legal_out = legal;
+    return actions ? launch_step<MODE_ACTIONS>(e, A, stream) : launch_step<MODE_RANDOM>(e, A, stream);
+}
+
+int g2048_env_step_egreedy(g2048_env* e, const void* q, int q_dtype, const double* eps_dev,
+                           double eps, int32_t* reward, uint8_t* done, uint8_t* action_out,
+                           g2048_replay* rb, void* stream) {
+    if (!e || !q) return fail(G2048_EINVAL, "env_step_egreedy: NULL env or q");
+    if (q_dtype != G2048_F32 && q_dtype != G2048_F64)
+        return fail(G2048_EINVAL, "env_step_egreedy: q_dtype %d", q_dtype);
+    if (!aligned16(q)) return fail(G2048_EINVAL, "env_step_egreedy: q must be 16-byte aligned");
+    StepArgs A;
+    int rc = make_args(e, rb, A);
+    if (rc) return rc;
+    A.q = q;
+    A.eps_dev = eps_dev;
+    A.eps = eps;
+    A.reward = reward;
+    A.done = done;
+    A.action_out = action_out;
+    return q_dtype == G2048_F32 ? launch_step<MODE_EG_F32>(e, A, stream)
+                                : launch_step<MODE_EG_F64>(e, A, stream);
+}
+
+int g2048_env_step_inject(g2048_env* e, const uint8_t* actions, const int8_t* spawn_idx,
+                          const uint8_t* spawn_exp, int32_t* reward, uint8_t* done,
+                          uint8_t* legal, void* stream) {
+    if (!e || !actions || !spawn_idx || !spawn_exp)
+        return fail(G2048_EINVAL, "env_step_inject: NULL argument");
+    StepArgs A;
+    int rc = make_args(e, nullptr, A);
+    if (rc) return rc;
+    A.actions = actions;
+    A.spawn_idx = spawn_idx;
+    A.spawn_exp = spawn_exp;
+    A.reward = reward;
+    A.done = done;
+    A.legal_out = legal;
+    return launch_step<MODE_INJECT>(e, A, stream);
+}
+
+int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* reward_sum,
+                      void* stream) {
+    if (!e || k_steps < 0) return fail(G2048_EINVAL, "env_rollout: NULL env or k_steps < 0");
+    if (k_steps == 0) return G2048_OK;
+    StepArgs A;
+    int rc = make_args(e, rb, A);
+    if (rc) return rc;
+    A.k_steps = k_steps;
+    A.reward_sum = reinterpret_cast<long long*>(reward_sum);
+    DeviceGuard g(e->device);
+    hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), A);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
+}
+
+int g2048_env_error_count(g2048_env* e, int64_t* count, void* stream) {
+    if (!e || !count) return fail(G2048_EINVAL, "env_error_count: NULL argument");
+    DeviceGuard g(e->device);
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long h = 0;
+    G_HIP(hipMemcpyAsync(&h, e->err, sizeof(h), hipMemcpyDeviceToHost, st));
+    G_HIP(hipStreamSynchronize(st));
+    G_HIP(hipMemsetAsync(e->err, 0, sizeof(h), st));
+    *count = (int64_t)h;
+    return G2048_OK;
+}
+
+int g2048_replay_wrap(g2048_replay** out, int64_t capacity, int device_id, uint8_t* s,
+                      uint8_t* s2, uint8_t* a, int32_t* r, uint8_t* d, uint64_t* count) {
+    if (!out || capacity <= 0) return fail(G2048_EINVAL, "replay_wrap: need capacity > 0");
+    if (!s || !s2 || !a || !r || !d || !count || !aligned16(s) || !aligned16(s2))
+        return fail(G2048_EINVAL, "replay_wrap: NULL buffer or s/s2 not 16-byte aligned");
+    DeviceGuard g(device_id);
+    auto* rb = new (std::nothrow) g2048_replay;
+    if (!rb) return fail(G2048_ENOMEM, "replay_wrap: host allocation failed");
+    rb->capacity = capacity;
+    rb->device = device_id;
+    rb->s = s;
+    rb->s2 = s2;
+    rb->a = a;
+    rb->r = r;
+    rb->d = d;
+    rb->count = reinterpret_cast<unsigned long long*>(count);
+    if (hipMalloc(&rb->err, sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(rb->err, 0, sizeof(unsigned long long)) != hipSuccess) {
+        delete rb;
+        return fail(G2048_ENOMEM, "replay_wrap: hipMalloc(err) failed");
+    }
+    *out = rb;
+    return G2048_OK;
+}
+
+int g2048_replay_create(g2048_replay** out, int64_t capacity, int device_id, void* stream) {
+    if (!out || capacity <= 0) return fail(G2048_EINVAL, "replay_create: need capacity > 0");
+    DeviceGuard g(device_id);
+    // one allocation, 256-byte aligned sections: s | s2 | r | a | d | count
+    auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    const int64_t o_s2 = up(16 * capacity), o_r = o_s2 + up(16 * capacity);
+    const int64_t o_a = o_r + up(4 * capacity), o_d = o_a + up(capacity);
+    const int64_t o_c = o_d + up(capacity), total = o_c + 256;
+    uint8_t* base = nullptr;
+    if (hipMalloc(&base, total) != hipSuccess)
+        return fail(G2048_ENOMEM, "replay_create: hipMalloc(%lld) failed", (long long)total);
+    if (hipMemsetAsync(base, 0, total, (hipStream_t)stream) != hipSuccess) {
+        (void)hipFree(base);
+        return fail(G2048_EHIP, "replay_create: hipMemsetAsync failed");
+    }
+    int rc = g2048_replay_wrap(out, capacity, device_id, base, base + o_s2, base + o_a,
+                               reinterpret_cast<int32_t*>(base + o_r), base + o_d,
+                               reinterpret_cast<uint64_t*>(base + o_c));
+    if (rc) {
+        (void)hipFree(base);
+        return rc;
+    }
+    (*out)->owns = true;
+    return G2048_OK;
+}
+
+void g2048_replay_destroy(g2048_replay* rb) {
+    if (!rb) return;
+    DeviceGuard g(rb->device);
+    if (rb->owns) (void)hipFree(rb->s);
+    (void)hipFree(rb->err);
+    delete rb;
+}
+
+int g2048_replay_views(g2048_replay* rb, uint8_t** s, uint8_t** s2, uint8_t** a, int32_t** r,
+                       uint8_t** d, uint64_t** count) {
+    if (!rb) return fail(G2048_EINVAL, "replay_views: NULL replay");
+    if (s) *s = rb->s;
+    if (s2) *s2 = rb->s2;
+    if (a) *a = rb->a;
+    if (r) *r = rb->r;
+    if (d) *d = rb->d;
+    if (count) *count = reinterpret_cast<uint64_t*>(rb->count);
+    return G2048_OK;
+}
+
+int g2048_replay_sample_encode(g2048_replay* rb, const int64_t* idx, int64_t batch, uint64_t seed,
+                               uint64_t epoch, int dtype, void* s_out, void* s2_out,
+                               int64_t* a_out, void* r_out, void* d_out, int64_t* idx_out,
+                               void* stream) {
+    if (!rb || batch <= 0) return fail(G2048_EINVAL, "replay_sample_encode: NULL rb or batch <= 0");
+    if (dtype != G2048_F32 && dtype != G2048_F64)
+        return fail(G2048_EINVAL, "replay_sample_encode: dtype %d", dtype);
+    if ((s_out && !aligned16(s_out)) || (s2_out && !aligned16(s2_out)))
+        return fail(G2048_EINVAL, "replay_sample_encode: s/s2 outputs must be 16-byte aligned");
+    SampleArgs S;
+    std::memset(&S, 0, sizeof(S));
+    S.s = reinterpret_cast<const uint4*>(rb->s);
+    S.s2 = reinterpret_cast<const uint4*>(rb->s2);
+    S.a = rb->a;
+    S.r = rb->r;
+    S.d = rb->d;
+    S.count = rb->count;
+    S.capacity = rb->capacity;
+    S.idx = idx;
+    S.batch = batch;
+    S.seed_lo = (uint32_t)seed;
+    S.seed_hi = (uint32_t)(seed >> 32);
+    S.epoch = epoch;
+    S.s_out = s_out;
+    S.s2_out = s2_out;
+    S.a_out = a_out;
+    S.r_out = r_out;
+    S.d_out = d_out;
+    S.idx_out = idx_out;
+    S.err = rb->err;
+    DeviceGuard g(rb->device);
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == G2048_F32)
+        hipLaunchKernelGGL(k_sample<float>, dim3(grid_for(batch)), dim3(kBlock), 0, st, S);
+    else
+        hipLaunchKernelGGL(k_sample<double>, dim3(grid_for(batch)), dim3(kBlock), 0, st, S);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,258 @@
+"""VecEnv2048 / ReplayBuffer: batched, HBM-resident replacements for Board2048 and the replay deque.
+
+Reference objects replaced (ribal-aladeeb/reinforcement-learning-2048):
+  Board2048                     src/board.py:8-237   -> one row of VecEnv2048 (N boards at once)
+  deque((s, a, r, s', done))    src/dqn_lib.py:172   -> ReplayBuffer (SoA ring in HBM)
+All state lives in torch-allocated device tensors that the C ABI wraps by pointer
+(g2048_env_wrap / g2048_replay_wrap), so the boards can be fed straight into the Q-network.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _native as N
+
+ACTIONS = ("up", "down", "left", "right")  # src/board.py:129, action ints at :191
+
+
+class VecEnv2048:
+    """N independent 2048 boards on one GPU, stepped by the HIP kernels in csrc/g2048.hip.
+
+    board  uint8 [N, 16]  log2 exponents (== Board2048.log_scale().state, src/board.py:224-231)
+    meta   int32 [N, 4]   {score (= merge_score()), moves (= len(_action_history)), steps_lo, hi}
+    ep     int32 [N, 4]   {episodes finished, last score, last moves, last max exponent}
+    """
+
+    def __init__(self, n_boards: int, seed: int = 0x2048, device="cuda", board_offset: int = 0,
+                 p4: float = 0.5, egreedy: str = "compat", autoreset: bool = True,
+                 reset: bool = True):
+        if p4 not in (0.5, 0.1):
+            raise ValueError("p4 must be 0.5 (reference, src/board.py:12) or 0.1")
+        if egreedy not in ("compat", "fixed"):
+            raise ValueError("egreedy must be 'compat' (src/dqn_lib.py:25-29) or 'fixed'")
+        self.device = N.require_gpu(device)
+        self.n = int(n_boards)
+        self.seed = int(seed)
+        self.board_offset = int(board_offset)
+        self.flags = ((N.P4_10 if p4 == 0.1 else 0) | (N.EGREEDY_FIXED if egreedy == "fixed" else 0)
+                      | (0 if autoreset else N.NO_AUTORESET))
+        lib = N.load()
+        kw = dict(device=self.device)
+        self.board = torch.zeros((self.n, 16), dtype=torch.uint8, **kw)
+        self.meta = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
+        self.ep = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
+        self._h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            N.check(lib.g2048_env_wrap(C.byref(self._h), self.n, self.seed, self.board_offset,
+                                       self.device.index, self.flags, N.ptr(self.board),
+                                       N.ptr(self.meta), N.ptr(self.ep), int(reset),
+                                       N.stream_of(self.device)), "g2048_env_wrap")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            N.load().g2048_env_destroy(h)
+            self._h = None
+
+    def __len__(self):
+        return self.n
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _stream(self):
+        return N.stream_of(self.device)
+
+    # ------------------------------------------------------------------ stepping
+    def reset(self, mask: torch.Tensor | None = None) -> None:
+        """Re-deal boards (2 spawns each, src/board.py:18-20) where mask != 0 (all if None)."""
+        if mask is not None:
+            mask = self._u8(mask, "mask")
+        N.check(N.load().g2048_env_reset(self._h, N.ptr(mask), self._stream()), "g2048_env_reset")
+
+    def step(self, actions: torch.Tensor | None = None, replay: "ReplayBuffer | None" = None,
+             reward=None, done=None, legal=None):
+        """One move on every board (peek_action + reward + done, src/board.py:185-202,
+        src/dqn_lib.py:87-88,17-18).  actions None = uniform random (np.random.randint(4)).
+        Returns (reward int32 [N], done uint8 [N], legal uint8 [N]) for the boards BEFORE the move."""
+        if actions is not None:
+            actions = self._u8(actions, "actions")
+        reward = self._out(reward, torch.int32)
+        done = self._out(done, torch.uint8)
+        legal = self._out(legal, torch.uint8)
+        N.check(N.load().g2048_env_step(self._h, N.ptr(actions), N.ptr(reward), N.ptr(done),
+                                        N.ptr(legal), replay.handle if replay else None,
+                                        self._stream()), "g2048_env_step")
+        return reward, done, legal
+
+    def step_egreedy(self, q: torch.Tensor, epsilon, replay: "ReplayBuffer | None" = None,
+                     reward=None, done=None, action=None):
+        """Fused epsilon_greedy_policy + peek_action + replay append (src/dqn_lib.py:16-30,91-107).
+        q: Q-values [N, 4] (float32 or float64) of the current boards; epsilon: float or a
+        float64 device scalar tensor (graph-safe).  Returns (action, reward, done)."""
+        if q.shape != (self.n, 4) or q.device != self.device or not q.is_contiguous():
+            raise ValueError(f"q must be a contiguous [{self.n}, 4] tensor on {self.device}")
+        if q.dtype not in (torch.float32, torch.float64):
+            raise TypeError("q must be float32 or float64")
+        dt = N.F32 if q.dtype == torch.float32 else N.F64
+        if isinstance(epsilon, torch.Tensor):
+            if epsilon.dtype != torch.float64 or epsilon.device != self.device or epsilon.numel() != 1:
+                raise ValueError("epsilon tensor must be one float64 on the env device")
+            eps_ptr, eps_val = N.ptr(epsilon), 0.0
+        else:
+            eps_ptr, eps_val = None, float(epsilon)
+        reward = self._out(reward, torch.int32)
+        done = self._out(done, torch.uint8)
+        action = self._out(action, torch.uint8)
+        N.check(N.load().g2048_env_step_egreedy(self._h, N.ptr(q), dt, eps_ptr, eps_val,
+                                                N.ptr(reward), N.ptr(done), N.ptr(action),
+                                                replay.handle if replay else None,
+                                                self._stream()), "g2048_env_step_egreedy")
+        return action, reward, done
+
+    def step_inject(self, actions, spawn_idx, spawn_exp):
+        """Test entry: the given actions with the given spawn cells (-1 = none) / exponents."""
+        actions = self._u8(actions, "actions")
+        spawn_idx = self._typed(spawn_idx, torch.int8, "spawn_idx")
+        spawn_exp = self._u8(spawn_exp, "spawn_exp")
+        reward, done, legal = (self._out(None, torch.int32), self._out(None, torch.uint8),
+                               self._out(None, torch.uint8))
+        N.check(N.load().g2048_env_step_inject(self._h, N.ptr(actions), N.ptr(spawn_idx),
+                                               N.ptr(spawn_exp), N.ptr(reward), N.ptr(done),
+                                               N.ptr(legal), self._stream()),
+                "g2048_env_step_inject")
+        return reward, done, legal
+
+    def rollout(self, k_steps: int, replay: "ReplayBuffer | None" = None,
+                reward_sum: torch.Tensor | None = None):
+        """k_steps random-policy steps in ONE launch (boards stay in registers)."""
+        if reward_sum is not None:
+            reward_sum = self._typed(reward_sum, torch.int64, "reward_sum")
+        N.check(N.load().g2048_env_rollout(self._h, int(k_steps), replay.handle if replay else None,
+                                           N.ptr(reward_sum), self._stream()), "g2048_env_rollout")
+        return reward_sum
+
+    def error_count(self) -> int:
+        c = C.c_int64()
+        N.check(N.load().g2048_env_error_count(self._h, C.byref(c), self._stream()),
+                "g2048_env_error_count")
+        return int(c.value)
+
+    def check_errors(self) -> None:
+        """Raise like the reference does (IndexError for an action outside 0..3, src/board.py:192)."""
+        n = self.error_count()
+        if n:
+            raise IndexError(f"{n} invalid action(s) / injected spawn(s) since the last check")
+
+    # ------------------------------------------------------------------ views
+    @property
+    def score(self):          # Board2048.merge_score(), src/board.py:207
+        return self.meta[:, 0]
+
+    @property
+    def moves(self):          # len(Board2048._action_history)
+        return self.meta[:, 1]
+
+    @property
+    def steps(self):
+        return (self.meta[:, 2].to(torch.int64) & 0xFFFFFFFF) | (self.meta[:, 3].to(torch.int64) << 32)
+
+    def max_tile(self):
+        return torch.where(self.board.amax(1) > 0, 1 << self.board.amax(1).to(torch.int64), 0)
+
+    def encode(self, dtype=torch.float32, conv: bool = True):
+        """board_as_4d_tensor / board_as_flattened_tensor (src/dqn_lib.py:8-13) for all boards."""
+        x = self.board.to(dtype)
+        return x.view(self.n, 1, 4, 4) if conv else x
+
+    # ------------------------------------------------------------------ helpers
+    def _typed(self, t, dtype, name):
+        t = torch.as_tensor(t, device=self.device)
+        if t.dtype != dtype:
+            t = t.to(dtype)
+        if t.numel() != self.n:
+            raise ValueError(f"{name} must have {self.n} elements")
+        return t.contiguous()
+
+    def _u8(self, t, name):
+        return self._typed(t, torch.uint8, name)
+
+    def _out(self, t, dtype):
+        if t is None:
+            return torch.empty(self.n, dtype=dtype, device=self.device)
+        if t.dtype != dtype or t.numel() != self.n or not t.is_contiguous() or t.device != self.device:
+            raise ValueError(f"output must be a contiguous {dtype} [{self.n}] tensor on {self.device}")
+        return t
+
+
+class ReplayBuffer:
+    """HBM ring of transitions (s u8[16], a u8, r i32, s' u8[16], done u8): the reference's
+    deque(maxlen=replay_buffer_length) of (Board2048, action, reward, Board2048, done) tuples
+    (src/dqn_lib.py:106,172), 38 bytes per transition instead of two Python objects."""
+
+    def __init__(self, capacity: int, device="cuda"):
+        self.device = N.require_gpu(device)
+        self.capacity = int(capacity)
+        kw = dict(device=self.device)
+        self.s = torch.zeros((self.capacity, 16), dtype=torch.uint8, **kw)
+        self.s2 = torch.zeros((self.capacity, 16), dtype=torch.uint8, **kw)
+        self.a = torch.zeros(self.capacity, dtype=torch.uint8, **kw)
+        self.r = torch.zeros(self.capacity, dtype=torch.int32, **kw)
+        self.d = torch.zeros(self.capacity, dtype=torch.uint8, **kw)
+        self.count = torch.zeros(1, dtype=torch.int64, **kw)
+        self._h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            N.check(N.load().g2048_replay_wrap(C.byref(self._h), self.capacity, self.device.index,
+                                               N.ptr(self.s), N.ptr(self.s2), N.ptr(self.a),
+                                               N.ptr(self.r), N.ptr(self.d), N.ptr(self.count)),
+                    "g2048_replay_wrap")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            N.load().g2048_replay_destroy(h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __len__(self):  # host sync
+        return int(self.count.item())
+
+    def load(self, s, a, r, s2, d) -> None:
+        """Fill the first rows from host/device arrays (tests, warm starts)."""
+        n = len(a)
+        self.s[:n].copy_(torch.as_tensor(s, dtype=torch.uint8).reshape(n, 16))
+        self.s2[:n].copy_(torch.as_tensor(s2, dtype=torch.uint8).reshape(n, 16))
+        self.a[:n].copy_(torch.as_tensor(a).to(torch.uint8))
+        self.r[:n].copy_(torch.as_tensor(r).to(torch.int32))
+        self.d[:n].copy_(torch.as_tensor(d).to(torch.uint8))
+        self.count.fill_(n)
+
+    def sample_encode(self, batch_size: int, dtype=torch.float32, idx: torch.Tensor | None = None,
+                      seed: int = 0, epoch: int = 0, out=None):
+        """sample_experiences (src/dqn_lib.py:67-84) with the encode of extract_samples_*
+        (:33-64) fused: returns (states [B,16], actions i64 [B], rewards [B], next_states [B,16],
+        dones [B], idx i64 [B]).  idx None = uniform with replacement over the filled rows."""
+        if dtype not in (torch.float32, torch.float64):
+            raise TypeError("dtype must be float32 or float64")
+        B = int(batch_size)
+        if idx is not None:
+            idx = torch.as_tensor(idx, device=self.device).to(torch.int64).contiguous()
+            if idx.numel() != B:
+                raise ValueError("idx must have batch_size elements")
+        kw = dict(device=self.device)
+        if out is None:
+            out = (torch.empty((B, 16), dtype=dtype, **kw), torch.empty(B, dtype=torch.int64, **kw),
+                   torch.empty(B, dtype=dtype, **kw), torch.empty((B, 16), dtype=dtype, **kw),
+                   torch.empty(B, dtype=dtype, **kw), torch.empty(B, dtype=torch.int64, **kw))
+        s, a, r, s2, d, io = out
+        N.check(N.load().g2048_replay_sample_encode(
+            self._h, N.ptr(idx), B, int(seed), int(epoch), N.F32 if dtype == torch.float32 else N.F64,
+            N.ptr(s), N.ptr(s2), N.ptr(a), N.ptr(r), N.ptr(d), N.ptr(io),
+            N.stream_of(self.device)), "g2048_replay_sample_encode")
+        return s, a, r, s2, d, io

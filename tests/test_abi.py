@@ -1,0 +1,54 @@
+"""CPU-side checks of the drop-in boundary: libg2048.so loads and exports every symbol that
+include/g2048.h declares (no compute calls -- there is no GPU here)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "g2048.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"G2048_API\s+[\w\s\*]+?\b(g2048_\w+)\s*\(", src)))
+
+
+def test_header_declares_abi():
+    names = _declared()
+    assert "g2048_env_step" in names and "g2048_replay_sample_encode" in names
+    assert len(names) == 18
+
+
+def test_library_exports_every_declared_symbol():
+    import g2048._native as N
+
+    lib = N.load()
+    for name in _declared():
+        assert hasattr(lib, name), name
+    assert set(_declared()) == set(N.SIGNATURES)
+    assert lib.g2048_abi_version() == 1
+    out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = sorted(set(re.findall(r" T (g2048_\w+)", out)))
+    assert exported == _declared()
+
+
+def test_no_cpu_fallback():
+    """The product path fails loudly without a GPU instead of falling back."""
+    import torch
+
+    import g2048
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    with pytest.raises(g2048.NativeError):
+        g2048.VecEnv2048(16, device="cuda:0")
+    with pytest.raises(g2048.NativeError):
+        g2048.VecEnv2048(16, device="cpu")
+
+
+def test_header_compiles_as_c():
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", HEADER],
+                   check=True)
