@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark of the 2048 hot path on MI355X (contract: see DESIGN.md "Measurement").
+
+Default workload = BASELINE.json configs[1]: 65 536 vectorised boards per GPU, env step only
+(uniform random actions drawn in-kernel from Philox), one g2048_env_step launch per step,
+replayed from hipGraphs of `--graph-steps` steps.  value = env steps/s over all ranks.
+Extra fields report the K-steps-per-launch rollout kernel and (with --train) DQN updates/s.
+
+Multi-GPU: one process per GPU (torchrun), boards sharded by board_offset = rank * N, no
+collective on the env path (weak scaling); timing = max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "reinforcement-learning-2048_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "2048 env steps/sec + DQN updates/sec at 64k parallel boards, 1→8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# algorithmic bytes per env step of k_step (random mode, reward + done + legal outputs):
+# board 16 R + 16 W, meta 16 R + 16 W, reward 4 W, done 1 W, legal 1 W
+STEP_BYTES = 70
+# rollout kernel with replay append, per step: transition s 16 + s' 16 + a 1 + r 4 + d 1
+ROLLOUT_BYTES = 38
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--boards", type=int, default=65536)
+    p.add_argument("--graph-steps", type=int, default=100)
+    p.add_argument("--seed", type=int, default=0x2048)
+    p.add_argument("--rollout-k", type=int, default=64, help="steps per rollout launch (0 = skip)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, torch.device("cuda", local if world > 1 else 0)
+
+
+def barrier(world, dev):
+    if world > 1:
+        dist.barrier(device_ids=[dev.index])
+
+
+def max_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int, dev) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def capture(fn, n_steps: int):
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()  # one eager call on the side stream before capture
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        for _ in range(n_steps):
+            fn()
+    return g
+
+
+def bench_env(args, world, rank, dev):
+    import g2048
+
+    n = args.boards
+    env = g2048.VecEnv2048(n, seed=args.seed, device=dev, board_offset=rank * n)
+    reward = torch.empty(n, dtype=torch.int32, device=dev)
+    done = torch.empty(n, dtype=torch.uint8, device=dev)
+    legal = torch.empty(n, dtype=torch.uint8, device=dev)
+
+    def one_step():
+        env.step(None, reward=reward, done=done, legal=legal)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    G = max(1, min(args.graph_steps, args.steps))
+    graphs = [(capture(one_step, G), args.steps // G)]
+    if args.steps % G:
+        graphs.append((capture(one_step, args.steps % G), 1))
+    for g, _ in graphs:  # warm the graphs
+        g.replay()
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for g, reps in graphs:
+        for _ in range(reps):
+            g.replay()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world, dev)
+    wall = time.perf_counter() - t0
+    ev_s = e0.elapsed_time(e1) / 1e3
+    wall_max = max_over_ranks(wall, world, dev)
+
+    # single-launch kernel duration (events bracketing one eager launch, median of 200)
+    durs = []
+    for _ in range(200):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        one_step()
+        b.record(stream)
+        b.synchronize()
+        durs.append(a.elapsed_time(b) / 1e3)
+    durs.sort()
+    single = durs[len(durs) // 2]
+    env.check_errors()
+    return dict(wall=wall_max, ev_s=ev_s, single_launch_s=single, n=n, G=G)
+
+
+def bench_rollout(args, world, rank, dev):
+    """K random steps per launch with fused replay append (replay pre-fill path)."""
+    import g2048
+
+    n, k = args.boards, args.rollout_k
+    env = g2048.VecEnv2048(n, seed=args.seed + 1, device=dev, board_offset=rank * n)
+    rb = g2048.ReplayBuffer(n * k, device=dev)
+    env.rollout(k, replay=rb)
+    torch.cuda.synchronize()
+    reps = 20
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        env.rollout(k, replay=rb)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    s = e0.elapsed_time(e1) / 1e3 / reps
+    return dict(launch_s=s, steps_per_s=n * k / s, bytes_per_launch=n * k * ROLLOUT_BYTES)
+
+
+def cpu_baseline(args):
+    """The oracle (plain-C restatement of src/board.py + dqn_lib.play_one_step) on ONE host core,
+    bounded sample: 4096 boards stepped with random actions for ~args.cpu_seconds."""
+    from oracle import oracle as O
+
+    O.build()
+    n = 4096
+    env = O.OracleEnv(n, seed=args.seed)
+    env.step(O.MODE_RANDOM)
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < args.cpu_seconds:
+        env.step(O.MODE_RANDOM)
+        steps += n
+    dt = time.perf_counter() - t0
+    return dict(value=steps / dt, unit="env steps/s", cores=1, kind="port",
+                sample=f"oracle/oracle2048.c random-policy steps, {n} boards x {steps // n} steps "
+                       f"({dt:.1f} s, 1 thread)")
+
+
+def main():
+    args = parse()
+    world, rank, dev = setup_dist(args)
+    torch.cuda.set_device(dev)
+    r = bench_env(args, world, rank, dev)
+    total_steps = sum_over_ranks(r["n"] * args.steps, world, dev)
+    value = total_steps / r["wall"]
+    per_step_s = r["ev_s"] / args.steps
+    achieved = STEP_BYTES * r["n"] / per_step_s / 1e9
+    ro = bench_rollout(args, world, rank, dev) if args.rollout_k > 0 else None
+    if ro:
+        ro_total = sum_over_ranks(ro["steps_per_s"], world, dev)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": r["wall"] / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (fresh boards from Philox spawns, uniform random actions)",
+            "config": {"workload": "BASELINE configs[1]: 64k vectorised boards, env-step-only "
+                                   "(no learner), random policy",
+                       "boards_per_gpu": r["n"], "global_boards": r["n"] * world,
+                       "parallelism": f"dp{world} (boards sharded, no collective)",
+                       "launch": f"1 g2048_env_step per step, hipGraph of {r['G']} steps"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_step<MODE_RANDOM>",
+                         "bytes_per_launch": STEP_BYTES * r["n"],
+                         "launch_us_graph": per_step_s * 1e6,
+                         "launch_us_single_eager": r["single_launch_s"] * 1e6},
+            "cpu_baseline": cpu,
+        }
+        if ro:
+            line["rollout"] = {"kernel": "k_rollout (K steps/launch, replay append)",
+                               "k": args.rollout_k, "env_steps_per_s": ro_total,
+                               "launch_ms": ro["launch_s"] * 1e3,
+                               "replay_write_GBs": ro["bytes_per_launch"] / ro["launch_s"] / 1e9}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -84,7 +84,7 @@ class VecEnv2048:
         done = self._out(done, torch.uint8)
         legal = self._out(legal, torch.uint8)
         N.check(N.load().g2048_env_step(self._h, N.ptr(actions), N.ptr(reward), N.ptr(done),
-                                        N.ptr(legal), replay.handle if replay else None,
+                                        N.ptr(legal), replay.handle if replay is not None else None,
                                         self._stream()), "g2048_env_step")
         return reward, done, legal
 
@@ -109,7 +109,7 @@ class VecEnv2048:
         action = self._out(action, torch.uint8)
         N.check(N.load().g2048_env_step_egreedy(self._h, N.ptr(q), dt, eps_ptr, eps_val,
                                                 N.ptr(reward), N.ptr(done), N.ptr(action),
-                                                replay.handle if replay else None,
+                                                replay.handle if replay is not None else None,
                                                 self._stream()), "g2048_env_step_egreedy")
         return action, reward, done
 
@@ -131,7 +131,7 @@ class VecEnv2048:
         """k_steps random-policy steps in ONE launch (boards stay in registers)."""
         if reward_sum is not None:
             reward_sum = self._typed(reward_sum, torch.int64, "reward_sum")
-        N.check(N.load().g2048_env_rollout(self._h, int(k_steps), replay.handle if replay else None,
+        N.check(N.load().g2048_env_rollout(self._h, int(k_steps), replay.handle if replay is not None else None,
                                            N.ptr(reward_sum), self._stream()), "g2048_env_rollout")
         return reward_sum
 

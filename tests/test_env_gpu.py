@@ -48,6 +48,21 @@ def _random_boards(n, seed):
     return b
 
 
+def _mask_boards():
+    """Boards realising all 16 legal masks: a terminal board with 1-2 holes / equal pairs, plus
+    one empty edge row/column for the four single-direction masks."""
+    T = np.array([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 1], np.uint8)
+    out = []
+    for i in range(16):
+        b = T.copy(); b[i] = 0; out.append(b)
+        for j in range(16):
+            b2 = b.copy(); b2[j] = 0; out.append(b2)
+            b3 = T.copy(); b3[j] = T[i]; out.append(b3)
+    for cells in ([0, 1, 2, 3], [12, 13, 14, 15], [0, 4, 8, 12], [3, 7, 11, 15]):
+        b = T.copy(); b[cells] = 0; out.append(b)
+    return out
+
+
 # ------------------------------------------------------------------ slide / score / legal
 @pytest.mark.parametrize("action", [0, 1, 2, 3])
 def test_row_lut_all_directions(g2048, golden_dir, action):
@@ -192,9 +207,8 @@ def test_egreedy_golden_rows(g2048, golden_dir):
     g = np.load(os.path.join(golden_dir, "egreedy.npz"))
     # one board per legal mask value (found by search), reused for every row with that mask
     by_mask = {}
-    for b in _random_boards(50000, 11):
-        m = O.legal_mask(b)
-        by_mask.setdefault(m, b)
+    for b in _mask_boards():
+        by_mask.setdefault(O.legal_mask(b), b)
     assert len(by_mask) == 16
     boards = np.stack([by_mask[int(m)] for m in g["mask"]])
     for dt, field in [(np.float64, "action"), (np.float32, "action_f32")]:

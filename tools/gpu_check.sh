@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, bench, rocprofv3 kernel trace (run via gpurun).
+mkdir -p gpurun_out
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+tail -3 gpurun_out/gpu_tests.log
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" || exit 1
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 1000 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { tail -20 gpurun_out/prof.log; exit 1; }
+find gpurun_out/prof -name "*stats*"
