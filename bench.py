@@ -43,6 +43,11 @@ def parse():
     p.add_argument("--graph-steps", type=int, default=100)
     p.add_argument("--seed", type=int, default=0x2048)
     p.add_argument("--rollout-k", type=int, default=64, help="steps per rollout launch (0 = skip)")
+    p.add_argument("--train", default="dense64,conv",
+                   help="learner workloads to time (comma list of dense64,conv,dense; '' = none)")
+    p.add_argument("--train-updates", type=int, default=200)
+    p.add_argument("--batch", type=int, default=8192)
+    p.add_argument("--replay", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -167,6 +172,57 @@ def bench_rollout(args, world, rank, dev):
     return dict(launch_s=s, steps_per_s=n * k / s, bytes_per_launch=n * k * ROLLOUT_BYTES)
 
 
+def bench_train(args, world, rank, dev, net):
+    """BASELINE configs[2]/[3] (configs[4] at --gpus 8): N boards + Double-DQN, replay 1M,
+    B=8192, fp32, graph-captured update with RCCL gradient all-reduce when world > 1.
+    Times (a) learner updates alone and (b) the full loop iteration = Q forward of all boards +
+    fused epsilon-greedy step/append + 1 update."""
+    import g2048
+    from g2048.learner import DQNLearner, Trainer, flops_per_update
+
+    n = args.boards
+    C = max(args.replay // n, 1) * n
+    env = g2048.VecEnv2048(n, seed=args.seed + 7, device=dev, board_offset=rank * n)
+    rb = g2048.ReplayBuffer(C, device=dev)
+    L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=args.batch, target_sync_every=100)
+    T = Trainer(env, rb, L, updates_per_step=1, min_fill=0)
+    T.prefill(C // n)  # replay pre-filled by random-policy rollout steps (one launch)
+    for _ in range(5):
+        T.step()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    K = args.train_updates
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(K):
+        L.update()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world, dev)
+    upd_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
+    upd_ev = e0.elapsed_time(e1) / 1e3
+    K2 = max(K // 2, 1)
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(K2):
+        T.step()
+    torch.cuda.synchronize()
+    barrier(world, dev)
+    loop_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
+    loss = float(L.last_loss)
+    env.check_errors()
+    fl = flops_per_update(net, args.batch)
+    return {"updates_per_s": K / upd_wall, "update_ms": upd_ev / K * 1e3,
+            "learner_tflops": fl / (upd_ev / K) / 1e12,
+            "loop_iter_ms": loop_wall / K2 * 1e3,
+            "loop_env_steps_per_s": sum_over_ranks(n * K2 / loop_wall, world, dev),
+            "loop_updates_per_s": K2 / loop_wall,
+            "batch": args.batch, "replay": C, "dtype": "fp32", "loss": loss,
+            "params": L.n_params}
+
+
 def cpu_baseline(args):
     """The oracle (plain-C restatement of src/board.py + dqn_lib.play_one_step) on ONE host core,
     bounded sample: 4096 boards stepped with random actions for ~args.cpu_seconds."""
@@ -198,6 +254,9 @@ def main():
     ro = bench_rollout(args, world, rank, dev) if args.rollout_k > 0 else None
     if ro:
         ro_total = sum_over_ranks(ro["steps_per_s"], world, dev)
+    train = {}
+    for net in [x for x in args.train.split(",") if x]:
+        train[net] = bench_train(args, world, rank, dev, net)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
@@ -233,6 +292,8 @@ def main():
                                "k": args.rollout_k, "env_steps_per_s": ro_total,
                                "launch_ms": ro["launch_s"] * 1e3,
                                "replay_write_GBs": ro["bytes_per_launch"] / ro["launch_s"] / 1e9}
+        if train:
+            line["learner"] = train
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,178 @@
+"""Batched mirror of the reference's src/dqn_lib.py over VecEnv2048 / ReplayBuffer.
+
+Same names, same argument meaning, same numerics (see the parity notes per function); the unit
+of work is N boards / B transitions per call instead of one Board2048.  The injected callables
+(board_to_tensor_function, extract_samples_function, reward_function) remain the plug points.
+
+Reference findings honoured here: F1 the reference's train_step calls
+zero_grad() between backward() and step(), so Adam never moves the weights -- reproduced with
+reference_compat=True, the default is the intended zero_grad -> backward -> step; F5 the
+epsilon-greedy normalisation bug (fused in the env kernel, "compat" flavour); F6 terminal
+self-transitions (s, a, 0, s, 1); F7 float64 learner (dtype follows the model); F10 the target
+network is evaluated without autograd.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+from .env import ReplayBuffer, VecEnv2048
+
+
+# ------------------------------------------------------------------ encoders (src/dqn_lib.py:8-13)
+def board_as_4d_tensor(env: VecEnv2048, device=None, dtype=torch.float64) -> torch.Tensor:
+    """log_scale().state_as_4d_tensor() for every board: [N, 1, 4, 4] exponents."""
+    return env.encode(dtype, conv=True)
+
+
+def board_as_flattened_tensor(env: VecEnv2048, device=None, dtype=torch.float64) -> torch.Tensor:
+    """log_scale().flattened_state_as_tensor() for every board: [N, 16] exponents."""
+    return env.encode(dtype, conv=False)
+
+
+def reward_func_merge_score(board=None, next_board=None, action=None, done=None):
+    """src/dqn_lib.py:87-88: next.merge_score() - board.merge_score().  The env kernel computes
+    exactly this gain in-register; passing this function selects the fused path."""
+    raise RuntimeError("reward_func_merge_score is computed inside the env step kernel")
+
+
+# ------------------------------------------------------------------ acting (src/dqn_lib.py:16-30, 91-107)
+def _model_dtype(model: torch.nn.Module) -> torch.dtype:
+    return next(model.parameters()).dtype
+
+
+@torch.no_grad()
+def q_values(env: VecEnv2048, model: torch.nn.Module, board_to_tensor_function: Callable) -> torch.Tensor:
+    dtype = _model_dtype(model)
+    return model(board_to_tensor_function(env, env.device, dtype)).reshape(env.n, 4).contiguous()
+
+
+def epsilon_greedy_policy(env: VecEnv2048, epsilon, model: torch.nn.Module, device=None,
+                          board_to_tensor_function: Callable = board_as_4d_tensor,
+                          replay_buffer: ReplayBuffer | None = None):
+    """src/dqn_lib.py:16-30 for every board, fused with the move it selects (the action is
+    applied in the same kernel, so this also advances the env like play_one_step).
+    Returns (actions uint8 [N], done uint8 [N], max_q [N])."""
+    q = q_values(env, model, board_to_tensor_function)
+    action, reward, done = env.step_egreedy(q, epsilon, replay=replay_buffer)
+    return action, done, q.amax(1)
+
+
+def play_one_step(env: VecEnv2048, epsilon, model: torch.nn.Module, replay_buffer: ReplayBuffer,
+                  device=None, reward_function: Callable = reward_func_merge_score,
+                  board_to_tensor_function: Callable = board_as_4d_tensor):
+    """src/dqn_lib.py:91-107 for N boards in one kernel: epsilon-greedy select (compat formula,
+    F5), move + spawn, merge-score reward, done flag, replay append.  Terminal boards record
+    (s, a, 0, s, 1) and are re-dealt.  With epsilon >= 1 no Q-values are needed and `model`
+    may be None (the random branch returns before the forward, :20-21).
+    Returns (env, actions, rewards, dones, max_q_values)."""
+    if reward_function is not reward_func_merge_score:
+        raise NotImplementedError("only the reference reward (merge-score gain) is fused in the "
+                                  "env kernel; compute custom rewards from the replay rows")
+    if model is None or (not isinstance(epsilon, torch.Tensor) and float(epsilon) >= 1.0):
+        q = torch.zeros((env.n, 4), dtype=torch.float32, device=env.device)
+    else:
+        q = q_values(env, model, board_to_tensor_function)
+    action, reward, done = env.step_egreedy(q, epsilon, replay=replay_buffer)
+    return env, action, reward, done, q.amax(1)
+
+
+# ------------------------------------------------------------------ sampling (src/dqn_lib.py:33-84)
+def extract_samples_conv(states: torch.Tensor) -> torch.Tensor:
+    """Layout of extract_samples_conv (:33-46): [B, 1, 4, 4] (the gather + encode ran in-kernel)."""
+    return states.view(states.shape[0], 1, 4, 4)
+
+
+def extract_samples_dense(states: torch.Tensor) -> torch.Tensor:
+    """Layout of extract_samples_dense (:49-64): [B, 16]."""
+    return states.view(states.shape[0], 16)
+
+
+def sample_experiences(batch_size: int, replay_buffer: ReplayBuffer, device=None,
+                       board_to_tensor_function: Callable | None = None,
+                       extract_sample_function: Callable = extract_samples_conv,
+                       dtype=torch.float64, idx: torch.Tensor | None = None):
+    """src/dqn_lib.py:67-84: B indices uniform with replacement over the filled rows
+    (np.random.randint(len, size=B) -> torch RNG on the device, graph-safe), then one fused
+    gather + log2-encode kernel.  Returns (states, actions i64, rewards, next_states, dones)."""
+    if idx is None:
+        idx = (torch.rand(batch_size, dtype=torch.float64, device=replay_buffer.device)
+               * replay_buffer.count.to(torch.float64)).to(torch.int64)
+    s, a, r, s2, d, _ = replay_buffer.sample_encode(batch_size, dtype, idx=idx)
+    return extract_sample_function(s), a, r, extract_sample_function(s2), d
+
+
+def one_hot(tensor: torch.Tensor, no_outputs: int, device=None) -> torch.Tensor:
+    """src/dqn_lib.py:110-116 (same assertions, float32 result)."""
+    assert tensor.max().item() + 1 <= no_outputs, \
+        "One hot encoded array size has to be bigger or equal than max scalar value"
+    assert len(tensor.shape) == 1, "should be 1D"
+    encoded = torch.zeros(tensor.shape[0], no_outputs, device=tensor.device)
+    encoded[torch.arange(tensor.shape[0], device=tensor.device), tensor] = 1
+    return encoded
+
+
+# ------------------------------------------------------------------ learning (src/dqn_lib.py:119-164)
+def bellman_targets(model, target_model, rewards, next_states, dones, discount_factor,
+                    use_double_dqn: bool = True) -> torch.Tensor:
+    """y = r + (1 - done) * gamma * Q_target(s', a*) with a* = argmax Q_online(s') (double,
+    :125-132) or max_a Q_target(s', a) (vanilla, :133-144).  No autograd (F10).
+    Parity: the reference multiplies the int64 (1 - dones) by the Python float gamma, which
+    torch evaluates in float32, so gamma enters as float32(0.8) -- reproduced here."""
+    with torch.no_grad():
+        if use_double_dqn:
+            a_star = torch.argmax(model(next_states), dim=1)
+            next_q = target_model(next_states).gather(1, a_star[:, None])[:, 0]
+        else:
+            next_q = torch.max(target_model(next_states), dim=1).values
+        disc = (1 - dones).to(torch.float32) * torch.tensor(discount_factor, dtype=torch.float32)
+        return rewards.to(next_q.dtype) + disc.to(next_q.dtype) * next_q
+
+
+def dqn_loss(model, target_model, states, actions, rewards, next_states, dones, discount_factor,
+             use_double_dqn: bool = True):
+    """MSELoss(reduction='sum') of Q_online(s)[a] against the Bellman target (:146-158).
+    The reference's one_hot-mask-and-sum picks the same element as gather (exact)."""
+    y = bellman_targets(model, target_model, rewards, next_states, dones, discount_factor,
+                        use_double_dqn)
+    q = model(states).gather(1, actions[:, None].to(torch.int64))[:, 0]
+    return ((q - y) ** 2).sum(), q, y
+
+
+def train_step(batch_size: int, discount_factor: float, model: torch.nn.Module,
+               target_model: torch.nn.Module, replay_buffer: ReplayBuffer,
+               loss_fn: Callable | None, optimizer: torch.optim.Optimizer, device=None,
+               use_double_dqn: bool = True,
+               board_to_tensor_function: Callable = board_as_4d_tensor,
+               extract_samples_function: Callable = extract_samples_conv,
+               reference_compat: bool = False, idx: torch.Tensor | None = None):
+    """src/dqn_lib.py:119-164 on one minibatch sampled from the HBM replay ring.
+    loss_fn is accepted for signature parity; the loss is MSE(sum) as in the configs
+    (src/configs/double_dqn_conv.py:38).  reference_compat=True reproduces the reference's
+    backward -> zero_grad -> step order, in which the optimizer never updates (F1)."""
+    dtype = _model_dtype(model)
+    states, actions, rewards, next_states, dones = sample_experiences(
+        batch_size, replay_buffer, device, board_to_tensor_function, extract_samples_function,
+        dtype=dtype, idx=idx)
+    if reference_compat:
+        loss, _, _ = dqn_loss(model, target_model, states, actions, rewards, next_states, dones,
+                              discount_factor, use_double_dqn)
+        loss.backward()
+        optimizer.zero_grad()
+        optimizer.step()
+        return loss
+    optimizer.zero_grad()
+    loss, _, _ = dqn_loss(model, target_model, states, actions, rewards, next_states, dones,
+                          discount_factor, use_double_dqn)
+    loss.backward()
+    optimizer.step()
+    return loss
+
+
+def sync_target(model: torch.nn.Module, target_model: torch.nn.Module) -> None:
+    """target_model.load_state_dict(copy.deepcopy(model.state_dict())) (src/dqn_lib.py:227-228),
+    as an in-place device copy."""
+    with torch.no_grad():
+        for pt, p in zip(target_model.parameters(), model.parameters()):
+            pt.copy_(p)

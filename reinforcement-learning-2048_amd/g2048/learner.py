@@ -1,0 +1,192 @@
+"""Device-resident Double-DQN learner and vectorised training loop.
+
+DQNLearner.update() is one reference train_step (src/dqn_lib.py:119-164) at batch B:
+sample (torch RNG on device) -> g2048 gather+encode kernel -> online(s'), target(s') -> Bellman
+target -> online(s) -> MSE(sum) -> backward -> [RCCL all_reduce of ONE flat gradient bucket when
+world > 1] -> Adam.  Everything except the collective is captured into hipGraphs, so an update
+costs one (single GPU) or two graph replays plus one all_reduce.
+
+Trainer is the vectorised training_loop (src/dqn_lib.py:167-244): every iteration steps all N
+boards once with the fused epsilon-greedy kernel (Q from the same online net) and runs
+`updates_per_step` learner updates; the epsilon schedule, target sync and episode statistics
+stay on the device.
+"""
+from __future__ import annotations
+
+import copy
+
+import torch
+import torch.distributed as dist
+
+from . import dqn_lib
+from .env import ReplayBuffer, VecEnv2048
+from .nets import NETS, make_net
+
+
+class DQNLearner:
+    def __init__(self, replay: ReplayBuffer, net: str = "conv", dtype=torch.float32,
+                 batch_size: int = 8192, discount_factor: float = 0.8, lr: float = 1e-2,
+                 use_double_dqn: bool = True, target_sync_every: int = 100, graph: bool = True,
+                 seed: int = 0, model: torch.nn.Module | None = None,
+                 process_group=None):
+        self.replay = replay
+        self.device = replay.device
+        self.dtype = dtype
+        self.B = int(batch_size)
+        self.gamma = float(discount_factor)
+        self.use_double_dqn = use_double_dqn
+        self.conv_input = NETS[net][1]
+        self.target_sync_every = int(target_sync_every)
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        if model is None:
+            torch.manual_seed(seed)
+            model = make_net(net, dtype=dtype, device=self.device)
+        self.model = model
+        if self.world > 1:  # identical init everywhere: broadcast rank 0's weights once
+            for p in self.model.parameters():
+                dist.broadcast(p.data, src=0, group=process_group)
+        self.target = copy.deepcopy(self.model).requires_grad_(False)
+        # one flat gradient bucket; p.grad are views, so the all-reduce is a single collective
+        params = list(self.model.parameters())
+        self.n_params = sum(p.numel() for p in params)
+        self.grad_flat = torch.zeros(self.n_params, dtype=dtype, device=self.device)
+        off = 0
+        for p in params:
+            p.grad = self.grad_flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.opt = torch.optim.Adam(params, lr=lr, capturable=graph, foreach=True)
+        self.updates = 0
+        self.last_loss = torch.zeros((), dtype=dtype, device=self.device)
+        self._graphs = None
+        self.graph = graph
+
+    # -------------------------------------------------------------- one train_step, in pieces
+    def _layout(self, s):
+        return dqn_lib.extract_samples_conv(s) if self.conv_input else dqn_lib.extract_samples_dense(s)
+
+    def _compute_grads(self):
+        self.grad_flat.zero_()
+        s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
+                                                    self._layout, dtype=self.dtype)
+        loss, _, _ = dqn_lib.dqn_loss(self.model, self.target, s, a, r, s2, d, self.gamma,
+                                      self.use_double_dqn)
+        loss.backward()
+        self.last_loss.copy_(loss.detach())
+
+    def _allreduce(self):
+        if self.world > 1:
+            dist.all_reduce(self.grad_flat, group=self.pg)
+            self.grad_flat.div_(self.world)
+
+    def _apply(self):
+        self.opt.step()
+
+    def _capture(self):
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):  # warm-up (allocates Adam state, autograd buffers)
+            for _ in range(2):
+                self._compute_grads()
+                self._allreduce()
+                self._apply()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1):
+            self._compute_grads()
+            if self.world == 1:
+                self._apply()
+        g2 = None
+        if self.world > 1:
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._apply()
+        self._graphs = (g1, g2)
+
+    def update(self) -> torch.Tensor:
+        """One Double-DQN update (intended order zero_grad -> backward -> step). Returns the loss
+        tensor of this update (device, no sync)."""
+        if self.graph:
+            if self._graphs is None:
+                self._capture()
+            g1, g2 = self._graphs
+            g1.replay()
+            if g2 is not None:
+                self._allreduce()
+                g2.replay()
+        else:
+            self._compute_grads()
+            self._allreduce()
+            self._apply()
+        self.updates += 1
+        if self.target_sync_every and self.updates % self.target_sync_every == 0:
+            dqn_lib.sync_target(self.model, self.target)
+        return self.last_loss
+
+    @torch.no_grad()
+    def q_values(self, env: VecEnv2048) -> torch.Tensor:
+        x = env.encode(self.dtype, conv=self.conv_input)
+        return self.model(x).reshape(env.n, 4).contiguous()
+
+
+class Trainer:
+    """Vectorised training_loop (src/dqn_lib.py:167-244).
+
+    Per iteration: Q = online(boards) -> fused epsilon-greedy step of all N boards with replay
+    append -> `updates_per_step` learner updates once the ring holds `min_fill` transitions.
+    epsilon = max((eps_decay_episodes - e) / eps_decay_episodes, min_epsilon) with e the mean
+    number of finished episodes per board (the reference's per-episode schedule, :184-188),
+    computed on the device each iteration."""
+
+    def __init__(self, env: VecEnv2048, replay: ReplayBuffer, learner: DQNLearner,
+                 updates_per_step: int = 1, min_fill: int | None = None,
+                 eps_decay_episodes: float = 1000.0, min_epsilon: float = 0.01):
+        self.env, self.replay, self.learner = env, replay, learner
+        self.updates_per_step = int(updates_per_step)
+        self.min_fill = int(min_fill if min_fill is not None else learner.B)
+        self.eps_decay = float(eps_decay_episodes)
+        self.min_eps = float(min_epsilon)
+        self.eps = torch.ones(1, dtype=torch.float64, device=env.device)
+        self.steps = 0
+
+    def _update_eps(self):
+        e = self.env.ep[:, 0].to(torch.float64).mean()
+        self.eps.copy_(torch.clamp((self.eps_decay - e) / self.eps_decay, min=self.min_eps))
+
+    def prefill(self, steps: int) -> None:
+        """Random-policy steps (eps = 1) in one rollout launch, appended to the ring."""
+        self.env.rollout(steps, replay=self.replay)
+        self.steps += steps
+
+    def step(self) -> None:
+        self._update_eps()
+        q = self.learner.q_values(self.env)
+        self.env.step_egreedy(q, self.eps, replay=self.replay)
+        self.steps += 1
+        if self.steps * self.env.n >= self.min_fill:
+            for _ in range(self.updates_per_step):
+                self.learner.update()
+
+    def episode_stats(self) -> dict:
+        """Experiment.add_episode fields (src/experiments.py:112-122) over the last finished
+        episode of every board (host sync)."""
+        ep = self.env.ep.to(torch.int64)
+        fin = ep[:, 0] > 0
+        if not bool(fin.any()):
+            return {"episodes": 0}
+        sel = ep[fin]
+        return {"episodes": int(ep[:, 0].sum()),
+                "merge_score_mean": float(sel[:, 1].double().mean()),
+                "number_moves_mean": float(sel[:, 2].double().mean()),
+                "max_tile_max": int(2 ** int(sel[:, 3].max())),
+                "max_tile_hist": {int(2 ** int(k)): int(v) for k, v in
+                                  zip(*torch.unique(sel[:, 3], return_counts=True))},
+                "epsilon": float(self.eps.item())}
+
+
+def flops_per_update(net: str, batch: int) -> float:
+    """Algorithmic FLOPs of one update: 3 forwards (online s', target s', online s) + backward of
+    the online forward (2x), i.e. 5 forward-equivalents, 2 FLOP per MAC."""
+    mac = {"conv": 84480, "dense": 402432, "dense64": 1280}[net]
+    return 5.0 * 2.0 * mac * batch
+

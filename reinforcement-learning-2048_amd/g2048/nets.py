@@ -1,0 +1,78 @@
+"""Q-networks of the reference configs, state_dict-compatible with them.
+
+conv    src/configs/double_dqn_conv.py:19-28  Conv2d(1,64,2) ReLU Conv2d(64,64,2) ReLU Flatten
+                                              Linear(256,64) ReLU Linear(64,4)      (33 476 params)
+dense   src/configs/double_dqn_dense.py:7-15  16-512-512-256-4 ReLU MLP              (403 716 params)
+dense64 BASELINE.json configs[2]              16-64-4 ReLU MLP                       (1 348 params)
+
+The conv net keeps nn.Conv2d / nn.Linear parameters under the reference's Sequential indices
+("0", "2", "5", "7") but runs its forward as three GEMMs on 2x2 patches of the 4x4 board:
+conv1 = [B*9, 4] @ [4, 64], conv2 = [B*4, 256] @ [256, 64] (channels-last activations), then
+the two Linears on the (C, H, W)-flattened features -- the same arithmetic as the reference's
+Sequential, routed to rocBLAS/hipBLASLt instead of tiny-kernel convolutions.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+
+class Conv2048(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.add_module("0", nn.Conv2d(1, 64, kernel_size=2))
+        self.add_module("2", nn.Conv2d(64, 64, kernel_size=2))
+        self.add_module("5", nn.Linear(2 * 2 * 64, 64))
+        self.add_module("7", nn.Linear(64, 4))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        c1, c2, l1, l2 = self._modules["0"], self._modules["2"], self._modules["5"], self._modules["7"]
+        B = x.shape[0]
+        x = x.reshape(B, 4, 4)
+        # conv1: 3x3 output positions, patch (kh, kw) flattened like weight[out, 1, kh, kw]
+        p1 = x.unfold(1, 2, 1).unfold(2, 2, 1).reshape(B, 9, 4)
+        h1 = F.relu(F.linear(p1, c1.weight.reshape(64, 4), c1.bias))          # [B, 9, 64] (H,W,C)
+        h1 = h1.reshape(B, 3, 3, 64)
+        # conv2: 2x2 output positions; patch ordered (in, kh, kw) like weight[out, in, kh, kw]
+        p2 = h1.unfold(1, 2, 1).unfold(2, 2, 1)                                # [B, 2, 2, 64, kh, kw]
+        h2 = F.relu(F.linear(p2.reshape(B, 4, 256), c2.weight.reshape(64, 256), c2.bias))  # [B,4,64]
+        feat = h2.transpose(1, 2).reshape(B, 256)                              # Flatten: (C, H, W)
+        return l2(F.relu(l1(feat)))
+
+
+def conv_net() -> nn.Module:
+    return Conv2048()
+
+
+def dense_net() -> nn.Module:
+    return nn.Sequential(nn.Linear(16, 512), nn.ReLU(), nn.Linear(512, 512), nn.ReLU(),
+                         nn.Linear(512, 256), nn.ReLU(), nn.Linear(256, 4))
+
+
+def dense64_net() -> nn.Module:
+    return nn.Sequential(nn.Linear(16, 64), nn.ReLU(), nn.Linear(64, 4))
+
+
+NETS = {"conv": (conv_net, True), "dense": (dense_net, False), "dense64": (dense64_net, False)}
+
+
+def make_net(kind: str, dtype=torch.float32, device=None) -> nn.Module:
+    """Build a reference-architecture Q-net; `conv_input` of NETS[kind] says whether it eats
+    [B, 1, 4, 4] (board_as_4d_tensor) or [B, 16] (board_as_flattened_tensor)."""
+    if kind not in NETS:
+        raise ValueError(f"unknown net {kind!r}; choose from {sorted(NETS)}")
+    return NETS[kind][0]().to(dtype=dtype, device=device)
+
+
+def det_init(model: nn.Module, phase: float) -> nn.Module:
+    """Deterministic weights p.flat[k] = sin(1.3 k + phase) / sqrt(fan_in) -- the pattern the
+    golden learner fixtures were generated with (tests/golden/gen_goldens.py)."""
+    with torch.no_grad():
+        for p in model.parameters():
+            k = torch.arange(p.numel(), dtype=torch.float64)
+            fan_in = int(math.prod(p.shape[1:])) if p.dim() > 1 else 4
+            p.copy_((torch.sin(1.3 * k + phase) / math.sqrt(fan_in)).reshape(p.shape).to(p.dtype))
+    return model

@@ -1,0 +1,120 @@
+"""Learner parity against the reference's train_step (tests/golden/learner_<net>.npz).
+
+The fixtures hold the reference's own loss for one B=512 minibatch (dqn_lib.train_step,
+src/dqn_lib.py:119-164) with deterministic weights, plus Q-values, Bellman targets, correct-order
+gradients and one Adam step.  Tolerance (north star): 1e-6 absolute on loss and Q-values in
+float64.  These CPU tests run the learner's torch code on CPU tensors; the GPU versions in
+test_learner_gpu.py run the same math after the HIP replay gather."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from g2048 import dqn_lib
+from g2048.nets import det_init, make_net
+
+NETS = ["conv", "dense", "dense64"]
+ATOL = 1e-6
+
+
+def load(golden_dir, net):
+    return np.load(os.path.join(golden_dir, f"learner_{net}.npz"))
+
+
+def batch(g, device="cpu", dtype=torch.float64):
+    idx = g["idx"]
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).to(device)
+    s = t(g["buf_s"][idx]).to(dtype)
+    s2 = t(g["buf_s2"][idx]).to(dtype)
+    return s, t(g["buf_a"][idx]), t(g["buf_r"][idx]).to(dtype), s2, t(g["buf_d"][idx]).to(dtype)
+
+
+def nets(net, device="cpu"):
+    m = det_init(make_net(net, torch.float64, device), 0.5)
+    tg = det_init(make_net(net, torch.float64, device), 0.2)
+    return m, tg
+
+
+@pytest.mark.parametrize("net", NETS)
+def test_loss_and_q_values_match_reference(golden_dir, net):
+    g = load(golden_dir, net)
+    m, tg = nets(net)
+    s, a, r, s2, d = batch(g)
+    if net == "conv":
+        s, s2 = dqn_lib.extract_samples_conv(s), dqn_lib.extract_samples_conv(s2)
+    loss, q, y = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]))
+    assert abs(float(loss) - float(g["loss_ref"])) <= ATOL + 1e-14 * abs(float(g["loss_ref"]))
+    np.testing.assert_allclose(q.detach().numpy(), g["q"], rtol=1e-12, atol=ATOL)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=1e-12, atol=ATOL)
+    with torch.no_grad():
+        np.testing.assert_allclose(m(s).numpy(), g["q_on_s"], rtol=1e-12, atol=ATOL)
+        np.testing.assert_allclose(m(s2).numpy(), g["q_on_s2"], rtol=1e-12, atol=ATOL)
+        np.testing.assert_allclose(tg(s2).numpy(), g["q_tgt_s2"], rtol=1e-12, atol=ATOL)
+        assert np.array_equal(torch.argmax(m(s2), 1).numpy(), g["a_star"])
+
+
+@pytest.mark.parametrize("net", NETS)
+def test_gradients_and_adam_step(golden_dir, net):
+    g = load(golden_dir, net)
+    m, tg = nets(net)
+    s, a, r, s2, d = batch(g)
+    if net == "conv":
+        s, s2 = dqn_lib.extract_samples_conv(s), dqn_lib.extract_samples_conv(s2)
+    opt = torch.optim.Adam(m.parameters(), lr=float(g["lr"]))
+    opt.zero_grad()
+    loss, _, _ = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]))
+    loss.backward()
+    grads = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).numpy()
+    opt.step()
+    after = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
+    if "grads" in g:
+        np.testing.assert_allclose(grads, g["grads"], rtol=1e-9, atol=1e-9 * np.abs(g["grads"]).max())
+        np.testing.assert_allclose(after, g["params_after"], rtol=1e-12, atol=1e-12)
+    else:
+        sel = g["grad_sel"]
+        np.testing.assert_allclose(grads[sel], g["grads_sampled"], rtol=1e-9,
+                                   atol=1e-9 * np.abs(g["grads_sampled"]).max())
+        np.testing.assert_allclose(grads.sum(), g["grad_sum"], rtol=1e-9)
+        np.testing.assert_allclose((grads * grads).sum(), g["grad_sumsq"], rtol=1e-9)
+        np.testing.assert_allclose(after[sel], g["params_after_sampled"], rtol=1e-12, atol=1e-12)
+
+
+def test_reference_compat_order_is_a_noop(golden_dir):
+    """F1: backward -> zero_grad -> step leaves the weights exactly unchanged."""
+    g = load(golden_dir, "dense64")
+    m, tg = nets("dense64")
+    before = [p.detach().clone() for p in m.parameters()]
+    s, a, r, s2, d = batch(g)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
+    loss, _, _ = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, 0.8)
+    loss.backward()
+    opt.zero_grad()
+    opt.step()
+    assert all(torch.equal(p, q) for p, q in zip(m.parameters(), before))
+
+
+def test_one_hot_matches_reference_semantics():
+    t = torch.tensor([0, 3, 1, 1])
+    oh = dqn_lib.one_hot(t, 4, "cpu")
+    assert oh.dtype == torch.float32 and oh.tolist() == [[1, 0, 0, 0], [0, 0, 0, 1], [0, 1, 0, 0],
+                                                         [0, 1, 0, 0]]
+    with pytest.raises(AssertionError):
+        dqn_lib.one_hot(torch.tensor([4]), 4, "cpu")
+    with pytest.raises(AssertionError):
+        dqn_lib.one_hot(torch.zeros(2, 2, dtype=torch.int64), 4, "cpu")
+
+
+def test_conv_net_state_dict_matches_reference_layout():
+    from torch import nn
+    m = make_net("conv", torch.float64)
+    ref = nn.Sequential(nn.Conv2d(1, 64, 2), nn.ReLU(), nn.Conv2d(64, 64, 2), nn.ReLU(),
+                        nn.Flatten(), nn.Linear(256, 64), nn.ReLU(), nn.Linear(64, 4)).double()
+    assert [(k, v.shape) for k, v in m.state_dict().items()] == \
+           [(k, v.shape) for k, v in ref.state_dict().items()]
+    ref.load_state_dict(m.state_dict())
+    x = torch.randint(0, 15, (300, 1, 4, 4)).double()
+    np.testing.assert_allclose(m(x).detach().numpy(), ref(x).detach().numpy(), rtol=1e-13, atol=1e-12)
+    assert sum(p.numel() for p in m.parameters()) == 33476
+    assert sum(p.numel() for p in make_net("dense").parameters()) == 403716
+    assert sum(p.numel() for p in make_net("dense64").parameters()) == 1348
