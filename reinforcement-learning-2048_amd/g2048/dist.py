@@ -1,0 +1,78 @@
+"""Data-parallel plumbing for the learner (one process per GPU, RCCL over xGMI).
+
+The reference is single-process (no distributed backend).  The build shards the
+BOARDS across ranks (board_offset = rank * N, no exchange on the env path) and keeps one learner
+replica per rank whose gradients are averaged with ONE all-reduce of a flat bucket per update:
+conv 33 476 params = 134 KB fp32, dense-64 5.4 KB, dense-ref 1.6 MB -- all latency-bound on
+xGMI, so a single bucket (one ring pass) beats per-tensor collectives.
+Backend-agnostic: the CPU tests run it over gloo.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def init_from_env(backend: str | None = None):
+    """torchrun-style init (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*).  Returns
+    (world, rank, device).  backend None -> "nccl" (RCCL) when a GPU is visible, else "gloo"."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        if use_gpu:
+            torch.cuda.set_device(dev)
+            dist.init_process_group(backend or "nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend or "gloo")
+    return world, rank, dev
+
+
+def world_size(group=None) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def broadcast_params(model: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Identical initial weights on every rank (target nets then stay in lockstep)."""
+    if world_size(group) > 1:
+        with torch.no_grad():
+            for p in model.parameters():
+                dist.broadcast(p.data, src=src, group=group)
+
+
+class FlatGradBucket:
+    """All parameter .grad tensors as views of ONE flat buffer, so zeroing and the gradient
+    all-reduce are single operations (and stay valid inside a captured hipGraph)."""
+
+    def __init__(self, model: torch.nn.Module, dtype=None):
+        params = list(model.parameters())
+        self.params = params
+        self.numel = sum(p.numel() for p in params)
+        dtype = dtype or params[0].dtype
+        self.flat = torch.zeros(self.numel, dtype=dtype, device=params[0].device)
+        off = 0
+        for p in params:
+            p.grad = self.flat[off:off + p.numel()].view_as(p)
+            off += p.numel()
+
+    def zero_(self):
+        self.flat.zero_()
+
+    def allreduce_mean_(self, group=None) -> None:
+        w = world_size(group)
+        if w > 1:
+            dist.all_reduce(self.flat, group=group)
+            self.flat.div_(w)
+
+    @property
+    def nbytes(self) -> int:
+        return self.flat.numel() * self.flat.element_size()
+
+
+def shard_offset(rank: int, boards_per_rank: int) -> int:
+    """Global id of a rank's first board: Philox subsequences never overlap across ranks."""
+    return rank * boards_per_rank

@@ -16,9 +16,9 @@ from __future__ import annotations
 import copy
 
 import torch
-import torch.distributed as dist
 
 from . import dqn_lib
+from .dist import FlatGradBucket, broadcast_params, world_size
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, make_net
 
@@ -38,23 +38,18 @@ class DQNLearner:
         self.conv_input = NETS[net][1]
         self.target_sync_every = int(target_sync_every)
         self.pg = process_group
-        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.world = world_size(process_group)
         if model is None:
             torch.manual_seed(seed)
             model = make_net(net, dtype=dtype, device=self.device)
         self.model = model
-        if self.world > 1:  # identical init everywhere: broadcast rank 0's weights once
-            for p in self.model.parameters():
-                dist.broadcast(p.data, src=0, group=process_group)
+        broadcast_params(self.model, 0, process_group)  # identical init on every rank
         self.target = copy.deepcopy(self.model).requires_grad_(False)
         # one flat gradient bucket; p.grad are views, so the all-reduce is a single collective
-        params = list(self.model.parameters())
-        self.n_params = sum(p.numel() for p in params)
-        self.grad_flat = torch.zeros(self.n_params, dtype=dtype, device=self.device)
-        off = 0
-        for p in params:
-            p.grad = self.grad_flat[off:off + p.numel()].view_as(p)
-            off += p.numel()
+        self.bucket = FlatGradBucket(self.model)
+        self.grad_flat = self.bucket.flat
+        self.n_params = self.bucket.numel
+        params = self.bucket.params
         self.opt = torch.optim.Adam(params, lr=lr, capturable=graph, foreach=True)
         self.updates = 0
         self.last_loss = torch.zeros((), dtype=dtype, device=self.device)
@@ -75,14 +70,15 @@ class DQNLearner:
         self.last_loss.copy_(loss.detach())
 
     def _allreduce(self):
-        if self.world > 1:
-            dist.all_reduce(self.grad_flat, group=self.pg)
-            self.grad_flat.div_(self.world)
+        self.bucket.allreduce_mean_(self.pg)
 
     def _apply(self):
         self.opt.step()
 
     def _capture(self):
+        # the warm-up below runs real updates; snapshot weights so capture leaves no trace
+        params = list(self.model.parameters())
+        snap = [p.detach().clone() for p in params]
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):  # warm-up (allocates Adam state, autograd buffers)
@@ -102,6 +98,15 @@ class DQNLearner:
             with torch.cuda.graph(g2):
                 self._apply()
         self._graphs = (g1, g2)
+        with torch.no_grad():  # restore in place (the graphs hold these addresses)
+            for p, s in zip(params, snap):
+                p.copy_(s)
+            for st in self.opt.state.values():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+            self.grad_flat.zero_()
+            self.last_loss.zero_()
 
     def update(self) -> torch.Tensor:
         """One Double-DQN update (intended order zero_grad -> backward -> step). Returns the loss
