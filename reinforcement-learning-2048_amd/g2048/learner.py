@@ -28,7 +28,7 @@ class DQNLearner:
                  batch_size: int = 8192, discount_factor: float = 0.8, lr: float = 1e-2,
                  use_double_dqn: bool = True, target_sync_every: int = 100, graph: bool = True,
                  seed: int = 0, model: torch.nn.Module | None = None,
-                 process_group=None):
+                 process_group=None, sampler=None):
         self.replay = replay
         self.device = replay.device
         self.dtype = dtype
@@ -38,6 +38,9 @@ class DQNLearner:
         self.conv_input = NETS[net][1]
         self.target_sync_every = int(target_sync_every)
         self.pg = process_group
+        # sampler(B, replay) -> int64 indices on the device; None = uniform with replacement over
+        # the filled rows (src/dqn_lib.py:68), drawn by torch's graph-safe device RNG
+        self.sampler = sampler
         self.world = world_size(process_group)
         if model is None:
             torch.manual_seed(seed)
@@ -62,8 +65,9 @@ class DQNLearner:
 
     def _compute_grads(self):
         self.grad_flat.zero_()
+        idx = self.sampler(self.B, self.replay) if self.sampler is not None else None
         s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
-                                                    self._layout, dtype=self.dtype)
+                                                    self._layout, dtype=self.dtype, idx=idx)
         loss, _, _ = dqn_lib.dqn_loss(self.model, self.target, s, a, r, s2, d, self.gamma,
                                       self.use_double_dqn)
         loss.backward()

@@ -43,7 +43,7 @@ def test_train_step_matches_reference(G, golden_dir, net):
     s, a, r, s2, d = dqn_lib.sample_experiences(len(idx), rb, DEV, None, ext, idx=idx)
     loss, q, y = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]))
     ref = float(g["loss_ref"])
-    assert abs(float(loss) - ref) <= 1e-6 + 1e-13 * abs(ref), (float(loss), ref)
+    assert abs(float(loss.detach()) - ref) <= 1e-6 + 1e-13 * abs(ref), (float(loss.detach()), ref)
     np.testing.assert_allclose(q.detach().cpu().numpy(), g["q"], rtol=1e-12, atol=1e-6)
     np.testing.assert_allclose(y.cpu().numpy(), g["y"], rtol=1e-12, atol=1e-6)
     with torch.no_grad():
@@ -81,24 +81,32 @@ def test_train_step_reference_compat_noop(G, golden_dir):
 
 @pytest.mark.parametrize("net", ["dense64", "conv"])
 def test_graphed_learner_equals_eager(G, net):
-    """hipGraph-captured update == eager update.  A ring holding one repeated transition makes
-    every sampled index give the same batch, so the two paths see identical data."""
+    """hipGraph-captured update == eager update on the same (deterministic) minibatches.
+    Gradients of the first update agree to fp64 roundoff; later losses only loosely, because
+    Adam's first steps are ~lr*sign(g) and amplify roundoff in near-zero gradients."""
     from g2048.learner import DQNLearner
 
-    C = 4096
-    rng = np.random.default_rng(0)
-    s = np.tile(rng.integers(0, 8, size=16), (C, 1))
-    s2 = np.tile(rng.integers(0, 8, size=16), (C, 1))
+    n, C = 2048, 16 * 2048
+    env = G.VecEnv2048(n, device=DEV, seed=12)
+    rb = G.ReplayBuffer(C, device=DEV)
+    env.rollout(C // n, replay=rb)
+    calls = {"k": 0}
+
+    def sampler(B, replay):  # fixed strided rows, identical for both paths
+        return (torch.arange(B, device=DEV) * 13 + 5) % C
+
     outs = []
     for graph in (True, False):
-        rb = G.ReplayBuffer(C, device=DEV)
-        rb.load(s, np.full(C, 2), np.full(C, 16), s2, np.zeros(C))
-        L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=1024, graph=graph, seed=3,
-                       target_sync_every=2)
-        losses = [float(L.update()) for _ in range(5)]
-        outs.append((losses, torch.cat([p.detach().reshape(-1) for p in L.model.parameters()])))
-    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-5)
-    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-6)
+        L = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=1024, graph=graph, seed=3,
+                       target_sync_every=2, sampler=sampler)
+        first = [float(L.update())]
+        g1 = L.grad_flat.clone()
+        first += [float(L.update()) for _ in range(4)]
+        outs.append((first, g1))
+    assert outs[0][0][0] == pytest.approx(outs[1][0][0], rel=1e-12)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-9, atol=1e-9 * float(outs[1][1].abs().max()))
+    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-3)
+    del calls
 
 
 def test_trainer_runs_and_learns_statistics(G):
