@@ -177,10 +177,14 @@ static void spawn(uint8_t b[16], uint32_t u_cell, uint32_t u_val, uint32_t flags
     }
 }
 
+/* board.py:18-20: two spawns on an empty board.  Both come from ONE Philox block u: the
+ * first takes (u2, u3), the second the low 28 bits of u2 for its cell and the low 30 bits of u0
+ * for its value -- exactly the words a terminal step leaves unused, so an auto-reset needs no
+ * second draw. */
 static void fresh_board(uint8_t b[16], const uint32_t u[4], uint32_t flags) {
     memset(b, 0, 16);
-    spawn(b, u[0], u[1], flags);   /* board.py:18-20: two spawns on an empty board */
     spawn(b, u[2], u[3], flags);
+    spawn(b, u[2] << 4, u[0] << 2, flags);
 }
 
 void o2048_env_reset(o2048_env* e, const uint8_t* mask, uint32_t epoch) {
@@ -284,9 +288,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             for (int k = 0; k < 16; ++k) if (b[k] > mx) mx = b[k];
             ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;
             if (autoreset) {
-                uint32_t ur[4];
-                draw(e->seed, gid, 1u, t, ur);
-                fresh_board(b, ur, e->flags);
+                fresh_board(b, u, e->flags);   /* the step's own block (see fresh_board) */
                 m[0] = 0; m[1] = 0;
             }
         }

@@ -90,7 +90,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         const bool fixed = (A.flags & G2048_EGREEDY_FIXED) != 0u;
         if (explore) {
             const uint32_t nl = __popc(legal);
-            act = (fixed && nl) ? kth_bit16(legal, __umulhi(u.x, nl)) : (u.x >> 30);
+            act = (fixed && nl) ? kth_bit4(legal, __umulhi(u.x, nl)) : (u.x >> 30);
         } else if constexpr (MODE == MODE_EG_F32) {
             const float4 q = reinterpret_cast<const float4*>(A.q)[i];
             act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
@@ -111,8 +111,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         r = apply_move(b, act);
         if constexpr (MODE == MODE_INJECT) {
             const int si = A.spawn_idx[i];
-            const uint32_t Z = empty_mask(b);
-            if (si >= 0 && si < 16 && ((Z >> si) & 1u)) set_cell(b, (uint32_t)si, A.spawn_exp[i]);
+            if (si >= 0 && si < 16 && cell_empty(b, (uint32_t)si)) set_cell(b, (uint32_t)si, A.spawn_exp[i]);
             else atomicAdd(A.err, 1ull);
         } else {
             spawn(b, u.z, u.w, A.p4_thresh);
@@ -135,7 +134,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     if (done) {
         A.ep[i] = make_uint4(A.ep[i].x + 1u, m.x, m.y, max_exp(b));
         if (!(A.flags & G2048_NO_AUTORESET)) {
-            b = fresh_board(draw(A.seed_lo, A.seed_hi, gid, DOMAIN_AUTORESET, t), A.p4_thresh);
+            b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m.x = 0u;
             m.y = 0u;
         }

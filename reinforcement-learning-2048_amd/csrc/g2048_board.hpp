@@ -1,21 +1,26 @@
 // g2048_board.hpp -- per-lane 2048 board arithmetic for gfx950 (device-only).
 //
-// A board is four u32 "rows" held in VGPRs; byte c of row r is the log2 exponent of cell (r, c)
-// (0 = empty).  All four moves are reduced to "slide every row toward byte 0":
-//   left = identity, right = byte-reverse, up = 4x4 byte transpose, down = transpose + reverse;
-// the transpose is 8 v_perm_b32, the reverse one v_perm_b32 per row with a per-lane selector, so
-// lanes taking different actions run the same instruction stream (no divergence).
-// The legal-move mask is computed without sliding at all: packed-byte (SWAR) zero / equality tests
-// give 16-bit occupancy masks whose shifts expose "a tile can move into a hole" and "two equal
-// neighbours can merge".
+// A board is four u32 words in VGPRs; byte c of word r is the log2 exponent of cell (r, c)
+// (0 = empty).  Every move is computed LINE-PARALLEL: the four cells along the move direction
+// become four words L0..L3 whose byte j belongs to line j, so one VALU op advances all four
+// rows (or columns) at once:
+//   up    L_k = row k              down  L_k = row 3-k
+//   left  L_k = column k           right L_k = column 3-k     (columns = 8-v_perm_b32 transpose)
+// and the slide is "compact the non-empty bytes toward L0, then merge equal neighbours once,
+// front first" on whole words: zero/equality tests are packed-byte (SWAR) adds, byte masks are
+// expanded with v_perm_b32's sign-replicate selectors, selects are v_bfi_b32.  Lanes taking
+// different actions run one instruction stream (no divergence).
 //
 // Reference semantics (ribal-aladeeb/reinforcement-learning-2048):
 //   slide/merge/score  src/board.py:92-126 (score += value of each NEW tile, :114)
 //   direction mapping  src/board.py:147-183
 //   legal mask         src/board.py:128-135
 //   spawn distribution src/board.py:41-51 (uniform empty cell, row-major; 2 or 4, p(4)=0.5)
-// Checked bit-for-bit against the oracle and the reference's exhaustive 65 536-row LUT in
-// tests/test_env_gpu.py.
+// Checked bit-for-bit against the reference's exhaustive 65 536-row LUT (all four directions),
+// its recorded trajectories and the CPU oracle in tests/test_env_gpu.py.
+//
+// Domain: exponents < 128 (tiles < 2^128; a 4x4 game cannot pass 2^17); the merge-score
+// reward is exact while merged tiles stay <= 2^30.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -23,19 +28,22 @@
 
 namespace g2048 {
 
+constexpr uint32_t K7F = 0x7F7F7F7Fu;
+constexpr uint32_t K80 = 0x80808080u;
+
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
     return __builtin_amdgcn_perm(hi, lo, sel);
 }
-
-// 0x80 in every non-zero byte of x, 0 elsewhere (exact, no cross-byte carries).
-__device__ __forceinline__ uint32_t nz_bytes(uint32_t x) {
-    return (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+// 0x80 in every non-zero / zero byte (bytes < 0x80: x + 0x7F never carries across bytes).
+__device__ __forceinline__ uint32_t nz80(uint32_t x) { return (x + K7F) & K80; }
+__device__ __forceinline__ uint32_t z80(uint32_t x) { return ~(x + K7F) & K80; }
+// 0x80 byte flags -> 0xFF byte masks: v_perm selectors 8/10/9/11 replicate bit 15/47/31/63 of
+// {hi, lo}, i.e. the flags of bytes 0/1/2/3 once lo = f << 8 and hi = f.
+__device__ __forceinline__ uint32_t expand80(uint32_t f) { return perm(f, f << 8, 0x0B090A08u); }
+// per-bit select (v_bfi_b32): bits of a where m, else b
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+    return (a & m) | (b & ~m);
 }
-// bit c set iff byte c of x is non-zero.
-__device__ __forceinline__ uint32_t nz4(uint32_t x) {
-    return (((nz_bytes(x) >> 7) * 0x00204081u) >> 21) & 0xFu;
-}
-__device__ __forceinline__ uint32_t z4(uint32_t x) { return (~nz4(x)) & 0xFu; }
 
 struct Board {
     uint32_t r0, r1, r2, r3;
@@ -54,94 +62,96 @@ __device__ __forceinline__ Board transpose(const Board& b) {
     return t;
 }
 
-// 16-bit empty-cell mask, bit 4r + c.
-__device__ __forceinline__ uint32_t empty_mask(const Board& b) {
-    return z4(b.r0) | (z4(b.r1) << 4) | (z4(b.r2) << 8) | (z4(b.r3) << 12);
-}
-
-// Legal-move mask (bit 0 up, 1 down, 2 left, 3 right) == src/board.py:128-135.
+// Legal-move mask (bit 0 up, 1 down, 2 left, 3 right) == src/board.py:128-135, without sliding:
+// a move is legal iff some tile has a hole next to it in the move direction, or two equal
+// non-empty neighbours lie along it.
 __device__ __forceinline__ uint32_t legal_mask(const Board& b) {
-    const uint32_t n0 = nz4(b.r0), n1 = nz4(b.r1), n2 = nz4(b.r2), n3 = nz4(b.r3);
-    const uint32_t N = n0 | (n1 << 4) | (n2 << 8) | (n3 << 12);
-    const uint32_t Z = (~N) & 0xFFFFu;
-    // a tile next to a hole in the move direction
-    const uint32_t left = Z & (N >> 1) & 0x7777u;
-    const uint32_t right = N & (Z >> 1) & 0x7777u;
-    const uint32_t up = Z & (N >> 4) & 0x0FFFu;
-    const uint32_t down = N & (Z >> 4) & 0x0FFFu;
-    // equal non-zero neighbours: horizontal (c, c+1) and vertical (r, r+1)
-    const uint32_t H = ((z4(b.r0 ^ (b.r0 >> 8)) & n0) | ((z4(b.r1 ^ (b.r1 >> 8)) & n1) << 4) |
-                        ((z4(b.r2 ^ (b.r2 >> 8)) & n2) << 8) |
-                        ((z4(b.r3 ^ (b.r3 >> 8)) & n3) << 12)) & 0x7777u;
-    const uint32_t V = (z4(b.r0 ^ b.r1) & n0) | ((z4(b.r1 ^ b.r2) & n1) << 4) |
-                       ((z4(b.r2 ^ b.r3) & n2) << 8);
-    return ((up | V) != 0u) | (((down | V) != 0u) << 1) | (((left | H) != 0u) << 2) |
-           (((right | H) != 0u) << 3);
+    const uint32_t n0 = nz80(b.r0), n1 = nz80(b.r1), n2 = nz80(b.r2), n3 = nz80(b.r3);
+    // within a row: hole at c, tile at c+1 (left) / tile at c, hole at c+1 (right)
+    const uint32_t s0 = n0 >> 8, s1 = n1 >> 8, s2 = n2 >> 8, s3 = n3 >> 8;
+    const uint32_t L = (~n0 & s0) | (~n1 & s1) | (~n2 & s2) | (~n3 & s3);
+    const uint32_t R = ((n0 & ~s0) | (n1 & ~s1) | (n2 & ~s2) | (n3 & ~s3)) & 0x00808080u;
+    const uint32_t H = ((z80(b.r0 ^ (b.r0 >> 8)) & n0) | (z80(b.r1 ^ (b.r1 >> 8)) & n1) |
+                        (z80(b.r2 ^ (b.r2 >> 8)) & n2) | (z80(b.r3 ^ (b.r3 >> 8)) & n3)) &
+                       0x00808080u;
+    // across rows: hole in row r, tile in row r+1 (up) / the reverse (down); equal pairs
+    const uint32_t U = (~n0 & n1) | (~n1 & n2) | (~n2 & n3);
+    const uint32_t D = (n0 & ~n1) | (n1 & ~n2) | (n2 & ~n3);
+    const uint32_t V = (z80(b.r0 ^ b.r1) & n0) | (z80(b.r1 ^ b.r2) & n1) | (z80(b.r2 ^ b.r3) & n2);
+    return (uint32_t)((U | V) != 0u) | ((uint32_t)((D | V) != 0u) << 1) |
+           ((uint32_t)((L | H) != 0u) << 2) | ((uint32_t)((R | H) != 0u) << 3);
 }
 
-// Slide one row toward byte 0, merging equal neighbours once, leftmost first; adds the value
-// of every new tile to `score` (src/board.py:92-126).
-__device__ __forceinline__ uint32_t slide_row(uint32_t x, uint32_t& score) {
-    // 1) compact the non-zero bytes to the front with one v_perm_b32; selector byte k = index of
-    //    the k-th non-zero byte, or 4 (= a byte of the zero hi operand) when there is none.
-    uint32_t m = nz4(x);
-    const uint32_t s0 = min((uint32_t)(__ffs(m) - 1), 4u);
-    m &= m - 1u;
-    const uint32_t s1 = min((uint32_t)(__ffs(m) - 1), 4u);
-    m &= m - 1u;
-    const uint32_t s2 = min((uint32_t)(__ffs(m) - 1), 4u);
-    m &= m - 1u;
-    const uint32_t s3 = min((uint32_t)(__ffs(m) - 1), 4u);
-    const uint32_t c = perm(0u, x, s0 | (s1 << 8) | (s2 << 16) | (s3 << 24));
-    // 2) merge pass over the compacted [a b c d]
-    const uint32_t a = c & 0xFFu, b = (c >> 8) & 0xFFu, e = (c >> 16) & 0xFFu, d = c >> 24;
-    const bool ab = (a == b) & (a != 0u);
-    const bool bc = (b == e) & (b != 0u) & !ab;          // b+c merge (only if a,b did not)
-    const bool cd = (e == d) & (e != 0u) & (ab | !((b == e) & (b != 0u)));
-    const uint32_t o0 = a + (uint32_t)ab;
-    const uint32_t o1 = ab ? (e + (uint32_t)cd) : (b + (uint32_t)bc);
-    const uint32_t o2 = ab ? (cd ? 0u : d) : (bc ? d : (e + (uint32_t)cd));
-    const uint32_t o3 = (ab | bc | cd) ? 0u : d;
-    score += (ab ? (2u << (a & 31u)) : 0u) + (bc ? (2u << (b & 31u)) : 0u) +
-             (cd ? (2u << (e & 31u)) : 0u);
-    return o0 | (o1 << 8) | (o2 << 16) | (o3 << 24);
+// Slide the four lines toward L0 (byte j of L_k = k-th cell of line j); returns the merge gain.
+__device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint32_t& l2,
+                                                uint32_t& l3) {
+    // 1) stable compaction, back to front: [c d] then [b c d] then [a b c d]
+    uint32_t m = expand80(z80(l2));
+    l2 = bsel(m, l3, l2);
+    l3 &= ~m;
+    m = expand80(z80(l1));
+    l1 = bsel(m, l2, l1);
+    l2 = bsel(m, l3, l2);
+    l3 &= ~m;
+    m = expand80(z80(l0));
+    l0 = bsel(m, l1, l0);
+    l1 = bsel(m, l2, l1);
+    l2 = bsel(m, l3, l2);
+    l3 &= ~m;
+    // 2) merges, front first; each tile merges at most once
+    const uint32_t ab = z80(l0 ^ l1) & nz80(l0);
+    const uint32_t bc_raw = z80(l1 ^ l2) & nz80(l1);
+    const uint32_t cd_raw = z80(l2 ^ l3) & nz80(l2);
+    const uint32_t bc = bc_raw & ~ab;
+    const uint32_t cd = cd_raw & (ab | ~bc_raw);
+    const uint32_t AB = expand80(ab), BC = expand80(bc), CD = expand80(cd);
+    const uint32_t c1 = l2 + (cd >> 7);  // merged c+d (when that merge happens)
+    const uint32_t b1 = l1 + (bc >> 7);  // merged b+c
+    const uint32_t o0 = l0 + (ab >> 7);  // merged a+b
+    const uint32_t o1 = bsel(AB, c1, b1);
+    const uint32_t o2 = bsel(AB, l3 & ~CD, bsel(BC, l3, c1));
+    const uint32_t o3 = l3 & ~(AB | BC | CD);
+    // 3) score = sum of 2^e over the merged tiles: 12 candidate bytes, zero bytes give 2^0 = 1
+    const uint32_t e0 = o0 & AB, e1 = b1 & BC, e2 = c1 & CD;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        s += 1u << ((e0 >> (8 * k)) & 31u);
+        s += 1u << ((e1 >> (8 * k)) & 31u);
+        s += 1u << ((e2 >> (8 * k)) & 31u);
+    }
+    s -= 12u - (uint32_t)(__popc(ab) + __popc(bc) + __popc(cd));
+    l0 = o0;
+    l1 = o1;
+    l2 = o2;
+    l3 = o3;
+    return s;
 }
 
 // Apply action a (0 up, 1 down, 2 left, 3 right) WITHOUT spawning; returns the merge gain.
 __device__ __forceinline__ uint32_t apply_move(Board& b, uint32_t act) {
-    const bool vert = act < 2u;
-    const uint32_t sel = (act & 1u) ? 0x00010203u : 0x03020100u;  // byte reverse or identity
-    Board t = transpose(b);
+    const bool horiz = act >= 2u, rev = (act & 1u) != 0u;
+    const Board t = transpose(b);
+    const uint32_t a0 = horiz ? t.r0 : b.r0, a1 = horiz ? t.r1 : b.r1;
+    const uint32_t a2 = horiz ? t.r2 : b.r2, a3 = horiz ? t.r3 : b.r3;
+    uint32_t l0 = rev ? a3 : a0, l1 = rev ? a2 : a1, l2 = rev ? a1 : a2, l3 = rev ? a0 : a3;
+    const uint32_t score = slide_lines(l0, l1, l2, l3);
     Board o;
-    o.r0 = vert ? t.r0 : b.r0;
-    o.r1 = vert ? t.r1 : b.r1;
-    o.r2 = vert ? t.r2 : b.r2;
-    o.r3 = vert ? t.r3 : b.r3;
-    uint32_t score = 0;
-    o.r0 = perm(0u, slide_row(perm(0u, o.r0, sel), score), sel);
-    o.r1 = perm(0u, slide_row(perm(0u, o.r1, sel), score), sel);
-    o.r2 = perm(0u, slide_row(perm(0u, o.r2, sel), score), sel);
-    o.r3 = perm(0u, slide_row(perm(0u, o.r3, sel), score), sel);
-    t = transpose(o);
-    b.r0 = vert ? t.r0 : o.r0;
-    b.r1 = vert ? t.r1 : o.r1;
-    b.r2 = vert ? t.r2 : o.r2;
-    b.r3 = vert ? t.r3 : o.r3;
+    o.r0 = rev ? l3 : l0;
+    o.r1 = rev ? l2 : l1;
+    o.r2 = rev ? l1 : l2;
+    o.r3 = rev ? l0 : l3;
+    const Board ot = transpose(o);
+    b = horiz ? ot : o;
     return score;
 }
 
-// Index of the k-th (0-based) set bit of a 16-bit mask (k < popcount(m)).
-__device__ __forceinline__ uint32_t kth_bit16(uint32_t m, uint32_t k) {
+// Index of the k-th (0-based) set bit of a 4-bit mask (k < popcount(m)).
+__device__ __forceinline__ uint32_t kth_bit4(uint32_t m, uint32_t k) {
     uint32_t pos = 0;
-    uint32_t c = __popc(m & 0xFFu);
-    if (k >= c) { k -= c; m >>= 8; pos += 8; }
-    c = __popc(m & 0xFu);
-    if (k >= c) { k -= c; m >>= 4; pos += 4; }
-    c = __popc(m & 0x3u);
-    if (k >= c) { k -= c; m >>= 2; pos += 2; }
-    c = m & 1u;
-    if (k >= c) { pos += 1; }
-    return pos;
+    const uint32_t c = __popc(m & 0x3u);
+    if (k >= c) { k -= c; m >>= 2; pos = 2; }
+    return pos + (k >= (m & 1u));
 }
 
 __device__ __forceinline__ void set_cell(Board& b, uint32_t pos, uint32_t e) {
@@ -153,15 +163,29 @@ __device__ __forceinline__ void set_cell(Board& b, uint32_t pos, uint32_t e) {
     b.r3 |= row == 3u ? v : 0u;
 }
 
-// One spawn (src/board.py:41-51): uniform empty cell in row-major order via
+__device__ __forceinline__ bool cell_empty(const Board& b, uint32_t pos) {
+    const uint32_t row = pos >> 2;
+    const uint32_t w = row == 0u ? b.r0 : row == 1u ? b.r1 : row == 2u ? b.r2 : b.r3;
+    return ((w >> ((pos & 3u) * 8u)) & 0xFFu) == 0u;
+}
+
+// One spawn (src/board.py:41-51): the k-th empty cell in row-major order with
 // k = floor(u_cell * n / 2^32); exponent 2 (a "4") iff u_val < p4_thresh.
 __device__ __forceinline__ void spawn(Board& b, uint32_t u_cell, uint32_t u_val,
                                       uint32_t p4_thresh) {
-    const uint32_t Z = empty_mask(b);
-    const uint32_t n = __popc(Z);
+    const uint32_t z0 = z80(b.r0), z1 = z80(b.r1), z2 = z80(b.r2), z3 = z80(b.r3);
+    const uint32_t p1 = __popc(z0), p2 = p1 + __popc(z1), p3 = p2 + __popc(z2);
+    const uint32_t n = p3 + __popc(z3);
     if (n == 0u) return;
-    const uint32_t k = __umulhi(u_cell, n);
-    set_cell(b, kth_bit16(Z, k), u_val < p4_thresh ? 2u : 1u);
+    uint32_t k = __umulhi(u_cell, n);
+    const uint32_t row = (uint32_t)(k >= p1) + (uint32_t)(k >= p2) + (uint32_t)(k >= p3);
+    uint32_t z = row == 0u ? z0 : row == 1u ? z1 : row == 2u ? z2 : z3;
+    k -= row == 0u ? 0u : row == 1u ? p1 : row == 2u ? p2 : p3;
+    uint32_t byte = 0;
+    const uint32_t c01 = __popc(z & 0x8080u);
+    if (k >= c01) { k -= c01; z >>= 16; byte = 2; }
+    byte += (uint32_t)(k >= ((z >> 7) & 1u));
+    set_cell(b, row * 4u + byte, u_val < p4_thresh ? 2u : 1u);
 }
 
 __device__ __forceinline__ uint32_t max_exp(const Board& b) {
@@ -190,7 +214,7 @@ __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-enum : uint32_t { DOMAIN_STEP = 0u, DOMAIN_AUTORESET = 1u, DOMAIN_RESET = 2u, DOMAIN_SAMPLE = 3u };
+enum : uint32_t { DOMAIN_STEP = 0u, DOMAIN_RESET = 2u, DOMAIN_SAMPLE = 3u };
 
 __device__ __forceinline__ uint4 draw(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
                                       uint32_t domain, uint64_t t) {
@@ -199,10 +223,17 @@ __device__ __forceinline__ uint4 draw(uint32_t seed_lo, uint32_t seed_hi, uint64
                     seed_lo, seed_hi);
 }
 
+// Two spawns on an empty board (src/board.py:18-20) from ONE Philox block: (u.z, u.w) for the
+// first, (u.z << 4, u.x << 2) for the second -- the words a terminal step leaves unused, so the
+// auto-reset reuses the step's own block.  With 16 empty cells the first is cell u.z >> 28; the
+// second is the k-th of the remaining 15.
 __device__ __forceinline__ Board fresh_board(uint4 u, uint32_t p4_thresh) {
+    const uint32_t ca = u.z >> 28;
+    const uint32_t k2 = __umulhi(u.z << 4, 15u);
+    const uint32_t cb = k2 + (uint32_t)(k2 >= ca);
     Board b{0u, 0u, 0u, 0u};
-    spawn(b, u.x, u.y, p4_thresh);
-    spawn(b, u.z, u.w, p4_thresh);
+    set_cell(b, ca, u.w < p4_thresh ? 2u : 1u);
+    set_cell(b, cb, (u.x << 2) < p4_thresh ? 2u : 1u);
     return b;
 }
 
