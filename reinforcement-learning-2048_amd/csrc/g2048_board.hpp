@@ -205,9 +205,11 @@ __device__ __forceinline__ uint32_t max_exp(const Board& b) {
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-        c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+        // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
+        const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
+        const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
+        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
+                       (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
