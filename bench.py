@@ -34,6 +34,22 @@ STEP_BYTES = 70
 ROLLOUT_BYTES = 38
 
 
+PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_step.json")
+
+
+def pmc_traffic(kernel: str, boards: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/gpu_pmc.sh:
+    separate FETCH_SIZE / WRITE_SIZE runs, FETCH_SIZE x2 gfx950 correction), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            rec = json.load(f).get(f"{kernel}@{boards}")
+    except (OSError, ValueError):
+        return None, None
+    if not rec:
+        return None, None
+    return rec["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, ROOT)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -260,6 +276,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
+    traffic, traffic_src = pmc_traffic("k_step", r["n"])
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -280,7 +297,8 @@ def main():
                        "parallelism": f"dp{world} (boards sharded, no collective)",
                        "launch": f"1 g2048_env_step per step, hipGraph of {r['G']} steps"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "k_step<MODE_RANDOM>",
                          "bytes_per_launch": STEP_BYTES * r["n"],
                          "launch_us_graph": per_step_s * 1e6,

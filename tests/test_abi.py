@@ -52,3 +52,14 @@ def test_no_cpu_fallback():
 def test_header_compiles_as_c():
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c", HEADER],
                    check=True)
+
+
+def test_c_caller_compiles_and_links(tmp_path):
+    """examples/abi_demo.c (a plain-C client) builds against the header and links libg2048.so."""
+    import g2048._native as N
+
+    libdir = os.path.dirname(N.LIB_PATH)
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "abi_demo.c"), "-L", libdir, "-l:libg2048.so",
+                    "-Wl,-rpath," + libdir, "-o", str(tmp_path / "abi_demo")], check=True)
+    assert (tmp_path / "abi_demo").exists()
