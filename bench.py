@@ -69,19 +69,30 @@ def parse():
     return p.parse_args()
 
 
+# RCCL ("nccl") in production; G2048_BENCH_BACKEND=gloo rehearses several ranks on one GPU
+BACKEND = os.environ.get("G2048_BENCH_BACKEND", "nccl")
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return world, rank, torch.device("cuda", local if world > 1 else 0)
+        torch.cuda.set_device(dev)
+        if BACKEND == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(BACKEND)
+    return world, rank, dev
 
 
 def barrier(world, dev):
     if world > 1:
-        dist.barrier(device_ids=[dev.index])
+        if BACKEND == "nccl":
+            dist.barrier(device_ids=[dev.index])
+        else:
+            dist.barrier()
 
 
 def max_over_ranks(x: float, world: int, dev) -> float:
