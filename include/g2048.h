@@ -140,6 +140,36 @@ G2048_API int g2048_replay_sample_encode(g2048_replay* rb, const int64_t* idx_de
                                void* s2_out, int64_t* a_out, void* r_out, void* d_out,
                                int64_t* idx_out, void* stream);
 
+/* ---- fused Q-network (learner fast path) -------------------------------------------------
+ * Forward of the reference conv Q-net (src/configs/double_dqn_conv.py:19-28) for n boards in
+ * one launch, fp32 on MFMA: Q[b] = net(log2 exponents of rows[idx ? idx[b] : b]).  Replaces
+ * board_as_4d_tensor / extract_samples_conv + model(state) (src/dqn_lib.py:8-9,23-24,126-130).
+ * Parameter pointers are device fp32 tensors in torch's layouts (Conv2d [out,in,kh,kw], Linear
+ * [out,in]); rows u8[*][16]; q_out f32[n][4]. */
+typedef struct {
+    const float *w1, *b1;       /* Conv2d(1, 64, 2)   */
+    const float *w2, *b2;       /* Conv2d(64, 64, 2)  */
+    const float *fc1_w, *fc1_b; /* Linear(256, 64)    */
+    const float *fc2_w, *fc2_b; /* Linear(64, 4)      */
+} g2048_convnet_params;
+
+G2048_API int g2048_convnet_forward(const g2048_convnet_params* params, const uint8_t* rows_dev,
+                                    const int64_t* idx_dev, int64_t n, float* q_out_dev,
+                                    void* stream);
+
+/* Gradient of the graded half of train_step (src/dqn_lib.py:146-161) for the conv net, fp32:
+ * q_b = Q(rows[idx[b]])[actions[idx[b]]], loss = sum_b (q_b - y_b)^2 (MSELoss(reduction='sum'))
+ * and d loss / d params written to grad_out (f32[33476], torch parameter order and layouts --
+ * the layout of a flat bucket of model.parameters()), loss to loss_out (f32 scalar, nullable).
+ * workspace: f32[g2048_convnet_train_workspace(batch)] device scratch (partial-gradient slabs;
+ * the final reduction is in a fixed order, so results are run-to-run deterministic). */
+G2048_API int64_t g2048_convnet_train_workspace(int64_t batch);
+G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* params,
+                                       const uint8_t* rows_dev, const uint8_t* actions_dev,
+                                       const int64_t* idx_dev, const float* y_dev, int64_t batch,
+                                       float* workspace_dev, float* grad_out_dev,
+                                       float* loss_out_dev, void* stream);
+
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);
 G2048_API int g2048_abi_version(void);

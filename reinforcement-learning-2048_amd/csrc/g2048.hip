@@ -22,6 +22,7 @@
 
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
+#include "g2048_common.hpp"
 
 using namespace g2048;
 
@@ -279,18 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_sample(SampleArgs S) {
 }
 
 // ------------------------------------------------------------------ host side
-thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof(buf), fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
+#define fail g2048_fail
 
 #define G_HIP(expr)                                                                        \
     do {                                                                                   \
@@ -314,6 +304,18 @@ struct DeviceGuard {
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
+
+thread_local std::string g_err;
+
+int g2048_fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
 
 struct g2048_env {
     int64_t n = 0;

@@ -40,9 +40,20 @@ SIGNATURES = {
     "g2048_replay_views": (_int, [_vp, _pp, _pp, _pp, _pp, _pp, _pp]),
     "g2048_replay_sample_encode": (_int, [_vp, _vp, _i64, _u64, _u64, _int, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
+    "g2048_convnet_forward": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "g2048_convnet_train_workspace": (_i64, [_i64]),
+    "g2048_convnet_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp]),
     "g2048_last_error": (C.c_char_p, []),
     "g2048_abi_version": (_int, []),
 }
+
+
+
+class ConvNetParams(C.Structure):
+    """g2048_convnet_params: device pointers of the conv Q-net's 8 fp32 tensors."""
+    _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2", "fc1_w", "fc1_b", "fc2_w",
+                                          "fc2_b")]
+
 
 _lib = None
 

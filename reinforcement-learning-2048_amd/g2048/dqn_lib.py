@@ -130,6 +130,18 @@ def bellman_targets(model, target_model, rewards, next_states, dones, discount_f
         return rewards.to(next_q.dtype) + disc.to(next_q.dtype) * next_q
 
 
+def targets_from_q(q_online_next, q_target_next, rewards, dones, discount_factor,
+                   use_double_dqn: bool = True) -> torch.Tensor:
+    """bellman_targets given precomputed Q_online(s') / Q_target(s') (same float32-gamma parity)."""
+    if use_double_dqn:
+        a_star = torch.argmax(q_online_next, dim=1)
+        next_q = q_target_next.gather(1, a_star[:, None])[:, 0]
+    else:
+        next_q = torch.max(q_target_next, dim=1).values
+    disc = (1 - dones).to(torch.float32) * torch.tensor(discount_factor, dtype=torch.float32)
+    return rewards.to(next_q.dtype) + disc.to(next_q.dtype) * next_q
+
+
 def dqn_loss(model, target_model, states, actions, rewards, next_states, dones, discount_factor,
              use_double_dqn: bool = True):
     """MSELoss(reduction='sum') of Q_online(s)[a] against the Bellman target (:146-158).

@@ -234,7 +234,8 @@ class ReplayBuffer:
         self.count.fill_(n)
 
     def sample_encode(self, batch_size: int, dtype=torch.float32, idx: torch.Tensor | None = None,
-                      seed: int = 0, epoch: int = 0, out=None):
+                      seed: int = 0, epoch: int = 0, out=None, want_s2: bool = True,
+                      want_s: bool = True):
         """sample_experiences (src/dqn_lib.py:67-84) with the encode of extract_samples_*
         (:33-64) fused: returns (states [B,16], actions i64 [B], rewards [B], next_states [B,16],
         dones [B], idx i64 [B]).  idx None = uniform with replacement over the filled rows."""
@@ -251,6 +252,10 @@ class ReplayBuffer:
                    torch.empty(B, dtype=dtype, **kw), torch.empty((B, 16), dtype=dtype, **kw),
                    torch.empty(B, dtype=dtype, **kw), torch.empty(B, dtype=torch.int64, **kw))
         s, a, r, s2, d, io = out
+        if not want_s2:
+            s2 = None
+        if not want_s:
+            s = None
         N.check(N.load().g2048_replay_sample_encode(
             self._h, N.ptr(idx), B, int(seed), int(epoch), N.F32 if dtype == torch.float32 else N.F64,
             N.ptr(s), N.ptr(s2), N.ptr(a), N.ptr(r), N.ptr(d), N.ptr(io),

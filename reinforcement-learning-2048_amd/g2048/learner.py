@@ -20,7 +20,8 @@ import torch
 from . import dqn_lib
 from .dist import FlatGradBucket, broadcast_params, world_size
 from .env import ReplayBuffer, VecEnv2048
-from .nets import NETS, make_net
+from .nets import NETS, Conv2048, make_net
+from . import qnet
 
 
 class DQNLearner:
@@ -58,18 +59,44 @@ class DQNLearner:
         self.last_loss = torch.zeros((), dtype=dtype, device=self.device)
         self._graphs = None
         self.graph = graph
+        # fused HIP forwards (csrc/g2048_qnet.hip) for the no-grad target nets of the conv net
+        self.fused = isinstance(self.model, Conv2048) and dtype == torch.float32
+        if self.fused:
+            self._p_on = qnet.conv_params(self.model)
+            self._p_tgt = qnet.conv_params(self.target)
+            # graded half (forward + MSE + backward) as one HIP launch + a slab reduction that
+            # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip)
+            self._train_grad = qnet.ConvTrainGrad(self.model, self.B)
 
     # -------------------------------------------------------------- one train_step, in pieces
     def _layout(self, s):
         return dqn_lib.extract_samples_conv(s) if self.conv_input else dqn_lib.extract_samples_dense(s)
 
+    def _sample_idx(self):
+        if self.sampler is not None:
+            return self.sampler(self.B, self.replay)
+        return (torch.rand(self.B, dtype=torch.float64, device=self.device)
+                * self.replay.count.to(torch.float64)).to(torch.int64)
+
     def _compute_grads(self):
         self.grad_flat.zero_()
-        idx = self.sampler(self.B, self.replay) if self.sampler is not None else None
-        s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
-                                                    self._layout, dtype=self.dtype, idx=idx)
-        loss, _, _ = dqn_lib.dqn_loss(self.model, self.target, s, a, r, s2, d, self.gamma,
-                                      self.use_double_dqn)
+        idx = self._sample_idx()
+        if self.fused:
+            # r, d for the targets; the two target-side forwards and the graded forward/backward
+            # read the ring rows directly through idx
+            _, _, r, _, d, _ = self.replay.sample_encode(self.B, self.dtype, idx=idx,
+                                                         want_s=False, want_s2=False)
+            q_on2 = qnet.conv_forward(self.model, self.replay.s2, idx, params=self._p_on)
+            q_tg2 = qnet.conv_forward(self.target, self.replay.s2, idx, params=self._p_tgt)
+            y = dqn_lib.targets_from_q(q_on2, q_tg2, r, d, self.gamma, self.use_double_dqn)
+            self._train_grad(self.replay.s, self.replay.a, idx, y.contiguous(), self.grad_flat,
+                             self.last_loss)
+            return
+        else:
+            s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
+                                                        self._layout, dtype=self.dtype, idx=idx)
+            loss, _, _ = dqn_lib.dqn_loss(self.model, self.target, s, a, r, s2, d, self.gamma,
+                                          self.use_double_dqn)
         loss.backward()
         self.last_loss.copy_(loss.detach())
 
@@ -134,6 +161,8 @@ class DQNLearner:
 
     @torch.no_grad()
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
+        if self.fused:
+            return qnet.conv_forward(self.model, env.board, params=self._p_on)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 
