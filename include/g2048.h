@@ -162,13 +162,33 @@ G2048_API int g2048_convnet_forward(const g2048_convnet_params* params, const ui
  * and d loss / d params written to grad_out (f32[33476], torch parameter order and layouts --
  * the layout of a flat bucket of model.parameters()), loss to loss_out (f32 scalar, nullable).
  * workspace: f32[g2048_convnet_train_workspace(batch)] device scratch (partial-gradient slabs;
- * the final reduction is in a fixed order, so results are run-to-run deterministic). */
+ * the final reduction is in a fixed order, so results are run-to-run deterministic).
+ * step_dev (u64, nullable) is incremented once: the update counter that g2048_convnet_targets
+ * (sampler epoch) and g2048_adam_step (bias correction) read -- graph-replay safe. */
 G2048_API int64_t g2048_convnet_train_workspace(int64_t batch);
 G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* params,
                                        const uint8_t* rows_dev, const uint8_t* actions_dev,
                                        const int64_t* idx_dev, const float* y_dev, int64_t batch,
                                        float* workspace_dev, float* grad_out_dev,
-                                       float* loss_out_dev, void* stream);
+                                       float* loss_out_dev, uint64_t* step_dev, void* stream);
+
+/* Double-DQN targets for a minibatch in one launch (src/dqn_lib.py:67-68,125-132): indices
+ * idx_out[b] = idx_in[b], or uniform over the ring's filled rows from Philox (seed, *epoch_dev)
+ * -- the same draw as g2048_replay_sample_encode's; then y[b] = r + ((1 - d) * float32(gamma)) *
+ * Q_target(s', argmax_a Q_online(s', a)) (vanilla DQN when double_dqn == 0: max_a Q_target). */
+G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,
+                                    const g2048_convnet_params* target, g2048_replay* rb,
+                                    const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                    const uint64_t* epoch_dev, float gamma, int double_dqn,
+                                    int64_t* idx_out_dev, float* y_out_dev, void* stream);
+
+/* One-launch Adam (torch.optim.Adam semantics, amsgrad off, no weight decay) over n_tensors
+ * (<= 16) fp32 parameter tensors whose gradients are packed back to back in grad_dev; exp_avg /
+ * exp_avg_sq are flat state buffers of the same length; the step t is read from *step_dev. */
+G2048_API int g2048_adam_step(float* const* params_dev, const int64_t* numels, int n_tensors,
+                              const float* grad_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
+                              const uint64_t* step_dev, double lr, double beta1, double beta2,
+                              double eps, void* stream);
 
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);

@@ -1,0 +1,84 @@
+// g2048_adam.hip -- one-launch Adam over a flat gradient bucket (the learner's optimizer step).
+//
+// Replaces torch.optim.Adam(model.parameters(), lr) .step() in the intended zero_grad ->
+// backward -> step order (src/configs/double_dqn_conv.py:39; the reference's own call order is a
+// no-op).  Same update as torch's single-tensor Adam (amsgrad off, no weight decay):
+//   m <- lerp(m, g, 1 - b1);  v <- v*b2 + (1 - b2)*g*g
+//   p <- p - (lr / (1 - b1^t)) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// with the bias corrections evaluated in double and rounded to f32 like torch's Python scalars,
+// and t read from the device update counter (bumped by the train-gradient launch), so the step
+// is graph-replay safe.  Parameters may be separate tensors; m and v are flat buffers.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/g2048.h"
+#include "g2048_common.hpp"
+
+namespace {
+
+constexpr int kMaxTensors = 16;
+
+struct AdamArgs {
+    float* p[kMaxTensors];
+    int64_t off[kMaxTensors + 1];
+    int nt;
+    const float* g;
+    float* m;
+    float* v;
+    const unsigned long long* step;
+    double lr, b1, b2, eps;
+};
+
+__global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.off[A.nt]) return;
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxTensors; ++j) k += (j < A.nt && i >= A.off[j]) ? 1 : 0;
+    float* p = A.p[k] + (i - A.off[k]);
+    const double t = (double)*A.step;
+    const float step_size = (float)(A.lr / (1.0 - pow(A.b1, t)));
+    const float bc2_sqrt = (float)sqrt(1.0 - pow(A.b2, t));
+    const float w1 = (float)(1.0 - A.b1), b2 = (float)A.b2, w2 = (float)(1.0 - A.b2);
+    const float eps = (float)A.eps;
+    const float g = A.g[i];
+    float m = A.m[i];
+    m = m + w1 * (g - m);                          // lerp(m, g, 1 - b1), weight < 0.5 branch
+    const float v = A.v[i] * b2 + w2 * g * g;      // mul_(b2).addcmul_(g, g, 1 - b2)
+    A.m[i] = m;
+    A.v[i] = v;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    *p = *p + (-step_size) * (m / denom);          // addcdiv_(m, denom, value=-step_size)
+}
+
+}  // namespace
+
+extern "C" G2048_API int g2048_adam_step(float* const* params, const int64_t* numels,
+                                         int n_tensors, const float* grad, float* exp_avg,
+                                         float* exp_avg_sq, const uint64_t* step_dev, double lr,
+                                         double beta1, double beta2, double eps, void* stream) {
+    if (!params || !numels || n_tensors <= 0 || n_tensors > kMaxTensors || !grad || !exp_avg ||
+        !exp_avg_sq || !step_dev)
+        return g2048_fail(G2048_EINVAL, "adam_step: bad arguments (n_tensors <= %d)", kMaxTensors);
+    AdamArgs A;
+    A.nt = n_tensors;
+    A.off[0] = 0;
+    for (int j = 0; j < kMaxTensors; ++j) {
+        A.p[j] = j < n_tensors ? params[j] : nullptr;
+        if (j < n_tensors) A.off[j + 1] = A.off[j] + numels[j];
+    }
+    for (int j = n_tensors + 1; j <= kMaxTensors; ++j) A.off[j] = A.off[n_tensors];
+    A.g = grad;
+    A.m = exp_avg;
+    A.v = exp_avg_sq;
+    A.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    A.lr = lr;
+    A.b1 = beta1;
+    A.b2 = beta2;
+    A.eps = eps;
+    const int64_t n = A.off[n_tensors];
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), A);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "adam_step: %s", hipGetErrorString(e));
+}

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "../../include/g2048.h"
+#include "g2048_board.hpp"
 #include "g2048_common.hpp"
 
 namespace {
@@ -61,8 +62,14 @@ struct ConvNetArgs {
     float* q;              // [n][4]
 };
 
-__global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+struct NetW {
+    const float *w1, *b1, *w2, *b2, *wf1, *bf1, *wf2, *bf2;
+};
+
+// Q-values of the S boards staged in lds[OFF_X] (exponents as floats) with net weights W;
+// writes qs[s*4 + a] (LDS).  Caller: __syncthreads() before (xs staged) -- this function ends
+// with one after qs is written.
+__device__ __forceinline__ void conv_forward_tile(const NetW& W, float* lds, float* qs) {
     float* xs = lds + OFF_X;
     float* sw1 = lds + OFF_SMALL;       // [c][4]
     float* sb1 = sw1 + 256;
@@ -78,38 +85,18 @@ __global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int wave = t >> 6;
-    const int64_t b0 = (int64_t)blockIdx.x * S;
 
-    // ---- stage boards (one u32 word = 4 exponents per thread: 32 boards x 4 words = 128 threads)
-    if (t < S * 4) {
-        const int s = t >> 2, w = t & 3;
-        const int64_t b = b0 + s;
-        uint32_t v = 0;
-        if (b < A.n) {
-            const int64_t row = A.idx ? A.idx[b] : b;
-            v = reinterpret_cast<const uint32_t*>(A.rows)[row * 4 + w];
-        }
-        float* dst = xs + s * 16 + w * 4;
-        dst[0] = (float)(v & 0xFFu);
-        dst[1] = (float)((v >> 8) & 0xFFu);
-        dst[2] = (float)((v >> 16) & 0xFFu);
-        dst[3] = (float)(v >> 24);
-    }
-    // ---- stage small weights
-    sw1[t] = A.w1[t];
+    // ---- stage small weights and W2 transposed: wt[k][n] = w2[n][k], k = c*4 + kh*2 + kw
+    sw1[t] = W.w1[t];
     if (t < 64) {
-        sb1[t] = A.b1[t];
-        sb2[t] = A.b2[t];
-        sbf1[t] = A.bf1[t];
+        sb1[t] = W.b1[t];
+        sb2[t] = W.b2[t];
+        sbf1[t] = W.bf1[t];
     }
-    swf2[(t >> 6) * 65 + (t & 63)] = A.wf2[t];
-    if (t < 4) sbf2[t] = A.bf2[t];
-    // ---- stage W2 transposed: wt[k][n] = w2[n][k], k = c*4 + kh*2 + kw (coalesced global reads)
+    swf2[(t >> 6) * 65 + (t & 63)] = W.wf2[t];
+    if (t < 4) sbf2[t] = W.bf2[t];
 #pragma unroll 4
-    for (int i = 0; i < 64; ++i) {
-        const int e = i * NT + t;  // n = e >> 8, k = e & 255
-        wt[(e & 255) * WT_STRIDE + (e >> 8)] = A.w2[e];
-    }
+    for (int i = 0; i < 64; ++i) wt[t * WT_STRIDE + i] = W.w2[i * NT + t];
     __syncthreads();
 
     // ---- conv1 -> h1 (VALU).  thread: channel c = lane, boards s = wave*8 .. wave*8+7
@@ -136,7 +123,7 @@ __global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
     // prefetch fc1 weights into registers (consumed after conv2): 64 per thread
     float pf[64];
 #pragma unroll
-    for (int i = 0; i < 64; ++i) pf[i] = A.wf1[i * NT + t];
+    for (int i = 0; i < 64; ++i) pf[i] = W.wf1[i * NT + t];
     __syncthreads();
 
     // ---- conv2 (MFMA 32x32x2): rows r = 32*wave + (lane&31): board s = r>>2, position q = r&3
@@ -210,11 +197,112 @@ __global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
     // ---- fc2 (VALU): thread t < 128 -> board s = t>>2, action a = t&3
     if (t < S * 4) {
         const int s = t >> 2, a = t & 3;
-        const int64_t b = b0 + s;
         float v = sbf2[a];
 #pragma unroll 16
         for (int j = 0; j < 64; ++j) v = fmaf(swf2[a * 65 + j], fa[s * F_STRIDE + j], v);
-        if (b < A.n) A.q[b * 4 + a] = v;
+        qs[t] = v;
+    }
+    __syncthreads();
+}
+
+// stage 32 boards (rows[idx[b]] or rows[b]) as float exponents into xs
+__device__ __forceinline__ void stage_boards(float* xs, const uint8_t* rows, const int64_t* idx,
+                                             int64_t b0, int64_t n) {
+    const int t = threadIdx.x;
+    if (t < S * 4) {
+        const int s = t >> 2, w = t & 3;
+        const int64_t b = b0 + s;
+        uint32_t v = 0;
+        if (b < n) {
+            const int64_t row = idx ? idx[b] : b;
+            v = reinterpret_cast<const uint32_t*>(rows)[row * 4 + w];
+        }
+        float* dst = xs + s * 16 + w * 4;
+        dst[0] = (float)(v & 0xFFu);
+        dst[1] = (float)((v >> 8) & 0xFFu);
+        dst[2] = (float)((v >> 16) & 0xFFu);
+        dst[3] = (float)(v >> 24);
+    }
+}
+
+__global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    __shared__ float qs[S * 4];
+    const int64_t b0 = (int64_t)blockIdx.x * S;
+    stage_boards(lds + OFF_X, A.rows, A.idx, b0, A.n);
+    __syncthreads();
+    conv_forward_tile(NetW{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2}, lds, qs);
+    const int t = threadIdx.x;
+    if (t < S * 4 && b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = qs[t];
+}
+
+// Double-DQN targets for a minibatch (src/dqn_lib.py:67-68,125-132), one launch:
+//   idx_b = uniform row of the ring (Philox, epoch = the learner's update counter) or idx_in,
+//   a*_b  = argmax_a Q_online(s'_b)  (first index on ties, torch.argmax),
+//   y_b   = r_b + ((1 - d_b) * float32(gamma)) * Q_target(s'_b, a*_b)   (vanilla: max_a Q_target)
+struct TargetArgs {
+    NetW on, tg;
+    const uint8_t* s2;
+    const int32_t* r;
+    const uint8_t* d;
+    const unsigned long long* count;
+    const unsigned long long* epoch;
+    const int64_t* idx_in;
+    int64_t batch;
+    uint32_t seed_lo, seed_hi;
+    float gamma;
+    int double_dqn;
+    int64_t* idx_out;
+    float* y;
+};
+
+__global__ __launch_bounds__(NT) void k_conv_targets(TargetArgs A) {
+    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
+    __shared__ float qon[S * 4], qtg[S * 4];
+    __shared__ int64_t sidx[S];
+    const int t = threadIdx.x;
+    const int64_t b0 = (int64_t)blockIdx.x * S;
+    if (t < S) {
+        const int64_t b = b0 + t;
+        int64_t j = 0;
+        if (b < A.batch) {
+            if (A.idx_in) {
+                j = A.idx_in[b];
+            } else {  // same draw as k_sample / o2048_replay_sample_f64 (domain 3)
+                const unsigned long long ep = *A.epoch;
+                const uint4 u = g2048::philox10(
+                    make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
+                               (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
+                    A.seed_lo, A.seed_hi);
+                const unsigned long long x = ((unsigned long long)u.y << 32) | u.x;
+                j = (int64_t)__umul64hi(x, *A.count);
+            }
+            A.idx_out[b] = j;
+        }
+        sidx[t] = j;
+    }
+    __syncthreads();
+    stage_boards(lds + OFF_X, A.s2, sidx, 0, S);  // rows of this tile (padding rows -> row 0)
+    __syncthreads();
+    conv_forward_tile(A.on, lds, qon);
+    conv_forward_tile(A.tg, lds, qtg);
+    if (t < S && b0 + t < A.batch) {
+#pragma clang fp contract(off)
+        const float* qo = qon + t * 4;
+        const float* qt = qtg + t * 4;
+        float next;
+        if (A.double_dqn) {
+            int a = 0;
+            float best = qo[0];
+            for (int k = 1; k < 4; ++k)
+                if (qo[k] > best) { best = qo[k]; a = k; }
+            next = qt[a];
+        } else {
+            next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+        }
+        const int64_t j = sidx[t];
+        const float disc = (float)(1 - (int)A.d[j]) * A.gamma;
+        A.y[b0 + t] = (float)A.r[j] + disc * next;
     }
 }
 
@@ -246,4 +334,43 @@ extern "C" G2048_API int g2048_convnet_forward(const g2048_convnet_params* p, co
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_forward: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,
+                                               const g2048_convnet_params* target,
+                                               g2048_replay* rb, const int64_t* idx_in,
+                                               int64_t batch, uint64_t seed,
+                                               const uint64_t* epoch_dev, float gamma,
+                                               int double_dqn, int64_t* idx_out, float* y_out,
+                                               void* stream) {
+    if (!online || !target || !rb || batch <= 0 || !idx_out || !y_out || (!idx_in && !epoch_dev))
+        return g2048_fail(G2048_EINVAL, "convnet_targets: NULL argument or batch <= 0");
+    uint8_t *s2 = nullptr, *d = nullptr;
+    int32_t* r = nullptr;
+    uint64_t* count = nullptr;
+    if (g2048_replay_views(rb, nullptr, &s2, nullptr, &r, &d, &count) != G2048_OK)
+        return G2048_EINVAL;
+    TargetArgs A;
+    A.on = NetW{online->w1, online->b1, online->w2, online->b2, online->fc1_w, online->fc1_b,
+                online->fc2_w, online->fc2_b};
+    A.tg = NetW{target->w1, target->b1, target->w2, target->b2, target->fc1_w, target->fc1_b,
+                target->fc2_w, target->fc2_b};
+    A.s2 = s2;
+    A.r = r;
+    A.d = d;
+    A.count = reinterpret_cast<const unsigned long long*>(count);
+    A.epoch = reinterpret_cast<const unsigned long long*>(epoch_dev);
+    A.idx_in = idx_in;
+    A.batch = batch;
+    A.seed_lo = (uint32_t)seed;
+    A.seed_hi = (uint32_t)(seed >> 32);
+    A.gamma = gamma;
+    A.double_dqn = double_dqn;
+    A.idx_out = idx_out;
+    A.y = y_out;
+    hipLaunchKernelGGL(k_conv_targets, dim3((unsigned)((batch + S - 1) / S)), dim3(NT), 0,
+                       reinterpret_cast<hipStream_t>(stream), A);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "convnet_targets: %s", hipGetErrorString(e));
 }

@@ -74,6 +74,7 @@ struct TrainArgs {
     const float* y;          // [B] Bellman targets
     int64_t batch;
     float* slab;             // [gridDim.x][SLAB]
+    unsigned long long* step;  // optional update counter, += 1 by one thread (nullable)
 };
 
 // conv1 pre-activation of board s (x in LDS) at output position (ph, pw), channel weights w/b
@@ -108,6 +109,9 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
 
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int half = lane >> 5, l32 = lane & 31;
+    // nothing else in this launch reads the counter; stream order makes the bump visible to the
+    // following optimizer launch and to the next update's sampler
+    if (A.step && blockIdx.x == 0 && t == 0) *A.step += 1ull;
 
     // small weights, once per workgroup
     sw1[t] = A.w1[t];
@@ -442,16 +446,36 @@ __device__ __forceinline__ int slab_to_param(int pos) {
     return P_BF2 + p3 - 704;
 }
 
+// Deterministic slab reduction: a block owns 64 slab positions; its 4 waves sum the slabs
+// g = wave, wave + 4, ... (8 independent loads in flight per lane), then the 4 partials are
+// added in a fixed order.  524 blocks keep enough loads in flight to stream the ~34 MB.
 __global__ __launch_bounds__(256) void k_reduce_slabs(const float* slab, int nslab, float* grad,
                                                       float* loss) {
-    const int pos = blockIdx.x * 256 + threadIdx.x;
-    if (pos > SL_LOSS) return;
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pos = blockIdx.x * 64 + lane;
     float v = 0.f;
-    for (int g = 0; g < nslab; ++g) v += slab[(int64_t)g * SLAB + pos];
-    if (pos == SL_LOSS) {
-        if (loss) *loss = v;
-    } else {
-        grad[slab_to_param(pos)] = v;
+    if (pos <= SL_LOSS) {
+        const float* p = slab + pos;
+        int g = wave;
+        for (; g + 28 < nslab; g += 32) {
+            float r[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) r[u] = p[(int64_t)(g + 4 * u) * SLAB];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v += r[u];
+        }
+        for (; g < nslab; g += 4) v += p[(int64_t)g * SLAB];
+    }
+    part[wave][lane] = v;
+    __syncthreads();
+    if (wave == 0 && pos <= SL_LOSS) {
+        const float s = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        if (pos == SL_LOSS) {
+            if (loss) *loss = s;
+        } else {
+            grad[slab_to_param(pos)] = s;
+        }
     }
 }
 
@@ -467,7 +491,8 @@ extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
                                                   const uint8_t* rows, const uint8_t* actions,
                                                   const int64_t* idx, const float* y, int64_t batch,
                                                   float* workspace, float* grad_out,
-                                                  float* loss_out, void* stream) {
+                                                  float* loss_out, uint64_t* step_dev,
+                                                  void* stream) {
     if (!p || !rows || !actions || !idx || !y || !workspace || !grad_out || batch <= 0)
         return g2048_fail(G2048_EINVAL, "convnet_train_grad: NULL argument or batch <= 0");
     TrainArgs A;
@@ -485,13 +510,14 @@ extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
     A.y = y;
     A.batch = batch;
     A.slab = workspace;
+    A.step = reinterpret_cast<unsigned long long*>(step_dev);
     const int64_t ntiles = (batch + S - 1) / S;
     const int grid = (int)(ntiles < 256 ? ntiles : 256);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_conv_train, dim3(grid), dim3(NT), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 256) / 256), dim3(256), 0, st, workspace,
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(256), 0, st, workspace,
                        grid, grad_out, loss_out);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK

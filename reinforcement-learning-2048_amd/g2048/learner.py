@@ -22,6 +22,7 @@ from .dist import FlatGradBucket, broadcast_params, world_size
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, Conv2048, make_net
 from . import qnet
+from .optim import FusedAdam
 
 
 class DQNLearner:
@@ -65,8 +66,15 @@ class DQNLearner:
             self._p_on = qnet.conv_params(self.model)
             self._p_tgt = qnet.conv_params(self.target)
             # graded half (forward + MSE + backward) as one HIP launch + a slab reduction that
-            # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip)
+            # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip); targets (sampler,
+            # both target-side forwards, Bellman) as one launch; Adam as one launch.  The device
+            # update counter is the sampler epoch and Adam's t (bumped by the train launch).
             self._train_grad = qnet.ConvTrainGrad(self.model, self.B)
+            self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
+            self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
+            self._adam = FusedAdam(params, lr=lr)
+            self.sample_seed = int(seed) * 0x9E3779B9 + 0x2048
 
     # -------------------------------------------------------------- one train_step, in pieces
     def _layout(self, s):
@@ -79,18 +87,16 @@ class DQNLearner:
                 * self.replay.count.to(torch.float64)).to(torch.int64)
 
     def _compute_grads(self):
-        self.grad_flat.zero_()
-        idx = self._sample_idx()
+        if not self.fused:
+            self.grad_flat.zero_()
+        idx = None if self.fused else self._sample_idx()
         if self.fused:
-            # r, d for the targets; the two target-side forwards and the graded forward/backward
-            # read the ring rows directly through idx
-            _, _, r, _, d, _ = self.replay.sample_encode(self.B, self.dtype, idx=idx,
-                                                         want_s=False, want_s2=False)
-            q_on2 = qnet.conv_forward(self.model, self.replay.s2, idx, params=self._p_on)
-            q_tg2 = qnet.conv_forward(self.target, self.replay.s2, idx, params=self._p_tgt)
-            y = dqn_lib.targets_from_q(q_on2, q_tg2, r, d, self.gamma, self.use_double_dqn)
-            self._train_grad(self.replay.s, self.replay.a, idx, y.contiguous(), self.grad_flat,
-                             self.last_loss)
+            idx_in = self.sampler(self.B, self.replay) if self.sampler is not None else None
+            qnet.conv_targets(self._p_on, self._p_tgt, self.replay, self.B, self._idx, self._y,
+                              self.gamma, self.use_double_dqn, self.sample_seed, self.step_dev,
+                              idx_in)
+            self._train_grad(self.replay.s, self.replay.a, self._idx, self._y, self.grad_flat,
+                             self.last_loss, self.step_dev)
             return
         else:
             s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
@@ -104,12 +110,16 @@ class DQNLearner:
         self.bucket.allreduce_mean_(self.pg)
 
     def _apply(self):
-        self.opt.step()
+        if self.fused:
+            self._adam.step(self.grad_flat, self.step_dev)
+        else:
+            self.opt.step()
 
     def _capture(self):
         # the warm-up below runs real updates; snapshot weights so capture leaves no trace
         params = list(self.model.parameters())
         snap = [p.detach().clone() for p in params]
+        step0 = self.step_dev.clone() if self.fused else None
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):  # warm-up (allocates Adam state, autograd buffers)
@@ -138,6 +148,9 @@ class DQNLearner:
                         v.zero_()
             self.grad_flat.zero_()
             self.last_loss.zero_()
+            if self.fused:
+                self._adam.reset_state()
+                self.step_dev.copy_(step0)
 
     def update(self) -> torch.Tensor:
         """One Double-DQN update (intended order zero_grad -> backward -> step). Returns the loss

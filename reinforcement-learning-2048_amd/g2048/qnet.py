@@ -55,12 +55,29 @@ class ConvTrainGrad:
         self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
 
     def __call__(self, rows: torch.Tensor, actions: torch.Tensor, idx: torch.Tensor,
-                 y: torch.Tensor, grad_out: torch.Tensor, loss_out: torch.Tensor | None = None):
+                 y: torch.Tensor, grad_out: torch.Tensor, loss_out: torch.Tensor | None = None,
+                 step: torch.Tensor | None = None):
         if idx.numel() != self.batch or y.numel() != self.batch:
             raise ValueError("idx / y must have `batch` elements")
         if y.dtype != torch.float32 or grad_out.dtype != torch.float32 or grad_out.numel() != 33476:
             raise ValueError("y and grad_out must be float32; grad_out has 33476 elements")
         N.check(N.load().g2048_convnet_train_grad(
             C.byref(self.params), N.ptr(rows), N.ptr(actions), N.ptr(idx), N.ptr(y), self.batch,
-            N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.stream_of(rows.device)),
+            N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(step),
+            N.stream_of(rows.device)),
             "g2048_convnet_train_grad")
+
+
+def conv_targets(online: N.ConvNetParams, target: N.ConvNetParams, replay, batch: int,
+                 idx_out: torch.Tensor, y_out: torch.Tensor, gamma: float = 0.8,
+                 double_dqn: bool = True, seed: int = 0, epoch: torch.Tensor | None = None,
+                 idx_in: torch.Tensor | None = None):
+    """Bellman targets y [B] (fp32) and the sampled ring indices in one launch
+    (g2048_convnet_targets); epoch is a device u64 counter (graph-safe sampler epoch)."""
+    if idx_in is None and epoch is None:
+        raise ValueError("need idx_in or a device epoch counter")
+    N.check(N.load().g2048_convnet_targets(
+        C.byref(online), C.byref(target), replay.handle, N.ptr(idx_in), int(batch), int(seed),
+        N.ptr(epoch), float(gamma), int(bool(double_dqn)), N.ptr(idx_out), N.ptr(y_out),
+        N.stream_of(y_out.device)), "g2048_convnet_targets")
+    return idx_out, y_out

@@ -109,3 +109,69 @@ def test_conv_train_grad_matches_autograd(G, B):
         g, r = grad[off:off + p.numel()].double(), ref[off:off + p.numel()]
         assert float((g - r).norm()) <= 1e-3 * float(r.norm()) + 1e-6, p.shape
         off += p.numel()
+
+
+def _filled_ring(G, seed, C=16384, n=4096):
+    env = G.VecEnv2048(n, device=DEV, seed=seed)
+    rb = G.ReplayBuffer(C, device=DEV)
+    env.rollout(C // n, replay=rb)
+    return rb
+
+
+@pytest.mark.parametrize("double_dqn", [True, False])
+def test_conv_targets_match_torch(G, double_dqn):
+    from g2048 import dqn_lib
+    from g2048.nets import make_net
+    from g2048.qnet import conv_forward, conv_params, conv_targets
+
+    rb = _filled_ring(G, 3)
+    torch.manual_seed(1)
+    on, tg = make_net("conv", torch.float32, DEV), make_net("conv", torch.float32, DEV)
+    B = 3000
+    idx = torch.randint(0, rb.capacity, (B,), device=DEV)
+    io = torch.empty(B, dtype=torch.int64, device=DEV)
+    y = torch.empty(B, dtype=torch.float32, device=DEV)
+    conv_targets(conv_params(on), conv_params(tg), rb, B, io, y, 0.8, double_dqn, idx_in=idx)
+    assert torch.equal(io, idx)
+    ref = dqn_lib.targets_from_q(conv_forward(on, rb.s2, idx), conv_forward(tg, rb.s2, idx),
+                                 rb.r[idx], rb.d[idx], 0.8, double_dqn)
+    torch.testing.assert_close(y, ref, rtol=1e-6, atol=1e-5)
+
+
+def test_conv_targets_sampler_matches_ring_sampler(G):
+    """In-kernel indices == g2048_replay_sample_encode's Philox draw for the same (seed, epoch)."""
+    from g2048.nets import make_net
+    from g2048.qnet import conv_params, conv_targets
+
+    rb = _filled_ring(G, 4)
+    m = make_net("conv", torch.float32, DEV)
+    B = 2048
+    epoch = torch.tensor([5], dtype=torch.int64, device=DEV)
+    io = torch.empty(B, dtype=torch.int64, device=DEV)
+    y = torch.empty(B, dtype=torch.float32, device=DEV)
+    conv_targets(conv_params(m), conv_params(m), rb, B, io, y, 0.8, True, seed=77, epoch=epoch)
+    ref_idx = rb.sample_encode(B, torch.float32, seed=77, epoch=5)[5]
+    assert torch.equal(io, ref_idx)
+    assert int(io.min()) >= 0 and int(io.max()) < rb.capacity
+
+
+def test_fused_adam_matches_torch_adam(G):
+    from g2048.nets import make_net
+    from g2048.optim import FusedAdam
+
+    torch.manual_seed(2)
+    m1 = make_net("conv", torch.float32, DEV)
+    m2 = make_net("conv", torch.float32, DEV)
+    m2.load_state_dict(m1.state_dict())
+    ref = torch.optim.Adam(m2.parameters(), lr=1e-2)
+    fa = FusedAdam(list(m1.parameters()), lr=1e-2)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    for it in range(5):
+        grads = [torch.randn_like(p) * (10.0 ** (it - 2)) for p in m1.parameters()]
+        for p, g in zip(m2.parameters(), grads):
+            p.grad = g.clone()
+        ref.step()
+        step += 1
+        fa.step(torch.cat([g.reshape(-1) for g in grads]), step)
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6)
