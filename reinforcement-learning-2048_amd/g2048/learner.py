@@ -74,7 +74,8 @@ class DQNLearner:
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
             self._adam = FusedAdam(params, lr=lr)
-            self.sample_seed = int(seed) * 0x9E3779B9 + 0x2048
+            rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
+            self.sample_seed = (int(seed) * 0x9E3779B9 + 0x2048 + (rank << 40)) & ((1 << 64) - 1)
 
     # -------------------------------------------------------------- one train_step, in pieces
     def _layout(self, s):
