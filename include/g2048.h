@@ -190,6 +190,27 @@ G2048_API int g2048_adam_step(float* const* params_dev, const int64_t* numels, i
                               const uint64_t* step_dev, double lr, double beta1, double beta2,
                               double eps, void* stream);
 
+/* ---- dense 16 -> 64 -> 4 Q-net (BASELINE configs[2]): the same four entry points ---------- */
+typedef struct {
+    const float *w1, *b1; /* Linear(16, 64) */
+    const float *w2, *b2; /* Linear(64, 4)  */
+} g2048_dense64_params;
+
+G2048_API int g2048_dense64_forward(const g2048_dense64_params* params, const uint8_t* rows_dev,
+                                    const int64_t* idx_dev, int64_t n, float* q_out_dev,
+                                    void* stream);
+G2048_API int g2048_dense64_targets(const g2048_dense64_params* online,
+                                    const g2048_dense64_params* target, g2048_replay* rb,
+                                    const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                    const uint64_t* epoch_dev, float gamma, int double_dqn,
+                                    int64_t* idx_out_dev, float* y_out_dev, void* stream);
+G2048_API int64_t g2048_dense64_train_workspace(int64_t batch);
+G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* params,
+                                       const uint8_t* rows_dev, const uint8_t* actions_dev,
+                                       const int64_t* idx_dev, const float* y_dev, int64_t batch,
+                                       float* workspace_dev, float* grad_out_dev,
+                                       float* loss_out_dev, uint64_t* step_dev, void* stream);
+
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);
 G2048_API int g2048_abi_version(void);

@@ -46,6 +46,11 @@ SIGNATURES = {
     "g2048_convnet_targets": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
                                      _vp, _vp]),
     "g2048_adam_step": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+    "g2048_dense64_forward": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "g2048_dense64_targets": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
+                                     _vp, _vp]),
+    "g2048_dense64_train_workspace": (_i64, [_i64]),
+    "g2048_dense64_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "g2048_last_error": (C.c_char_p, []),
     "g2048_abi_version": (_int, []),
 }
@@ -56,6 +61,13 @@ class ConvNetParams(C.Structure):
     """g2048_convnet_params: device pointers of the conv Q-net's 8 fp32 tensors."""
     _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2", "fc1_w", "fc1_b", "fc2_w",
                                           "fc2_b")]
+
+
+
+
+class Dense64Params(C.Structure):
+    """g2048_dense64_params: device pointers of the dense 16-64-4 Q-net's 4 fp32 tensors."""
+    _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2")]
 
 
 _lib = None

@@ -20,7 +20,7 @@ import torch
 from . import dqn_lib
 from .dist import FlatGradBucket, broadcast_params, world_size
 from .env import ReplayBuffer, VecEnv2048
-from .nets import NETS, Conv2048, make_net
+from .nets import NETS, make_net
 from . import qnet
 from .optim import FusedAdam
 
@@ -60,16 +60,18 @@ class DQNLearner:
         self.last_loss = torch.zeros((), dtype=dtype, device=self.device)
         self._graphs = None
         self.graph = graph
-        # fused HIP forwards (csrc/g2048_qnet.hip) for the no-grad target nets of the conv net
-        self.fused = isinstance(self.model, Conv2048) and dtype == torch.float32
+        # fused HIP kernels (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip) for the fp32
+        # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
+        self.kind = qnet.kind_of(self.model)
+        self.fused = self.kind is not None
         if self.fused:
-            self._p_on = qnet.conv_params(self.model)
-            self._p_tgt = qnet.conv_params(self.target)
+            self._p_on = qnet.net_params(self.model)
+            self._p_tgt = qnet.net_params(self.target)
             # graded half (forward + MSE + backward) as one HIP launch + a slab reduction that
             # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip); targets (sampler,
             # both target-side forwards, Bellman) as one launch; Adam as one launch.  The device
             # update counter is the sampler epoch and Adam's t (bumped by the train launch).
-            self._train_grad = qnet.ConvTrainGrad(self.model, self.B)
+            self._train_grad = qnet.TrainGrad(self.model, self.B)
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
@@ -93,9 +95,9 @@ class DQNLearner:
         idx = None if self.fused else self._sample_idx()
         if self.fused:
             idx_in = self.sampler(self.B, self.replay) if self.sampler is not None else None
-            qnet.conv_targets(self._p_on, self._p_tgt, self.replay, self.B, self._idx, self._y,
-                              self.gamma, self.use_double_dqn, self.sample_seed, self.step_dev,
-                              idx_in)
+            qnet.targets(self.kind, self._p_on, self._p_tgt, self.replay, self.B, self._idx,
+                         self._y, self.gamma, self.use_double_dqn, self.sample_seed, self.step_dev,
+                         idx_in)
             self._train_grad(self.replay.s, self.replay.a, self._idx, self._y, self.grad_flat,
                              self.last_loss, self.step_dev)
             return
@@ -176,7 +178,7 @@ class DQNLearner:
     @torch.no_grad()
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
         if self.fused:
-            return qnet.conv_forward(self.model, env.board, params=self._p_on)
+            return qnet.forward(self.model, env.board, params=self._p_on)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 

@@ -1,33 +1,79 @@
-"""Fused Q-network kernels (csrc/g2048_qnet.hip) behind the C ABI.
+"""Fused Q-network kernels behind the C ABI (csrc/g2048_qnet.hip, g2048_qtrain.hip,
+g2048_mlp.hip), for the two fp32 fast-path nets:
 
-conv_forward(model, rows, idx) == model(board_as_4d_tensor(rows[idx])) for the reference conv
-net (src/configs/double_dqn_conv.py:19-28) in fp32, as ONE launch that reads the u8 boards
-(optionally through replay indices) and writes Q [n, 4]."""
+  conv     src/configs/double_dqn_conv.py:19-28   (g2048.nets.Conv2048)
+  dense64  BASELINE.json configs[2]: 16 -> 64 -> 4 (nn.Sequential(Linear, ReLU, Linear))
+
+forward(model, rows, idx)   == model(board_as_*_tensor(rows[idx]))        one launch
+targets(...)                == sampler + Q_online(s') + Q_target(s') + Bellman target, one launch
+TrainGrad(model, B)(...)    == d/dtheta sum_b (Q(s_b)[a_b] - y_b)^2 into a flat bucket, 2 launches
+"""
 from __future__ import annotations
 
 import ctypes as C
 
 import torch
+from torch import nn
 
 from . import _native as N
 from .nets import Conv2048
 
-_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias", "5.weight", "5.bias", "7.weight", "7.bias")
+_CONV_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias", "5.weight", "5.bias", "7.weight",
+               "7.bias")
+_DENSE_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias")
+
+
+def is_dense64(model) -> bool:
+    return (isinstance(model, nn.Sequential) and len(model) == 3
+            and isinstance(model[0], nn.Linear) and model[0].in_features == 16
+            and model[0].out_features == 64 and isinstance(model[1], nn.ReLU)
+            and isinstance(model[2], nn.Linear) and model[2].in_features == 64
+            and model[2].out_features == 4)
+
+
+def kind_of(model) -> str | None:
+    """'conv' / 'dense64' when a fused fp32 kernel exists for this model, else None."""
+    if next(model.parameters()).dtype != torch.float32:
+        return None
+    if isinstance(model, Conv2048):
+        return "conv"
+    if is_dense64(model):
+        return "dense64"
+    return None
+
+
+def _tensors(model, order):
+    sd = dict(model.named_parameters())
+    ts = [sd[k] for k in order]
+    for t in ts:
+        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
+            raise ValueError("fused Q-net kernels run fp32 contiguous CUDA parameters")
+    return ts
+
+
+def net_params(model):
+    """ctypes parameter struct (device pointers) for the model's fused kernels."""
+    k = kind_of(model)
+    if k == "conv":
+        return N.ConvNetParams(*[t.data_ptr() for t in _tensors(model, _CONV_ORDER)])
+    if k == "dense64":
+        return N.Dense64Params(*[t.data_ptr() for t in _tensors(model, _DENSE_ORDER)])
+    raise TypeError("no fused kernel for this model (fp32 Conv2048 or dense 16-64-4 only)")
+
+
+def _sym(model_or_kind, what):
+    k = model_or_kind if isinstance(model_or_kind, str) else kind_of(model_or_kind)
+    return getattr(N.load(), f"g2048_{'convnet' if k == 'conv' else 'dense64'}_{what}")
 
 
 def conv_params(model: Conv2048) -> N.ConvNetParams:
     if not isinstance(model, Conv2048):
-        raise TypeError("conv_forward needs the reference conv net (g2048.nets.Conv2048)")
-    sd = dict(model.named_parameters())
-    ts = [sd[k] for k in _ORDER]
-    for t in ts:
-        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
-            raise ValueError("fused conv net runs fp32 contiguous CUDA parameters")
-    return N.ConvNetParams(*[t.data_ptr() for t in ts])
+        raise TypeError("conv_params needs the reference conv net (g2048.nets.Conv2048)")
+    return net_params(model)
 
 
-def conv_forward(model: Conv2048, rows: torch.Tensor, idx: torch.Tensor | None = None,
-                 out: torch.Tensor | None = None, params: N.ConvNetParams | None = None):
+def forward(model, rows: torch.Tensor, idx: torch.Tensor | None = None,
+            out: torch.Tensor | None = None, params=None):
     """Q-values [n, 4] (fp32) of boards rows[idx] (or rows) -- no autograd."""
     if rows.dtype != torch.uint8 or rows.dim() != 2 or rows.shape[1] != 16 or not rows.is_contiguous():
         raise ValueError("rows must be a contiguous uint8 [*, 16] board tensor")
@@ -36,22 +82,27 @@ def conv_forward(model: Conv2048, rows: torch.Tensor, idx: torch.Tensor | None =
         raise ValueError("idx must be contiguous int64")
     if out is None:
         out = torch.empty((n, 4), dtype=torch.float32, device=rows.device)
-    p = params if params is not None else conv_params(model)
-    N.check(N.load().g2048_convnet_forward(C.byref(p), N.ptr(rows), N.ptr(idx), n, N.ptr(out),
-                                           N.stream_of(rows.device)), "g2048_convnet_forward")
+    p = params if params is not None else net_params(model)
+    N.check(_sym(model, "forward")(C.byref(p), N.ptr(rows), N.ptr(idx), n, N.ptr(out),
+                                   N.stream_of(rows.device)), "fused forward")
     return out
 
 
-class ConvTrainGrad:
-    """Fused graded half of train_step for the conv net (csrc/g2048_qtrain.hip): writes the loss
-    and the gradient of sum_b (Q(s_b)[a_b] - y_b)^2 into a flat fp32 buffer laid out like
+conv_forward = forward
+
+
+class TrainGrad:
+    """Graded half of train_step for a fused net: writes the loss and the gradient of
+    sum_b (Q(s_b)[a_b] - y_b)^2 into a flat fp32 buffer laid out like
     torch.cat([p.reshape(-1) for p in model.parameters()])."""
 
-    def __init__(self, model: Conv2048, batch: int):
-        self.params = conv_params(model)
+    def __init__(self, model, batch: int):
+        self.kind = kind_of(model)
+        self.params = net_params(model)
         self.batch = int(batch)
+        self.n_params = sum(p.numel() for p in model.parameters())
         dev = next(model.parameters()).device
-        n = N.load().g2048_convnet_train_workspace(self.batch)
+        n = _sym(self.kind, "train_workspace")(self.batch)
         self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
 
     def __call__(self, rows: torch.Tensor, actions: torch.Tensor, idx: torch.Tensor,
@@ -59,25 +110,33 @@ class ConvTrainGrad:
                  step: torch.Tensor | None = None):
         if idx.numel() != self.batch or y.numel() != self.batch:
             raise ValueError("idx / y must have `batch` elements")
-        if y.dtype != torch.float32 or grad_out.dtype != torch.float32 or grad_out.numel() != 33476:
-            raise ValueError("y and grad_out must be float32; grad_out has 33476 elements")
-        N.check(N.load().g2048_convnet_train_grad(
+        if (y.dtype != torch.float32 or grad_out.dtype != torch.float32
+                or grad_out.numel() != self.n_params):
+            raise ValueError(f"y and grad_out must be float32; grad_out has {self.n_params} elements")
+        N.check(_sym(self.kind, "train_grad")(
             C.byref(self.params), N.ptr(rows), N.ptr(actions), N.ptr(idx), N.ptr(y), self.batch,
             N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(step),
-            N.stream_of(rows.device)),
-            "g2048_convnet_train_grad")
+            N.stream_of(rows.device)), "fused train_grad")
 
 
-def conv_targets(online: N.ConvNetParams, target: N.ConvNetParams, replay, batch: int,
-                 idx_out: torch.Tensor, y_out: torch.Tensor, gamma: float = 0.8,
-                 double_dqn: bool = True, seed: int = 0, epoch: torch.Tensor | None = None,
-                 idx_in: torch.Tensor | None = None):
-    """Bellman targets y [B] (fp32) and the sampled ring indices in one launch
-    (g2048_convnet_targets); epoch is a device u64 counter (graph-safe sampler epoch)."""
+ConvTrainGrad = TrainGrad
+
+
+def targets(kind: str, online, target, replay, batch: int, idx_out: torch.Tensor,
+            y_out: torch.Tensor, gamma: float = 0.8, double_dqn: bool = True, seed: int = 0,
+            epoch: torch.Tensor | None = None, idx_in: torch.Tensor | None = None):
+    """Bellman targets y [B] (fp32) and the sampled ring indices in one launch; epoch is a device
+    u64 counter (graph-safe sampler epoch).  online/target: net_params() structs."""
     if idx_in is None and epoch is None:
         raise ValueError("need idx_in or a device epoch counter")
-    N.check(N.load().g2048_convnet_targets(
+    N.check(_sym(kind, "targets")(
         C.byref(online), C.byref(target), replay.handle, N.ptr(idx_in), int(batch), int(seed),
         N.ptr(epoch), float(gamma), int(bool(double_dqn)), N.ptr(idx_out), N.ptr(y_out),
-        N.stream_of(y_out.device)), "g2048_convnet_targets")
+        N.stream_of(y_out.device)), "fused targets")
     return idx_out, y_out
+
+
+def conv_targets(online, target, replay, batch, idx_out, y_out, gamma=0.8, double_dqn=True,
+                 seed=0, epoch=None, idx_in=None):
+    return targets("conv", online, target, replay, batch, idx_out, y_out, gamma, double_dqn,
+                   seed, epoch, idx_in)

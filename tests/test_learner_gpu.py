@@ -141,3 +141,27 @@ def test_play_one_step_mirror(G):
     # greedy actions must be the compat argmax of the model's Q on the boards before the step
     env3, a3, r3, d3, _ = dqn_lib.play_one_step(G.VecEnv2048(n, device=DEV, seed=8), 1.0, None, rb)
     assert a3.max() <= 3
+
+
+@pytest.mark.parametrize("net", ["dense64", "conv"])
+def test_fused_graphed_learner_equals_eager(G, net):
+    """fp32 fused path (targets + train-grad + reduce + FusedAdam): the captured hipGraph update
+    reproduces the eager one -- checks the capture warm-up leaves no trace (weights, Adam state,
+    device update counter) and that the sampler epoch advances per replay."""
+    from g2048.learner import DQNLearner
+
+    n, C = 2048, 16 * 2048
+    env = G.VecEnv2048(n, device=DEV, seed=31)
+    rb = G.ReplayBuffer(C, device=DEV)
+    env.rollout(C // n, replay=rb)
+    outs = []
+    for graph in (True, False):
+        L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=1024, graph=graph, seed=9,
+                       target_sync_every=3)
+        assert L.fused
+        losses = [float(L.update()) for _ in range(7)]
+        outs.append((losses, torch.cat([p.detach().reshape(-1) for p in L.model.parameters()]),
+                     int(L.step_dev)))
+    assert outs[0][2] == outs[1][2] == 7
+    np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-7)

@@ -175,3 +175,53 @@ def test_fused_adam_matches_torch_adam(G):
         fa.step(torch.cat([g.reshape(-1) for g in grads]), step)
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6)
+
+
+# ------------------------------------------------------------------ dense 16-64-4 (configs[2])
+def test_dense64_forward_and_targets(G):
+    from g2048 import dqn_lib
+    from g2048.nets import make_net
+    from g2048.qnet import forward, net_params, targets
+
+    rb = _filled_ring(G, 9)
+    torch.manual_seed(3)
+    on, tg = make_net("dense64", torch.float32, DEV), make_net("dense64", torch.float32, DEV)
+    idx = torch.randint(0, rb.capacity, (5000,), device=DEV)
+    q = forward(on, rb.s2, idx)
+    with torch.no_grad():
+        ref = on(rb.s2[idx].float())
+    torch.testing.assert_close(q, ref, rtol=2e-5, atol=2e-5 * float(ref.abs().max()))
+    io = torch.empty(5000, dtype=torch.int64, device=DEV)
+    y = torch.empty(5000, dtype=torch.float32, device=DEV)
+    targets("dense64", net_params(on), net_params(tg), rb, 5000, io, y, 0.8, True, idx_in=idx)
+    ref_y = dqn_lib.targets_from_q(forward(on, rb.s2, idx), forward(tg, rb.s2, idx), rb.r[idx],
+                                   rb.d[idx], 0.8, True)
+    torch.testing.assert_close(y, ref_y, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("B", [64, 1000, 20000])
+def test_dense64_train_grad_matches_autograd(G, B):
+    from g2048.nets import make_net
+    from g2048.qnet import TrainGrad
+
+    rb = _filled_ring(G, B)
+    torch.manual_seed(B)
+    m = make_net("dense64", torch.float32, DEV)
+    idx = torch.randint(0, rb.capacity, (B,), device=DEV)
+    y = (torch.randn(B, device=DEV) * 20 + 30).float()
+    grad = torch.full((1348,), float("nan"), device=DEV)
+    loss = torch.zeros((), device=DEV)
+    TrainGrad(m, B)(rb.s, rb.a, idx, y, grad, loss)
+    m64 = make_net("dense64", torch.float64, DEV)
+    m64.load_state_dict({k: v.double() for k, v in m.state_dict().items()})
+    ref_loss = ((m64(rb.s[idx].double()).gather(1, rb.a[idx].long()[:, None])[:, 0]
+                 - y.double()) ** 2).sum()
+    ref_loss.backward()
+    ref = torch.cat([p.grad.reshape(-1) for p in m64.parameters()])
+    assert torch.isfinite(grad).all()
+    assert float(loss) == pytest.approx(float(ref_loss.detach()), rel=1e-5)
+    off = 0
+    for p in m64.parameters():
+        g, r = grad[off:off + p.numel()].double(), ref[off:off + p.numel()]
+        assert float((g - r).norm()) <= 1e-4 * float(r.norm()) + 1e-6, p.shape
+        off += p.numel()
