@@ -103,6 +103,14 @@ G2048_API int g2048_env_step_egreedy(g2048_env* env, const void* q_dev, int q_dt
                            double eps, int32_t* reward_dev, uint8_t* done_dev,
                            uint8_t* action_dev, g2048_replay* rb, void* stream);
 
+/* The same with the reference's per-episode schedule applied per board (src/dqn_lib.py:184-188):
+ * eps_b = max((eps_decay_episodes - episodes_b) / eps_decay_episodes, eps_min), episodes_b = the
+ * board's finished-episode count (ep[i][0]); graph-safe, no host input per step. */
+G2048_API int g2048_env_step_egreedy_schedule(g2048_env* env, const void* q_dev, int q_dtype,
+                                              double eps_decay_episodes, double eps_min,
+                                              int32_t* reward_dev, uint8_t* done_dev,
+                                              uint8_t* action_dev, g2048_replay* rb, void* stream);
+
 /* Test entry: actions + injected spawns (cell index -1..15, exponent) instead of Philox draws,
  * so trajectories recorded from the reference replay bit-for-bit. */
 G2048_API int g2048_env_step_inject(g2048_env* env, const uint8_t* actions_dev, const int8_t* spawn_idx_dev,

@@ -58,8 +58,8 @@ def lib():
         L.o2048_env_reset.restype = None
         L.o2048_env_reset.argtypes = [C.POINTER(_Env), vp, C.c_uint32]
         L.o2048_env_step.restype = C.c_int64
-        L.o2048_env_step.argtypes = [C.POINTER(_Env), C.c_int, vp, vp, C.c_double, vp, vp,
-                                     vp, vp, vp, vp, C.POINTER(_Replay)]
+        L.o2048_env_step.argtypes = [C.POINTER(_Env), C.c_int, vp, vp, C.c_double, C.c_double,
+                                     C.c_double, vp, vp, vp, vp, vp, vp, C.POINTER(_Replay)]
         L.o2048_replay_sample_f64.restype = None
         L.o2048_replay_sample_f64.argtypes = [C.POINTER(_Replay), vp, C.c_int64, C.c_uint64,
                                               C.c_uint64, vp, vp, vp, vp, vp, vp]
@@ -150,7 +150,7 @@ class OracleEnv:
         self.epoch += 1
 
     def step(self, mode=MODE_RANDOM, actions=None, q=None, eps=0.0, spawn_idx=None,
-             spawn_exp=None, replay: OracleReplay | None = None):
+             spawn_exp=None, replay: OracleReplay | None = None, eps_schedule=None):
         n = self.n
         reward = np.zeros(n, np.int32)
         done = np.zeros(n, np.uint8)
@@ -163,7 +163,9 @@ class OracleEnv:
         if spawn_idx is not None:
             spawn_idx = np.ascontiguousarray(spawn_idx, dtype=np.int8)
             spawn_exp = np.ascontiguousarray(spawn_exp, dtype=np.uint8)
+        dec, mn = eps_schedule if eps_schedule is not None else (0.0, 0.0)
         bad = lib().o2048_env_step(C.byref(self._c), mode, _p(actions), _p(q), float(eps),
+                                   float(dec), float(mn),
                                    _p(spawn_idx), _p(spawn_exp), _p(reward), _p(done),
                                    _p(legal), _p(act),
                                    C.byref(replay._c) if replay is not None else None)

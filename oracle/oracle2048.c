@@ -200,6 +200,7 @@ void o2048_env_reset(o2048_env* e, const uint8_t* mask, uint32_t epoch) {
 
 /* One transition per board: the contract of include/g2048.h g2048_env_step*. */
 int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const void* q, double eps,
+                       double eps_decay, double eps_min,
                        const int8_t* spawn_idx, const uint8_t* spawn_exp,
                        int32_t* reward, uint8_t* done_out, uint8_t* legal_out,
                        uint8_t* action_out, o2048_replay* rb) {
@@ -222,7 +223,13 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
         } else if (mode == 1) {
             a = (int)(u[0] >> 30);
         } else {
-            const int explore = (double)u[1] * (1.0 / 4294967296.0) < eps;  /* dqn_lib.py:20 */
+            double eps_i = eps;
+            if (eps_decay > 0) {  /* dqn_lib.py:184-188, ep = this board's episode count */
+                const double ep_i = (double)e->ep[4 * i];
+                eps_i = (eps_decay - ep_i) / eps_decay;
+                if (eps_i < eps_min) eps_i = eps_min;
+            }
+            const int explore = (double)u[1] * (1.0 / 4294967296.0) < eps_i;  /* dqn_lib.py:20 */
             if (explore) {
                 int nl = 0;
                 for (int j = 0; j < 4; ++j) nl += (legal >> j) & 1;

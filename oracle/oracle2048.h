@@ -60,6 +60,7 @@ typedef struct {
 void o2048_env_reset(o2048_env* e, const uint8_t* mask_or_null, uint32_t epoch);
 /* returns number of invalid inputs seen (bad action / occupied injected cell) */
 int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const void* q, double eps,
+                       double eps_decay, double eps_min,
                        const int8_t* spawn_idx, const uint8_t* spawn_exp,
                        int32_t* reward, uint8_t* done, uint8_t* legal_out,
                        uint8_t* action_out, o2048_replay* rb);

@@ -55,6 +55,8 @@ struct StepArgs {
     const void* q;
     const double* eps_dev;
     double eps;
+    double eps_decay;  // > 0: per-board schedule eps_b = max((D - episodes_b) / D, eps_min)
+    double eps_min;
     const int8_t* spawn_idx;
     const uint8_t* spawn_exp;
     int32_t* reward;
@@ -162,7 +164,14 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
     double eps = 0.0;
-    if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) eps = A.eps_dev ? *A.eps_dev : A.eps;
+    if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
+        if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board: ep = its episode count
+            const double e = (double)reinterpret_cast<const uint32_t*>(A.ep)[4 * i];
+            eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
+        } else {
+            eps = A.eps_dev ? *A.eps_dev : A.eps;
+        }
+    }
     int32_t rew;
     uint32_t done, legal, act;
     step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, rew, done, legal, act);
@@ -404,6 +413,11 @@ int launch_step(g2048_env* e, const StepArgs& A, void* stream) {
 }  // namespace
 
 // ------------------------------------------------------------------ extern "C" ABI
+static int g2048_env_step_egreedy_impl(g2048_env* e, const void* q, int q_dtype,
+                                       const double* eps_dev, double eps, double eps_decay,
+                                       double eps_min, int32_t* reward, uint8_t* done,
+                                       uint8_t* action_out, g2048_replay* rb, void* stream);
+
 extern "C" {
 
 const char* g2048_last_error(void) { return g_err.c_str(); }
@@ -522,9 +536,27 @@ int g2048_env_step(g2048_env* e, const uint8_t* actions, int32_t* reward, uint8_
     return actions ? launch_step<MODE_ACTIONS>(e, A, stream) : launch_step<MODE_RANDOM>(e, A, stream);
 }
 
+int g2048_env_step_egreedy_schedule(g2048_env* e, const void* q, int q_dtype,
+                                    double eps_decay_episodes, double eps_min, int32_t* reward,
+                                    uint8_t* done, uint8_t* action_out, g2048_replay* rb,
+                                    void* stream) {
+    if (!(eps_decay_episodes > 0.0))
+        return fail(G2048_EINVAL, "env_step_egreedy_schedule: eps_decay_episodes must be > 0");
+    return g2048_env_step_egreedy_impl(e, q, q_dtype, nullptr, 0.0, eps_decay_episodes, eps_min,
+                                       reward, done, action_out, rb, stream);
+}
+
 int g2048_env_step_egreedy(g2048_env* e, const void* q, int q_dtype, const double* eps_dev,
                            double eps, int32_t* reward, uint8_t* done, uint8_t* action_out,
                            g2048_replay* rb, void* stream) {
+    return g2048_env_step_egreedy_impl(e, q, q_dtype, eps_dev, eps, 0.0, 0.0, reward, done,
+                                       action_out, rb, stream);
+}
+
+static int g2048_env_step_egreedy_impl(g2048_env* e, const void* q, int q_dtype,
+                                       const double* eps_dev, double eps, double eps_decay,
+                                       double eps_min, int32_t* reward, uint8_t* done,
+                                       uint8_t* action_out, g2048_replay* rb, void* stream) {
     if (!e || !q) return fail(G2048_EINVAL, "env_step_egreedy: NULL env or q");
     if (q_dtype != G2048_F32 && q_dtype != G2048_F64)
         return fail(G2048_EINVAL, "env_step_egreedy: q_dtype %d", q_dtype);
@@ -535,6 +567,8 @@ int g2048_env_step_egreedy(g2048_env* e, const void* q, int q_dtype, const doubl
     A.q = q;
     A.eps_dev = eps_dev;
     A.eps = eps;
+    A.eps_decay = eps_decay;
+    A.eps_min = eps_min;
     A.reward = reward;
     A.done = done;
     A.action_out = action_out;

@@ -31,6 +31,8 @@ SIGNATURES = {
     "g2048_env_reset": (_int, [_vp, _vp, _vp]),
     "g2048_env_step": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "g2048_env_step_egreedy": (_int, [_vp, _vp, _int, _vp, _dbl, _vp, _vp, _vp, _vp, _vp]),
+    "g2048_env_step_egreedy_schedule": (_int, [_vp, _vp, _int, _dbl, _dbl, _vp, _vp, _vp, _vp,
+                                               _vp]),
     "g2048_env_step_inject": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "g2048_env_rollout": (_int, [_vp, _i32, _vp, _vp, _vp]),
     "g2048_env_error_count": (_int, [_vp, C.POINTER(C.c_int64), _vp]),

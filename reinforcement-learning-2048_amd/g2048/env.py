@@ -89,16 +89,20 @@ class VecEnv2048:
         return reward, done, legal
 
     def step_egreedy(self, q: torch.Tensor, epsilon, replay: "ReplayBuffer | None" = None,
-                     reward=None, done=None, action=None):
+                     reward=None, done=None, action=None, eps_schedule=None):
         """Fused epsilon_greedy_policy + peek_action + replay append (src/dqn_lib.py:16-30,91-107).
         q: Q-values [N, 4] (float32 or float64) of the current boards; epsilon: float or a
-        float64 device scalar tensor (graph-safe).  Returns (action, reward, done)."""
+        float64 device scalar tensor (graph-safe); or eps_schedule = (decay_episodes, min_eps)
+        for the reference's per-episode schedule per board (src/dqn_lib.py:184-188, epsilon is
+        then ignored).  Returns (action, reward, done)."""
         if q.shape != (self.n, 4) or q.device != self.device or not q.is_contiguous():
             raise ValueError(f"q must be a contiguous [{self.n}, 4] tensor on {self.device}")
         if q.dtype not in (torch.float32, torch.float64):
             raise TypeError("q must be float32 or float64")
         dt = N.F32 if q.dtype == torch.float32 else N.F64
-        if isinstance(epsilon, torch.Tensor):
+        if eps_schedule is not None:
+            eps_ptr, eps_val = None, 0.0
+        elif isinstance(epsilon, torch.Tensor):
             if epsilon.dtype != torch.float64 or epsilon.device != self.device or epsilon.numel() != 1:
                 raise ValueError("epsilon tensor must be one float64 on the env device")
             eps_ptr, eps_val = N.ptr(epsilon), 0.0
@@ -107,6 +111,13 @@ class VecEnv2048:
         reward = self._out(reward, torch.int32)
         done = self._out(done, torch.uint8)
         action = self._out(action, torch.uint8)
+        if eps_schedule is not None:
+            N.check(N.load().g2048_env_step_egreedy_schedule(
+                self._h, N.ptr(q), dt, float(eps_schedule[0]), float(eps_schedule[1]),
+                N.ptr(reward), N.ptr(done), N.ptr(action),
+                replay.handle if replay is not None else None, self._stream()),
+                "g2048_env_step_egreedy_schedule")
+            return action, reward, done
         N.check(N.load().g2048_env_step_egreedy(self._h, N.ptr(q), dt, eps_ptr, eps_val,
                                                 N.ptr(reward), N.ptr(done), N.ptr(action),
                                                 replay.handle if replay is not None else None,

@@ -188,9 +188,9 @@ class Trainer:
 
     Per iteration: Q = online(boards) -> fused epsilon-greedy step of all N boards with replay
     append -> `updates_per_step` learner updates once the ring holds `min_fill` transitions.
-    epsilon = max((eps_decay_episodes - e) / eps_decay_episodes, min_epsilon) with e the mean
-    number of finished episodes per board (the reference's per-episode schedule, :184-188),
-    computed on the device each iteration."""
+    epsilon_b = max((eps_decay_episodes - e_b) / eps_decay_episodes, min_epsilon) with e_b the
+    number of episodes board b has finished -- the reference's per-episode schedule (:184-188)
+    applied per board inside the fused step kernel."""
 
     def __init__(self, env: VecEnv2048, replay: ReplayBuffer, learner: DQNLearner,
                  updates_per_step: int = 1, min_fill: int | None = None,
@@ -200,12 +200,7 @@ class Trainer:
         self.min_fill = int(min_fill if min_fill is not None else learner.B)
         self.eps_decay = float(eps_decay_episodes)
         self.min_eps = float(min_epsilon)
-        self.eps = torch.ones(1, dtype=torch.float64, device=env.device)
         self.steps = 0
-
-    def _update_eps(self):
-        e = self.env.ep[:, 0].to(torch.float64).mean()
-        self.eps.copy_(torch.clamp((self.eps_decay - e) / self.eps_decay, min=self.min_eps))
 
     def prefill(self, steps: int) -> None:
         """Random-policy steps (eps = 1) in one rollout launch, appended to the ring."""
@@ -213,9 +208,9 @@ class Trainer:
         self.steps += steps
 
     def step(self) -> None:
-        self._update_eps()
         q = self.learner.q_values(self.env)
-        self.env.step_egreedy(q, self.eps, replay=self.replay)
+        self.env.step_egreedy(q, None, replay=self.replay,
+                              eps_schedule=(self.eps_decay, self.min_eps))
         self.steps += 1
         if self.steps * self.env.n >= self.min_fill:
             for _ in range(self.updates_per_step):
@@ -235,7 +230,11 @@ class Trainer:
                 "max_tile_max": int(2 ** int(sel[:, 3].max())),
                 "max_tile_hist": {int(2 ** int(k)): int(v) for k, v in
                                   zip(*torch.unique(sel[:, 3], return_counts=True))},
-                "epsilon": float(self.eps.item())}
+                "epsilon_mean": float(self.current_epsilon().mean())}
+
+    def current_epsilon(self) -> torch.Tensor:
+        e = self.env.ep[:, 0].to(torch.float64)
+        return torch.clamp((self.eps_decay - e) / self.eps_decay, min=self.min_eps)
 
 
 def flops_per_update(net: str, batch: int) -> float:

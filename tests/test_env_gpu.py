@@ -318,3 +318,27 @@ def test_sharded_boards_match_single_env(g2048):
         a.step(None)
         b.step(None)
     assert torch.equal(whole.board, torch.cat([a.board, b.board]))
+
+
+@pytest.mark.parametrize("qdtype", [np.float32, np.float64])
+def test_egreedy_per_board_schedule_vs_oracle(g2048, qdtype):
+    """src/dqn_lib.py:184-188 per board: eps_b from the board's own episode count."""
+    n, seed = 3000, 23
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    rb = g2048.ReplayBuffer(4 * n, device=DEV)
+    ref = O.OracleEnv(n, seed=seed)
+    ref_rb = O.OracleReplay(4 * n)
+    eps_counts = np.random.default_rng(1).integers(0, 1500, size=n).astype(np.int32)
+    env.ep[:, 0] = torch.from_numpy(eps_counts).to(DEV)
+    ref.ep[:, 0] = eps_counts.view(np.uint32)
+    gen = np.random.default_rng(4)
+    mode = O.MODE_EGREEDY_F32 if qdtype == np.float32 else O.MODE_EGREEDY_F64
+    for step in range(30):
+        q = gen.normal(size=(n, 4)).astype(qdtype)
+        a, r, d = env.step_egreedy(torch.from_numpy(q).to(DEV), None, replay=rb,
+                                   eps_schedule=(1000.0, 0.01))
+        o = ref.step(mode, q=q, replay=ref_rb, eps_schedule=(1000.0, 0.01))
+        assert np.array_equal(_np(a), o["action"]), step
+        assert np.array_equal(_np(r), o["reward"]), step
+    assert np.array_equal(_np(env.board), ref.board)
+    assert np.array_equal(_np(rb.s2), ref_rb.s2)
