@@ -16,7 +16,7 @@ def G():
     return g2048
 
 
-@pytest.mark.parametrize("n", [1, 31, 32, 1000, 65536])
+@pytest.mark.parametrize("n", [1, 31, 32, 1000, 16383, 20001, 65536])
 def test_conv_forward_matches_torch(G, n):
     from g2048.nets import det_init, make_net
     from g2048.qnet import conv_forward

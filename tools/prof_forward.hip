@@ -1,0 +1,129 @@
+// Phase timing of k_conv_forward_persist (s_memtime deltas of block 0, per wave), built only
+// for kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip
+#define G2048_PHASE_PROF 1
+#include <cstdarg>
+#include <cstdio>
+#include <vector>
+int g2048_fail(int code, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vfprintf(stderr, fmt, ap);
+    va_end(ap);
+    return code;
+}
+#include "../reinforcement-learning-2048_amd/csrc/g2048_qnet.hip"
+
+extern "C" int g2048_replay_views(g2048_replay*, uint8_t**, uint8_t**, uint8_t**, int32_t**, uint8_t**,
+                                  uint64_t**) {
+    return -1;
+}
+// calibration: 16 x 128 f32 32x32x2 MFMAs on two accumulator chains, register operands
+__global__ __launch_bounds__(256) void k_mfma_cal(float* out, unsigned long long* cyc, int chains) {
+    float a = threadIdx.x * 1e-3f, b = 1.0f - threadIdx.x * 1e-4f;
+    f32x16 c0 = f32x16{0}, c1 = f32x16{0}, c2 = f32x16{0}, c3 = f32x16{0};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < 16; ++it) {
+        if (chains == 2) {
+#pragma unroll
+            for (int j = 0; j < 64; ++j) {
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
+            }
+        } else if (chains == 3) {  // 2 chains + 5 independent VALU FMAs per MFMA
+            float v0 = a, v1 = b, v2 = a + b, v3 = a - b, v4 = a * b;
+#pragma unroll
+            for (int j = 0; j < 64; ++j) {
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
+                v0 = fmaf(v0, 1.0001f, 0.5f);
+                v1 = fmaf(v1, 1.0001f, 0.5f);
+                v2 = fmaf(v2, 1.0001f, 0.5f);
+                v3 = fmaf(v3, 1.0001f, 0.5f);
+                v4 = fmaf(v4, 1.0001f, 0.5f);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
+                v0 = fmaf(v0, 1.0001f, 0.25f);
+                v1 = fmaf(v1, 1.0001f, 0.25f);
+                v2 = fmaf(v2, 1.0001f, 0.25f);
+                v3 = fmaf(v3, 1.0001f, 0.25f);
+                v4 = fmaf(v4, 1.0001f, 0.25f);
+            }
+            a += v0 + v1 + v2 + v3 + v4;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
+                c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c2, 0, 0, 0);
+                c3 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, b, c3, 0, 0, 0);
+            }
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    float s = 0;
+    for (int i = 0; i < 16; ++i) s += c0[i] + c1[i] + c2[i] + c3[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) cyc[threadIdx.x >> 6] = t1 - t0;
+}
+
+int main(int argc, char** argv) {
+    {
+        float* o;
+        unsigned long long* cyc;
+        (void)hipMalloc(&o, 256 * 256 * 4);
+        (void)hipMalloc(&cyc, 64);
+        for (int chains = 2; chains <= 4; ++chains) {
+            hipEvent_t e0, e1;
+            (void)hipEventCreate(&e0);
+            (void)hipEventCreate(&e1);
+            hipLaunchKernelGGL(k_mfma_cal, dim3(256), dim3(256), 0, nullptr, o, cyc, chains);
+            (void)hipEventRecord(e0, nullptr);
+            hipLaunchKernelGGL(k_mfma_cal, dim3(256), dim3(256), 0, nullptr, o, cyc, chains);
+            (void)hipEventRecord(e1, nullptr);
+            (void)hipEventSynchronize(e1);
+            float ms;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            unsigned long long h[4];
+            (void)hipMemcpy(h, cyc, 32, hipMemcpyDeviceToHost);
+            printf("mfma cal chains=%d: 2048 MFMAs/wave: memtime %llu %llu %llu %llu, %.2f us "
+                   "(%.1f TF)\n", chains, h[0], h[1], h[2], h[3], ms * 1e3,
+                   256.0 * 4 * 2048 * 4096 / (ms * 1e-3) / 1e12);
+        }
+    }
+    const long n = argc > 1 ? atol(argv[1]) : 65536;
+    const int sizes[8] = {256, 64, 16384, 64, 16384, 64, 256, 4};
+    float* w[8];
+    for (int i = 0; i < 8; ++i) {
+        std::vector<float> h(sizes[i]);
+        for (int j = 0; j < sizes[i]; ++j) h[j] = 0.01f * ((j * 37 + i) % 17 - 8);
+        (void)hipMalloc(&w[i], sizes[i] * 4);
+        (void)hipMemcpy(w[i], h.data(), sizes[i] * 4, hipMemcpyHostToDevice);
+    }
+    uint8_t* rows;
+    float* q;
+    (void)hipMalloc(&rows, n * 16);
+    (void)hipMalloc(&q, n * 16);
+    std::vector<uint8_t> hb(n * 16);
+    for (long i = 0; i < n * 16; ++i) hb[i] = (uint8_t)((i * 2654435761u >> 13) % 12);
+    (void)hipMemcpy(rows, hb.data(), n * 16, hipMemcpyHostToDevice);
+    g2048_convnet_params p{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    for (int it = 0; it < 5; ++it) g2048_convnet_forward(&p, rows, nullptr, n, q, nullptr);
+    (void)hipEventRecord(a, nullptr);
+    for (int it = 0; it < 20; ++it) g2048_convnet_forward(&p, rows, nullptr, n, q, nullptr);
+    (void)hipEventRecord(b, nullptr);
+    (void)hipEventSynchronize(b);
+    float ms;
+    (void)hipEventElapsedTime(&ms, a, b);
+    unsigned long long ph[4][8];
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
+    printf("n=%ld  %.2f us/launch\n", n, ms * 1e3 / 20);
+    const char* names[8] = {"top_sync", "stage+sync", "conv2", "h2+sync", "fc1", "sync",
+                            "fc2", "weights"};
+    for (int k = 0; k < 8; ++k) {
+        printf("%-11s", names[k]);
+        for (int wv = 0; wv < 4; ++wv) printf(" %9llu", ph[wv][k]);
+        printf("\n");
+    }
+    return 0;
+}
