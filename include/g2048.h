@@ -59,6 +59,21 @@ typedef enum { G2048_F32 = 0, G2048_F64 = 1 } g2048_dtype;
 typedef struct g2048_env g2048_env;
 typedef struct g2048_replay g2048_replay;
 
+/* One finished episode (the Experiment.add_episode fields, src/experiments.py:112-122).  40 B.
+ * mean reward = score / moves (the rewards of an episode sum to its merge score);
+ * q_value = q_sum / moves (max_a Q per step, 0 on explore / non-greedy steps, src/dqn_lib.py:19,29);
+ * epsilon follows from `episode` and the schedule. */
+typedef struct {
+    uint64_t step;     /* the board's step counter at its terminal step */
+    double q_sum;      /* sum over the episode's steps of max_a Q(s) */
+    uint32_t board;    /* global board id (board_offset + i) */
+    uint32_t episode;  /* the board's episode index (0-based) */
+    uint32_t score;    /* Board2048.merge_score() */
+    uint32_t moves;    /* len(_action_history), including the terminal self-transition */
+    uint32_t max_exp;  /* log2 of max(state) */
+    uint32_t reserved;
+} g2048_episode;
+
 /* ---- environment -------------------------------------------------------------------------
  * State per board i: board u8[16]; meta u32[4] = {score, moves, steps_lo, steps_hi} (score =
  * Board2048._mergescore, moves = len(_action_history) of the running episode, steps = RNG
@@ -80,6 +95,24 @@ G2048_API int64_t g2048_env_size(const g2048_env* env);
 
 /* Re-deal fresh boards (2 spawns, src/board.py:18-20) where reset_mask_dev[i] != 0 (all if NULL). */
 G2048_API int g2048_env_reset(g2048_env* env, const uint8_t* reset_mask_dev, void* stream);
+
+/* Explicit-reset epoch (host state of the env: the Philox counter of the next g2048_env_reset),
+ * for checkpoint / resume. */
+G2048_API int g2048_env_get_epoch(const g2048_env* env, uint32_t* epoch_out);
+G2048_API int g2048_env_set_epoch(g2048_env* env, uint32_t epoch);
+
+/* Attach (log_dev != NULL) or detach an episode log: every later terminal step of any step /
+ * rollout call appends one g2048_episode at slot (count % capacity) (count_dev: u64, advanced
+ * atomically -- records of one launch land in arbitrary order; sort by (step, board)).
+ * qsum_dev f64[n] holds each board's running max-Q sum (zero it before attaching).  With
+ * G2048_NO_AUTORESET a board that stays terminal logs again on every step.  Replaces the
+ * per-episode bookkeeping of training_loop (src/dqn_lib.py:184-213). */
+G2048_API int g2048_env_set_episode_log(g2048_env* env, g2048_episode* log_dev, int64_t capacity,
+                                        uint64_t* count_dev, double* qsum_dev);
+
+/* Legal-move mask of every current board: available_moves_as_torch_unit_vector
+ * (src/board.py:128-135) as bits (bit a = move a changes the board). */
+G2048_API int g2048_env_legal_mask(g2048_env* env, uint8_t* legal_dev, void* stream);
 
 /* One env step of every board.  Replaces Board2048.peek_action (src/board.py:185-202) +
  * available_moves_as_torch_unit_vector (:128-135) + reward_func_merge_score

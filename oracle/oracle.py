@@ -28,7 +28,15 @@ def build() -> str:
 class _Env(C.Structure):
     _fields_ = [("n", C.c_int64), ("board_offset", C.c_uint64), ("seed", C.c_uint64),
                 ("flags", C.c_uint32), ("board", C.c_void_p), ("meta", C.c_void_p),
-                ("ep", C.c_void_p)]
+                ("ep", C.c_void_p), ("qsum", C.c_void_p), ("log", C.c_void_p),
+                ("log_cap", C.c_int64), ("log_count", C.c_void_p)]
+
+
+# g2048_episode / o2048_episode (40 bytes)
+EPISODE_DTYPE = np.dtype([("step", "<u8"), ("q_sum", "<f8"), ("board", "<u4"), ("episode", "<u4"),
+                          ("score", "<u4"), ("moves", "<u4"), ("max_exp", "<u4"),
+                          ("reserved", "<u4")])
+assert EPISODE_DTYPE.itemsize == 40
 
 
 class _Replay(C.Structure):
@@ -140,9 +148,27 @@ class OracleEnv:
         self.meta = np.zeros((n, 4), np.uint32)
         self.ep = np.zeros((n, 4), np.uint32)
         self.epoch = 0
-        self._c = _Env(n, board_offset, seed, flags, _p(self.board), _p(self.meta), _p(self.ep))
+        self._c = _Env(n, board_offset, seed, flags, _p(self.board), _p(self.meta), _p(self.ep),
+                       None, None, 0, None)
         if reset:
             self.reset()
+
+    def attach_episode_log(self, capacity: int):
+        """Append one EPISODE_DTYPE record per finished episode (g2048_env_set_episode_log)."""
+        self.log = np.zeros(capacity, EPISODE_DTYPE)
+        self.log_count = np.zeros(1, np.uint64)
+        self.qsum = np.zeros(self.n, np.float64)
+        self._c.qsum, self._c.log = _p(self.qsum), self.log.ctypes.data
+        self._c.log_cap, self._c.log_count = capacity, _p(self.log_count)
+
+    def episodes(self):
+        """Logged records so far (ring order = append order), as a structured array."""
+        n = int(self.log_count[0])
+        cap = len(self.log)
+        if n <= cap:
+            return self.log[:n].copy()
+        k = n % cap
+        return np.concatenate([self.log[k:], self.log[:k]])
 
     def reset(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)

@@ -214,6 +214,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
         const uint64_t t = (uint64_t)m[2] | ((uint64_t)m[3] << 32);
         uint32_t u[4];
         draw(e->seed, gid, 0u, t, u);
+        double qs = e->qsum ? e->qsum[i] : 0.0;
 
         const uint8_t legal = o2048_legal_mask(b);   /* dqn_lib.py:17 */
         const int done = legal == 0;                 /* dqn_lib.py:18 */
@@ -245,9 +246,17 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
                     a = (int)(u[0] >> 30);               /* np.random.randint(4) */
                 }
             } else if (mode == 2) {
-                a = o2048_greedy_f32((const float*)q + 4 * i, legal, fixed);
+                const float* qi = (const float*)q + 4 * i;
+                a = o2048_greedy_f32(qi, legal, fixed);
+                float mq = qi[0];                         /* torch.max(Q), dqn_lib.py:29 */
+                for (int j = 1; j < 4; ++j) mq = qi[j] > mq ? qi[j] : mq;
+                qs += (double)mq;
             } else {
-                a = o2048_greedy_f64((const double*)q + 4 * i, legal, fixed);
+                const double* qi = (const double*)q + 4 * i;
+                a = o2048_greedy_f64(qi, legal, fixed);
+                double mq = qi[0];
+                for (int j = 1; j < 4; ++j) mq = qi[j] > mq ? qi[j] : mq;
+                qs += mq;
             }
         }
 
@@ -293,12 +302,26 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             uint32_t* ep = e->ep + 4 * i;
             uint8_t mx = 0;
             for (int k = 0; k < 16; ++k) if (b[k] > mx) mx = b[k];
+            if (e->log) {  /* experiments.py:112-122 add_episode, one record per episode */
+                o2048_episode* rec = e->log + (int64_t)(*e->log_count % (uint64_t)e->log_cap);
+                rec->step = t;
+                rec->q_sum = qs;
+                rec->board = (uint32_t)gid;
+                rec->episode = ep[0];
+                rec->score = m[0];
+                rec->moves = m[1];
+                rec->max_exp = mx;
+                rec->reserved = 0;
+                *e->log_count += 1;
+            }
+            qs = 0.0;
             ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;
             if (autoreset) {
                 fresh_board(b, u, e->flags);   /* the step's own block (see fresh_board) */
                 m[0] = 0; m[1] = 0;
             }
         }
+        if (e->qsum) e->qsum[i] = qs;
         const uint64_t t1 = t + 1;
         m[2] = (uint32_t)t1;
         m[3] = (uint32_t)(t1 >> 32);

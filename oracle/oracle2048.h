@@ -37,6 +37,13 @@ int o2048_greedy_f32(const float q[4], uint8_t legal, int fixed);
  *       4 = actions in + injected spawns.
  * meta: uint32[N][4] = {score, moves, steps_lo, steps_hi}; ep: uint32[N][4] = {episodes,
  * last_score, last_moves, last_max_exp}.  Replay pointers may be NULL (no append). */
+/* One finished episode, the layout of include/g2048.h g2048_episode (40 B). */
+typedef struct {
+    uint64_t step;
+    double q_sum;
+    uint32_t board, episode, score, moves, max_exp, reserved;
+} o2048_episode;
+
 typedef struct {
     int64_t n;               /* boards in this shard */
     uint64_t board_offset;   /* global id of board 0 (rank * n for sharded envs) */
@@ -45,6 +52,10 @@ typedef struct {
     uint8_t* board;          /* [n][16] */
     uint32_t* meta;          /* [n][4]  */
     uint32_t* ep;            /* [n][4]  */
+    double* qsum;            /* [n] running max-Q sum, or NULL (episode log off) */
+    o2048_episode* log;      /* episode log ring, appended in board order, or NULL */
+    int64_t log_cap;
+    uint64_t* log_count;
 } o2048_env;
 
 typedef struct {

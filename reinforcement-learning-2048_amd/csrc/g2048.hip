@@ -7,6 +7,8 @@
 //   meta  u32[N][4]   {score, moves, steps_lo, steps_hi}
 //   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (touched on done only)
 // Replay ring (capacity C): s u8[C][16], s2 u8[C][16], a u8[C], r i32[C], d u8[C], count u64.
+// Optional episode log (g2048_env_set_episode_log): ring of g2048_episode records appended on
+// every terminal step + qsum f64[N] (running sum of max_a Q over the board's episode).
 //
 // One lane owns one board for the whole launch: load board + meta (2 x dwordx4), do the
 // legal-mask / select / slide / spawn / reset arithmetic in VGPRs (g2048_board.hpp), store them
@@ -67,6 +69,10 @@ struct StepArgs {
     ReplayDev rb;
     int k_steps;
     long long* reward_sum;
+    g2048_episode* log;  // episode log ring (NULL = off)
+    int64_t log_cap;
+    unsigned long long* log_count;
+    double* qsum;  // per-board running sum of max Q (NULL = off)
 };
 
 __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v.y, v.z, v.w}; }
@@ -75,7 +81,7 @@ __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v
 // which restates src/dqn_lib.py:91-107 + src/board.py.
 template <int MODE>
 __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, Board& b,
-                                         uint4& m, double eps, int32_t& rew_out,
+                                         uint4& m, double eps, double& qs, int32_t& rew_out,
                                          uint32_t& done_out, uint32_t& legal_out,
                                          uint32_t& act_out) {
     const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
@@ -98,11 +104,13 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
             const float4 q = reinterpret_cast<const float4*>(A.q)[i];
             act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
                         : greedy_compat(q.x, q.y, q.z, q.w, legal);
+            qs += (double)fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w));  // torch.max(Q) (:29)
         } else {
             const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
             const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
             act = fixed ? greedy_fixed(q01.x, q01.y, q23.x, q23.y, legal)
                         : greedy_compat(q01.x, q01.y, q23.x, q23.y, legal);
+            qs += fmax(fmax(q01.x, q01.y), fmax(q23.x, q23.y));
         }
     }
 
@@ -135,7 +143,23 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     }
 
     if (done) {
-        A.ep[i] = make_uint4(A.ep[i].x + 1u, m.x, m.y, max_exp(b));
+        const uint4 e0 = A.ep[i];
+        const uint32_t mx = max_exp(b);
+        A.ep[i] = make_uint4(e0.x + 1u, m.x, m.y, mx);
+        if (A.log) {  // Experiment.add_episode (src/experiments.py:112-122), one record per episode
+            const unsigned long long k = atomicAdd(A.log_count, 1ull);
+            g2048_episode rec;
+            rec.step = t;
+            rec.q_sum = qs;
+            rec.board = (uint32_t)gid;
+            rec.episode = e0.x;
+            rec.score = m.x;
+            rec.moves = m.y;
+            rec.max_exp = mx;
+            rec.reserved = 0u;
+            A.log[(int64_t)(k % (unsigned long long)A.log_cap)] = rec;
+        }
+        qs = 0.0;
         if (!(A.flags & G2048_NO_AUTORESET)) {
             b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m.x = 0u;
@@ -174,9 +198,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     }
     int32_t rew;
     uint32_t done, legal, act;
-    step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, rew, done, legal, act);
+    double qs = A.qsum ? A.qsum[i] : 0.0;
+    step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
+    if (A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
     if (A.legal_out) A.legal_out[i] = (uint8_t)legal;
@@ -192,14 +218,16 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     uint4 m = A.meta[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
     long long rsum = 0;
+    double qs = A.qsum ? A.qsum[i] : 0.0;
     for (int s = 0; s < A.k_steps; ++s) {
         int32_t rew;
         uint32_t done, legal, act;
-        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, rew, done, legal, act);
+        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, qs, rew, done, legal, act);
         rsum += rew;
     }
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
+    if (A.qsum) A.qsum[i] = qs;
     if (A.reward_sum) A.reward_sum[i] += rsum;
     if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
 }
@@ -218,6 +246,13 @@ __global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint4* meta, int
     m.x = 0u;
     m.y = 0u;
     meta[i] = m;
+}
+
+// available_moves_as_torch_unit_vector (src/board.py:128-135) of every board, as a bit mask.
+__global__ __launch_bounds__(kBlock) void k_legal(const uint4* board, int64_t n, uint8_t* legal) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    legal[i] = (uint8_t)legal_mask(load_board(board[i]));
 }
 
 struct SampleArgs {
@@ -337,6 +372,10 @@ struct g2048_env {
     unsigned long long* err = nullptr;
     bool owns = false;
     uint32_t epoch = 0;
+    g2048_episode* log = nullptr;
+    int64_t log_cap = 0;
+    unsigned long long* log_count = nullptr;
+    double* qsum = nullptr;
 };
 
 struct g2048_replay {
@@ -383,6 +422,10 @@ int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
     A.p4_thresh = p4_thresh(e->flags);
     A.flags = e->flags;
     A.err = e->err;
+    A.log = e->log;
+    A.log_cap = e->log_cap;
+    A.log_count = e->log_count;
+    A.qsum = e->qsum;
     if (rb) {
         if (rb->device != e->device)
             return fail(G2048_EINVAL, "replay on device %d, env on device %d", rb->device, e->device);
@@ -521,6 +564,41 @@ int64_t g2048_env_size(const g2048_env* e) { return e ? e->n : 0; }
 int g2048_env_reset(g2048_env* e, const uint8_t* mask, void* stream) {
     if (!e) return fail(G2048_EINVAL, "env_reset: NULL env");
     return launch_reset(e, mask, (hipStream_t)stream);
+}
+
+int g2048_env_get_epoch(const g2048_env* e, uint32_t* epoch) {
+    if (!e || !epoch) return fail(G2048_EINVAL, "env_get_epoch: NULL argument");
+    *epoch = e->epoch;
+    return G2048_OK;
+}
+
+int g2048_env_set_epoch(g2048_env* e, uint32_t epoch) {
+    if (!e) return fail(G2048_EINVAL, "env_set_epoch: NULL env");
+    e->epoch = epoch;
+    return G2048_OK;
+}
+
+int g2048_env_set_episode_log(g2048_env* e, g2048_episode* log, int64_t capacity,
+                              uint64_t* count, double* qsum) {
+    if (!e) return fail(G2048_EINVAL, "env_set_episode_log: NULL env");
+    if (log && (capacity <= 0 || !count || !qsum || ((uintptr_t)log & 7u) || ((uintptr_t)qsum & 7u)))
+        return fail(G2048_EINVAL,
+                    "env_set_episode_log: need capacity > 0, count and qsum, 8-byte alignment");
+    e->log = log;
+    e->log_cap = log ? capacity : 0;
+    e->log_count = log ? reinterpret_cast<unsigned long long*>(count) : nullptr;
+    e->qsum = log ? qsum : nullptr;
+    return G2048_OK;
+}
+
+int g2048_env_legal_mask(g2048_env* e, uint8_t* legal, void* stream) {
+    if (!e || !legal) return fail(G2048_EINVAL, "env_legal_mask: NULL argument");
+    DeviceGuard g(e->device);
+    hipLaunchKernelGGL(k_legal, dim3(grid_for(e->n)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream),
+                       reinterpret_cast<const uint4*>(e->board), e->n, legal);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
 }
 
 int g2048_env_step(g2048_env* e, const uint8_t* actions, int32_t* reward, uint8_t* done,

@@ -10,11 +10,67 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
 import torch
 
 from . import _native as N
 
 ACTIONS = ("up", "down", "left", "right")  # src/board.py:129, action ints at :191
+
+# g2048_episode (include/g2048.h), 40 bytes per finished episode
+EPISODE_FIELDS = ("step", "q_sum", "board", "episode", "score", "moves", "max_exp")
+
+
+def decode_episodes(raw: torch.Tensor) -> dict:
+    """int64 [k, 5] records -> dict of int64 / float64 host tensors, sorted by (step, board)
+    (records of one launch are appended in arbitrary order)."""
+    raw = raw.cpu()
+    lo = raw[:, 2:5] & 0xFFFFFFFF
+    hi = (raw[:, 2:5] >> 32) & 0xFFFFFFFF
+    out = {"step": raw[:, 0].clone(), "q_sum": raw[:, 1].view(torch.float64).clone(),
+           "board": lo[:, 0], "episode": hi[:, 0], "score": lo[:, 1], "moves": hi[:, 1],
+           "max_exp": lo[:, 2]}
+    order = torch.from_numpy(np.lexsort((out["board"].numpy(), out["step"].numpy())))
+    return {k: v[order] for k, v in out.items()}
+
+
+class EpisodeLog:
+    """Device ring of finished-episode records, appended by the step kernels themselves
+    (g2048_env_set_episode_log) -- the per-episode bookkeeping of training_loop
+    (src/dqn_lib.py:184-213) and Experiment.add_episode (src/experiments.py:112-122) without a
+    host round trip per step.  `read()` returns the records appended since the last read."""
+
+    def __init__(self, env: "VecEnv2048", capacity: int):
+        self.env = env
+        self.capacity = int(capacity)
+        kw = dict(device=env.device)
+        self.raw = torch.zeros((self.capacity, 5), dtype=torch.int64, **kw)
+        self.count = torch.zeros(1, dtype=torch.int64, **kw)
+        self.qsum = torch.zeros(env.n, dtype=torch.float64, **kw)
+        self.read_upto = 0
+        N.check(N.load().g2048_env_set_episode_log(env.handle, N.ptr(self.raw), self.capacity,
+                                                   N.ptr(self.count), N.ptr(self.qsum)),
+                "g2048_env_set_episode_log")
+
+    def detach(self) -> None:
+        N.check(N.load().g2048_env_set_episode_log(self.env.handle, None, 0, None, None),
+                "g2048_env_set_episode_log")
+
+    def total(self) -> int:  # host sync
+        return int(self.count.item())
+
+    def read(self, strict: bool = True) -> dict:
+        """Records appended since the last read (host sync).  strict: raise if the ring wrapped
+        past unread records (raise the capacity or read more often)."""
+        n = self.total()
+        lost = n - self.read_upto - self.capacity
+        if lost > 0:
+            if strict:
+                raise RuntimeError(f"episode log overflow: {lost} records lost")
+            self.read_upto = n - self.capacity
+        idx = torch.arange(self.read_upto, n, device=self.raw.device) % self.capacity
+        self.read_upto = n
+        return decode_episodes(self.raw[idx])
 
 
 class VecEnv2048:
@@ -65,6 +121,35 @@ class VecEnv2048:
 
     def _stream(self):
         return N.stream_of(self.device)
+
+    # ------------------------------------------------------------------ state
+    @property
+    def epoch(self) -> int:
+        """Explicit-reset epoch (host state of the env; saved by checkpoints)."""
+        v = C.c_uint32()
+        N.check(N.load().g2048_env_get_epoch(self._h, C.byref(v)), "g2048_env_get_epoch")
+        return int(v.value)
+
+    @epoch.setter
+    def epoch(self, value: int) -> None:
+        N.check(N.load().g2048_env_set_epoch(self._h, int(value)), "g2048_env_set_epoch")
+
+    def attach_episode_log(self, capacity: int = 1 << 20) -> EpisodeLog:
+        self.episode_log = EpisodeLog(self, capacity)
+        return self.episode_log
+
+    def legal_mask(self, out: torch.Tensor | None = None) -> torch.Tensor:
+        """available_moves (src/board.py:128-145) of every current board as a u8 bit mask."""
+        out = self._out(out, torch.uint8)
+        N.check(N.load().g2048_env_legal_mask(self._h, N.ptr(out), self._stream()),
+                "g2048_env_legal_mask")
+        return out
+
+    def available_moves_as_unit_vectors(self, dtype=torch.float32) -> torch.Tensor:
+        """available_moves_as_torch_unit_vector (src/board.py:128-135) for all boards: [N, 4]."""
+        m = self.legal_mask().to(torch.int32)
+        bits = torch.arange(4, device=self.device, dtype=torch.int32)
+        return ((m[:, None] >> bits) & 1).to(dtype)
 
     # ------------------------------------------------------------------ stepping
     def reset(self, mask: torch.Tensor | None = None) -> None:

@@ -342,3 +342,80 @@ def test_egreedy_per_board_schedule_vs_oracle(g2048, qdtype):
         assert np.array_equal(_np(r), o["reward"]), step
     assert np.array_equal(_np(env.board), ref.board)
     assert np.array_equal(_np(rb.s2), ref_rb.s2)
+
+
+def _oracle_records(o):
+    r = o.episodes()
+    order = np.lexsort((r["board"], r["step"]))
+    return r[order]
+
+
+@pytest.mark.parametrize("qdt", [np.float32, np.float64])
+def test_episode_log_matches_oracle(g2048, qdt):
+    """In-kernel episode log (g2048_env_set_episode_log) == oracle records, field by field,
+    over eps-greedy steps with the per-board schedule (many episodes per board)."""
+    n, steps = 512, 300
+    env = g2048.VecEnv2048(n, seed=11, device=DEV)
+    log = env.attach_episode_log(1 << 16)
+    o = O.OracleEnv(n, 11)
+    o.attach_episode_log(1 << 16)
+    rng = np.random.default_rng(3)
+    mode = O.MODE_EGREEDY_F32 if qdt == np.float32 else O.MODE_EGREEDY_F64
+    for t in range(steps):
+        q = rng.standard_normal((n, 4)).astype(qdt)
+        env.step_egreedy(torch.from_numpy(q).to(DEV), None, eps_schedule=(40.0, 0.05))
+        o.step(mode, q=q, eps_schedule=(40.0, 0.05))
+    got = log.read()
+    want = _oracle_records(o)
+    assert len(want) > 500 and len(got["step"]) == len(want)
+    for f in ("step", "board", "episode", "score", "moves", "max_exp"):
+        np.testing.assert_array_equal(got[f].numpy(), want[f].astype(np.int64), err_msg=f)
+    np.testing.assert_array_equal(got["q_sum"].numpy(), want["q_sum"])  # same order, same f64 sum
+    np.testing.assert_array_equal(_np(env.ep), o.ep.view(np.int32))
+    assert log.read()["step"].numel() == 0  # nothing new since the last read
+
+
+def test_episode_log_rollout_and_overflow(g2048):
+    n = 256
+    env = g2048.VecEnv2048(n, seed=5, device=DEV)
+    log = env.attach_episode_log(64)
+    env.rollout(200)
+    with pytest.raises(RuntimeError, match="overflow"):
+        log.read()
+    env2 = g2048.VecEnv2048(n, seed=5, device=DEV)
+    log2 = env2.attach_episode_log(1 << 14)
+    env2.rollout(200)
+    o = O.OracleEnv(n, 5)
+    o.attach_episode_log(1 << 14)
+    for _ in range(200):
+        o.step(O.MODE_RANDOM)
+    got, want = log2.read(), _oracle_records(o)
+    for f in ("step", "board", "episode", "score", "moves", "max_exp"):
+        np.testing.assert_array_equal(got[f].numpy(), want[f].astype(np.int64), err_msg=f)
+    assert float(got["q_sum"].abs().sum()) == 0.0  # random policy: max_q_value = 0 (:19)
+    log2.detach()
+    env2.rollout(50)
+    assert log2.total() == len(want)
+
+
+def test_legal_mask_kernel(g2048):
+    boards = np.concatenate([_mask_boards(), _random_boards(2000, 9)])
+    env = _env_with(g2048, boards)
+    got = _np(env.legal_mask())
+    want = np.array([O.legal_mask(b) for b in boards], np.uint8)
+    np.testing.assert_array_equal(got, want)
+    assert set(np.unique(got)) == set(range(16))
+    uv = _np(env.available_moves_as_unit_vectors())
+    np.testing.assert_array_equal(uv, ((want[:, None] >> np.arange(4)) & 1).astype(np.float32))
+
+
+def test_epoch_roundtrip(g2048):
+    a = g2048.VecEnv2048(64, seed=2, device=DEV)
+    a.reset()
+    a.reset()
+    assert a.epoch == 3  # construction reset + 2
+    b = g2048.VecEnv2048(64, seed=2, device=DEV)
+    b.epoch = a.epoch
+    a.reset()
+    b.reset()
+    np.testing.assert_array_equal(_np(a.board), _np(b.board))
