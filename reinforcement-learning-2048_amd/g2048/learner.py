@@ -123,6 +123,14 @@ class DQNLearner:
         params = list(self.model.parameters())
         snap = [p.detach().clone() for p in params]
         step0 = self.step_dev.clone() if self.fused else None
+        loss0 = self.last_loss.clone()
+        rng0 = torch.cuda.get_rng_state(self.device)  # the warm-up draws must not shift the stream
+        # optimizer moments too (a resumed learner captures with non-zero Adam state)
+        if self.fused:
+            adam0 = (self._adam.exp_avg.clone(), self._adam.exp_avg_sq.clone())
+        else:
+            adam0 = {p: {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
+                     for p, st in self.opt.state.items()}
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):  # warm-up (allocates Adam state, autograd buffers)
@@ -145,14 +153,18 @@ class DQNLearner:
         with torch.no_grad():  # restore in place (the graphs hold these addresses)
             for p, s in zip(params, snap):
                 p.copy_(s)
-            for st in self.opt.state.values():
-                for v in st.values():
+            for p, st in self.opt.state.items():
+                prev = adam0.get(p, {}) if not self.fused else {}
+                for k, v in st.items():
                     if torch.is_tensor(v):
-                        v.zero_()
+                        v.copy_(prev[k]) if k in prev else v.zero_()
             self.grad_flat.zero_()
-            self.last_loss.zero_()
+            self.last_loss.copy_(loss0)
+        torch.cuda.set_rng_state(rng0, self.device)
+        with torch.no_grad():
             if self.fused:
-                self._adam.reset_state()
+                self._adam.exp_avg.copy_(adam0[0])
+                self._adam.exp_avg_sq.copy_(adam0[1])
                 self.step_dev.copy_(step0)
 
     def update(self) -> torch.Tensor:
@@ -182,6 +194,60 @@ class DQNLearner:
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 
+    # -------------------------------------------------------------- checkpoint / resume
+    def state_dict(self) -> dict:
+        """Everything an update depends on (tensors cloned to the host)."""
+        cpu = lambda t: t.detach().cpu().clone()  # noqa: E731
+        st = {"fused": self.fused, "kind": self.kind or "", "dtype": str(self.dtype),
+              "batch_size": self.B, "gamma": self.gamma, "double_dqn": self.use_double_dqn,
+              "target_sync_every": self.target_sync_every, "updates": self.updates, "last_loss": cpu(self.last_loss),
+              "model": {k: cpu(v) for k, v in self.model.state_dict().items()},
+              "target": {k: cpu(v) for k, v in self.target.state_dict().items()},
+              "cuda_rng": torch.cuda.get_rng_state(self.device)}
+        if self.fused:
+            st.update(adam_exp_avg=cpu(self._adam.exp_avg), adam_exp_avg_sq=cpu(self._adam.exp_avg_sq),
+                      step_dev=cpu(self.step_dev), sample_seed=self.sample_seed)
+        else:
+            params = self.bucket.params
+            st["adam"] = [{k: cpu(v) for k, v in self.opt.state[p].items() if torch.is_tensor(v)}
+                          if p in self.opt.state else {} for p in params]
+        return st
+
+    @torch.no_grad()
+    def load_state_dict(self, st: dict) -> None:
+        """Restore in place: parameter, optimizer and counter tensors keep their addresses, so
+        already-captured graphs stay valid."""
+        if bool(st["fused"]) != self.fused or st["kind"] != (self.kind or ""):
+            raise ValueError("checkpoint was written by a learner of another net / path")
+        for k, v in (("batch_size", self.B), ("gamma", self.gamma), ("double_dqn", self.use_double_dqn),
+                     ("dtype", str(self.dtype))):
+            if st[k] != v:
+                raise ValueError(f"checkpoint {k}={st[k]!r} != this learner's {v!r}")
+        for mod, key in ((self.model, "model"), (self.target, "target")):
+            cur = mod.state_dict()
+            if set(cur) != set(st[key]):
+                raise ValueError(f"{key}: parameter names differ from the checkpoint")
+            for k, v in cur.items():
+                v.copy_(st[key][k])
+        self.updates = int(st["updates"])
+        self.last_loss.copy_(st["last_loss"])
+        torch.cuda.set_rng_state(st["cuda_rng"], self.device)
+        if self.fused:
+            self._adam.exp_avg.copy_(st["adam_exp_avg"])
+            self._adam.exp_avg_sq.copy_(st["adam_exp_avg_sq"])
+            self.step_dev.copy_(st["step_dev"])
+            self.sample_seed = int(st["sample_seed"])
+        else:
+            for p, saved in zip(self.bucket.params, st["adam"]):
+                if not saved:
+                    continue
+                cur = self.opt.state[p]
+                for k, v in saved.items():
+                    if k in cur and torch.is_tensor(cur[k]):
+                        cur[k].copy_(v)
+                    else:
+                        cur[k] = v.to(p.device) if (k != "step" or self.graph) else v
+
 
 class Trainer:
     """Vectorised training_loop (src/dqn_lib.py:167-244).
@@ -190,35 +256,117 @@ class Trainer:
     append -> `updates_per_step` learner updates once the ring holds `min_fill` transitions.
     epsilon_b = max((eps_decay_episodes - e_b) / eps_decay_episodes, min_epsilon) with e_b the
     number of episodes board b has finished -- the reference's per-episode schedule (:184-188)
-    applied per board inside the fused step kernel."""
+    applied per board inside the fused step kernel.  Every finished episode is appended to the
+    env's device episode log by the step kernel itself (add_episode fields, :206-207); the
+    first `track_boards` boards also keep a device ring of their last `history_len`
+    transitions, from which complete games are cut for snapshot_game (:208-209)."""
 
     def __init__(self, env: VecEnv2048, replay: ReplayBuffer, learner: DQNLearner,
                  updates_per_step: int = 1, min_fill: int | None = None,
-                 eps_decay_episodes: float = 1000.0, min_epsilon: float = 0.01):
+                 eps_decay_episodes: float = 1000.0, min_epsilon: float = 0.01,
+                 episode_log_capacity: int = 1 << 20, track_boards: int = 0,
+                 history_len: int = 4096):
         self.env, self.replay, self.learner = env, replay, learner
         self.updates_per_step = int(updates_per_step)
         self.min_fill = int(min_fill if min_fill is not None else learner.B)
         self.eps_decay = float(eps_decay_episodes)
         self.min_eps = float(min_epsilon)
         self.steps = 0
+        self.log = env.attach_episode_log(episode_log_capacity) if episode_log_capacity else None
+        self.track = int(min(track_boards, env.n))
+        self.history_len = int(history_len)
+        if self.track:
+            kw = dict(device=env.device)
+            self.h_s = torch.zeros((self.history_len, self.track, 16), dtype=torch.uint8, **kw)
+            self.h_a = torch.zeros((self.history_len, self.track), dtype=torch.uint8, **kw)
+            self.h_r = torch.zeros((self.history_len, self.track), dtype=torch.int32, **kw)
+            self.h_d = torch.zeros((self.history_len, self.track), dtype=torch.uint8, **kw)
+            self.h_t0 = self.steps  # first trainer step the ring holds
+            # per tracked board: its running episode starts inside the window (no moves yet)
+            self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
+        self._action = torch.empty(env.n, dtype=torch.uint8, device=env.device)
+        self._reward = torch.empty(env.n, dtype=torch.int32, device=env.device)
+        self._done = torch.empty(env.n, dtype=torch.uint8, device=env.device)
+        self._numbers = {}  # (board, board_episode) -> Experiment episode number
 
     def prefill(self, steps: int) -> None:
         """Random-policy steps (eps = 1) in one rollout launch, appended to the ring."""
+        if self.track:
+            raise RuntimeError("prefill before enabling board tracking (histories need every step)")
         self.env.rollout(steps, replay=self.replay)
         self.steps += steps
 
     def step(self) -> None:
         q = self.learner.q_values(self.env)
-        self.env.step_egreedy(q, None, replay=self.replay,
-                              eps_schedule=(self.eps_decay, self.min_eps))
+        if self.track:
+            row = self.steps % self.history_len
+            self.h_s[row].copy_(self.env.board[:self.track])
+        self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward, done=self._done,
+                              action=self._action, eps_schedule=(self.eps_decay, self.min_eps))
+        if self.track:
+            self.h_a[row].copy_(self._action[:self.track])
+            self.h_r[row].copy_(self._reward[:self.track])
+            self.h_d[row].copy_(self._done[:self.track])
         self.steps += 1
         if self.steps * self.env.n >= self.min_fill:
             for _ in range(self.updates_per_step):
                 self.learner.update()
 
+    # ------------------------------------------------------------------ statistics
+    def collect_episodes(self, experiment=None) -> dict:
+        """Drain the device episode log (host sync).  With an Experiment, append one reference
+        add_episode dict per finished episode (src/experiments.py:112-122)."""
+        rec = self.log.read()
+        if experiment is not None and rec["step"].numel():
+            base = len(experiment.episodes)
+            experiment.add_episodes_from_log(rec, self.eps_decay, self.min_eps)
+            for j, (b, e) in enumerate(zip(rec["board"].tolist(), rec["episode"].tolist())):
+                self._numbers[(b, e)] = base + j
+        return rec
+
+    def game_histories(self) -> list:
+        """Complete games of the tracked boards still inside the history ring, as
+        (board, board_episode, [(state int64[4,4], 'u'|'d'|'l'|'r', reward), ...]) --
+        the board_history of src/dqn_lib.py:196-199."""
+        from .experiment import ACTION_LETTERS, real_state
+        if not self.track:
+            return []
+        T = self.history_len
+        lo = max(self.h_t0, self.steps - T)
+        rows = [t % T for t in range(lo, self.steps)]
+        s = self.h_s[rows].cpu().numpy()
+        a = self.h_a[rows].cpu().numpy()
+        r = self.h_r[rows].cpu().numpy()
+        d = self.h_d[rows].cpu().numpy()
+        ep = self.env.ep[:self.track, 0].cpu().numpy()
+        games = []
+        for j in range(self.track):
+            ends = [k for k in range(len(rows)) if d[k, j]]
+            n_done_after = len(ends)
+            # episode index of the first game ending in the window
+            first_ep = int(ep[j]) - n_done_after
+            start = 0 if (lo == self.h_t0 and self._clean[j]) else None
+            for g, k in enumerate(ends):
+                if start is not None:
+                    hist = [(real_state(s[t, j]), ACTION_LETTERS[int(a[t, j])], int(r[t, j]))
+                            for t in range(start, k + 1)]
+                    games.append((self.env.board_offset + j, first_ep + g, hist))
+                start = k + 1
+        return games
+
+    def snapshot_games(self, experiment) -> int:
+        """snapshot_game (src/experiments.py:124) of every complete tracked game, named by its
+        episode number in the experiment (collect_episodes first)."""
+        n = 0
+        for b, e, hist in self.game_histories():
+            num = self._numbers.get((b, e))
+            if num is not None:
+                experiment.snapshot_game(hist, num)
+                n += 1
+        return n
+
     def episode_stats(self) -> dict:
-        """Experiment.add_episode fields (src/experiments.py:112-122) over the last finished
-        episode of every board (host sync)."""
+        """Summary of the last finished episode of every board (host sync)."""
         ep = self.env.ep.to(torch.int64)
         fin = ep[:, 0] > 0
         if not bool(fin.any()):
@@ -235,6 +383,57 @@ class Trainer:
     def current_epsilon(self) -> torch.Tensor:
         e = self.env.ep[:, 0].to(torch.float64)
         return torch.clamp((self.eps_decay - e) / self.eps_decay, min=self.min_eps)
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def state_dict(self) -> dict:
+        cpu = lambda t: t.detach().cpu().clone()  # noqa: E731
+        env, rb = self.env, self.replay
+        st = {"trainer": {"steps": self.steps, "updates_per_step": self.updates_per_step,
+                          "min_fill": self.min_fill, "eps_decay": self.eps_decay,
+                          "min_eps": self.min_eps},
+              "env": {"n": env.n, "seed": env.seed, "board_offset": env.board_offset,
+                      "flags": env.flags, "epoch": env.epoch, "board": cpu(env.board),
+                      "meta": cpu(env.meta), "ep": cpu(env.ep)},
+              "replay": {"capacity": rb.capacity, "s": cpu(rb.s), "s2": cpu(rb.s2), "a": cpu(rb.a),
+                         "r": cpu(rb.r), "d": cpu(rb.d), "count": cpu(rb.count)},
+              "learner": self.learner.state_dict()}
+        if self.log is not None:
+            st["episode_log"] = {"capacity": self.log.capacity, "raw": cpu(self.log.raw),
+                                 "count": cpu(self.log.count), "qsum": cpu(self.log.qsum),
+                                 "read_upto": self.log.read_upto}
+        return st
+
+    @torch.no_grad()
+    def load_state_dict(self, st: dict) -> None:
+        env, rb = self.env, self.replay
+        e = st["env"]
+        for k in ("n", "seed", "board_offset", "flags"):
+            if e[k] != getattr(env, k):
+                raise ValueError(f"checkpoint env {k}={e[k]} != this env's {getattr(env, k)}")
+        if st["replay"]["capacity"] != rb.capacity:
+            raise ValueError("checkpoint replay capacity differs")
+        env.board.copy_(e["board"])
+        env.meta.copy_(e["meta"])
+        env.ep.copy_(e["ep"])
+        env.epoch = e["epoch"]
+        for k in ("s", "s2", "a", "r", "d", "count"):
+            getattr(rb, k).copy_(st["replay"][k])
+        if self.log is not None and "episode_log" in st:
+            lg = st["episode_log"]
+            if lg["capacity"] != self.log.capacity:
+                raise ValueError("checkpoint episode-log capacity differs")
+            self.log.raw.copy_(lg["raw"])
+            self.log.count.copy_(lg["count"])
+            self.log.qsum.copy_(lg["qsum"])
+            self.log.read_upto = int(lg["read_upto"])
+        t = st["trainer"]
+        self.steps = int(t["steps"])
+        self.updates_per_step, self.min_fill = int(t["updates_per_step"]), int(t["min_fill"])
+        self.eps_decay, self.min_eps = float(t["eps_decay"]), float(t["min_eps"])
+        self.learner.load_state_dict(st["learner"])
+        if self.track:
+            self.h_t0 = self.steps
+            self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
 
 
 def flops_per_update(net: str, batch: int) -> float:

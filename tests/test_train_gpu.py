@@ -1,0 +1,135 @@
+"""GPU tests of the device-resident training loop (g2048.train / Trainer): bit-exact resume
+from binary/checkpoint.pt, episode records and game snapshots in the reference's artefact
+format, checked against the device state and the oracle's move rule."""
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def G():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    import g2048
+    g2048.load_native()
+    from g2048 import train
+    return train
+
+
+def _small(G, net="conv", **kw):
+    args = dict(n_boards=1024, net=net, batch_size=256, replay_buffer_length=32 * 1024,
+                min_fill=2048, target_sync_every=5, no_episodes_to_reach_epsilon=4.0,
+                min_epsilon=0.05, seed=3, device=DEV, track_boards=2)
+    args.update(kw)
+    return G.build_trainer(**args)
+
+
+def _fingerprint(tr):
+    torch.cuda.synchronize()
+    L = tr.learner
+    return {"board": tr.env.board.cpu().clone(), "meta": tr.env.meta.cpu().clone(),
+            "ep": tr.env.ep.cpu().clone(), "replay_s": tr.replay.s.cpu().clone(),
+            "count": tr.replay.count.cpu().clone(), "log": tr.log.raw.cpu().clone(),
+            "params": [p.detach().cpu().clone() for p in L.model.parameters()],
+            "target": [p.detach().cpu().clone() for p in L.target.parameters()],
+            "loss": L.last_loss.cpu().clone()}
+
+
+@pytest.mark.parametrize("net", ["conv", "dense"])
+def test_resume_is_bit_exact(G, net, tmp_path):
+    a = _small(G, net)
+    for _ in range(12):
+        a.step()
+    state = a.state_dict()
+    from g2048.experiment import Experiment
+    exp = Experiment("ck", root=str(tmp_path))
+    exp.save_checkpoint(state)
+    for _ in range(9):
+        a.step()
+    want = _fingerprint(a)
+
+    b = _small(G, net)
+    b.load_state_dict(exp.load_checkpoint())
+    for _ in range(9):
+        b.step()
+    got = _fingerprint(b)
+    for k in ("board", "meta", "ep", "replay_s", "count", "log", "loss"):
+        assert torch.equal(got[k], want[k]), k
+    for x, y in zip(got["params"] + got["target"], want["params"] + want["target"]):
+        assert torch.equal(x, y)
+    assert b.learner.updates == a.learner.updates and b.steps == a.steps
+
+
+def test_load_rejects_mismatch(G):
+    a = _small(G, "conv")
+    st = a.state_dict()
+    b = _small(G, "conv", batch_size=128)
+    with pytest.raises(ValueError):
+        b.load_state_dict(st)
+    c = _small(G, "conv", seed=4)
+    with pytest.raises(ValueError):
+        c.load_state_dict(st)
+
+
+def _move_ok(s, a, s2, r, letters=("u", "d", "l", "r")):
+    """s2 follows s under action a: the oracle slide (+ one spawned 2/4) or no change."""
+    e = np.where(s > 0, np.log2(np.maximum(s, 1)), 0).astype(np.uint8).reshape(16)
+    e2 = np.where(s2 > 0, np.log2(np.maximum(s2, 1)), 0).astype(np.uint8).reshape(16)
+    slid, gain = O.move(e, letters.index(a))
+    if np.array_equal(slid, e):
+        return np.array_equal(e2, e) and r == 0
+    diff = np.nonzero(slid != e2)[0]
+    return (len(diff) == 1 and slid[diff[0]] == 0 and e2[diff[0]] in (1, 2) and r == gain)
+
+
+def test_training_loop_artefacts(G, tmp_path):
+    from g2048.experiment import Experiment, load_pickle
+    tr = _small(G, "conv", n_boards=512)
+    exp = Experiment("run", root=str(tmp_path))
+    exp.add_hyperparameter(G.hyperparameters(tr, 600, 50))
+    G.training_loop(tr, no_episodes=600, experiment=exp, snapshot_game_every_n_episodes=50,
+                    save_every_episodes=200, check_every=16, max_steps=4000)
+    eps = load_pickle(exp.folder, "episodes.p")
+    assert len(eps) >= 600 and [e["number"] for e in eps] == list(range(len(eps)))
+    # per board, the logged episodes agree with the env's own counters
+    ep = tr.env.ep.cpu().numpy()
+    per_board = {}
+    for e in eps:
+        per_board.setdefault(e["board"], []).append(e)
+    for b, lst in per_board.items():
+        assert [x["board_episode"] for x in lst] == list(range(len(lst)))
+        assert len(lst) == ep[b, 0]
+        last = lst[-1]
+        assert int(last["merge_score"]) == ep[b, 1] and last["number_moves"] == ep[b, 2]
+        assert int(last["max_tile"]) == 1 << ep[b, 3]
+    for e in eps:
+        assert e["reward"] == float(e["merge_score"]) / e["number_moves"]
+        assert e["epsilon"] == max((4.0 - e["board_episode"]) / 4.0, 0.05)
+    # snapshots: complete games of tracked boards, consistent move by move
+    hist_dir = os.path.join(exp.folder, "binary", "board_histories")
+    files = sorted(os.listdir(hist_dir))
+    assert files
+    by_num = {e["number"]: e for e in eps}
+    for fn in files:
+        num = int(fn[len("episode_"):-2])
+        hist = load_pickle(exp.folder, os.path.join("board_histories", fn))
+        e = by_num[num]
+        assert e["board"] in (0, 1) and len(hist) == e["number_moves"]
+        assert int(hist[-1][0].max()) == int(e["max_tile"])
+        assert sum(h[2] for h in hist) == int(e["merge_score"])
+        for k in range(len(hist) - 1):
+            assert _move_ok(hist[k][0], hist[k][1], hist[k + 1][0], hist[k][2]), (fn, k)
+    # resume from the folder continues from the checkpoint
+    exp2, tr2 = G.resume("run", root=str(tmp_path), net="conv", batch_size=256,
+                         min_fill=2048, target_sync_every=5, no_episodes_to_reach_epsilon=4.0,
+                         min_epsilon=0.05, device=DEV, track_boards=2)
+    assert tr2.steps == tr.steps and len(exp2.episodes) == len(eps)
+    assert torch.equal(tr2.env.board.cpu(), tr.env.board.cpu())
