@@ -101,14 +101,16 @@ G2048_API int g2048_env_reset(g2048_env* env, const uint8_t* reset_mask_dev, voi
 G2048_API int g2048_env_get_epoch(const g2048_env* env, uint32_t* epoch_out);
 G2048_API int g2048_env_set_epoch(g2048_env* env, uint32_t epoch);
 
-/* Attach (log_dev != NULL) or detach an episode log: every later terminal step of any step /
- * rollout call appends one g2048_episode at slot (count % capacity) (count_dev: u64, advanced
- * atomically -- records of one launch land in arbitrary order; sort by (step, board)).
+/* Attach (log_dev != NULL) or detach an episode log: on every later terminal step of any step /
+ * rollout call, board i writes its episode e as a g2048_episode into slot i*S + (e % S) of
+ * log_dev [n][S] (S = slots_per_board; no atomics, so the layout is deterministic).  A reader
+ * that remembers each board's episode count (ep[i][0]) at its last read finds the new records
+ * in those slots, as long as no board finished more than S episodes in between.
  * qsum_dev f64[n] holds each board's running max-Q sum (zero it before attaching).  With
  * G2048_NO_AUTORESET a board that stays terminal logs again on every step.  Replaces the
  * per-episode bookkeeping of training_loop (src/dqn_lib.py:184-213). */
-G2048_API int g2048_env_set_episode_log(g2048_env* env, g2048_episode* log_dev, int64_t capacity,
-                                        uint64_t* count_dev, double* qsum_dev);
+G2048_API int g2048_env_set_episode_log(g2048_env* env, g2048_episode* log_dev,
+                                        int64_t slots_per_board, double* qsum_dev);
 
 /* Legal-move mask of every current board: available_moves_as_torch_unit_vector
  * (src/board.py:128-135) as bits (bit a = move a changes the board). */

@@ -29,7 +29,7 @@ class _Env(C.Structure):
     _fields_ = [("n", C.c_int64), ("board_offset", C.c_uint64), ("seed", C.c_uint64),
                 ("flags", C.c_uint32), ("board", C.c_void_p), ("meta", C.c_void_p),
                 ("ep", C.c_void_p), ("qsum", C.c_void_p), ("log", C.c_void_p),
-                ("log_cap", C.c_int64), ("log_count", C.c_void_p)]
+                ("log_slots", C.c_int64)]
 
 
 # g2048_episode / o2048_episode (40 bytes)
@@ -149,26 +149,28 @@ class OracleEnv:
         self.ep = np.zeros((n, 4), np.uint32)
         self.epoch = 0
         self._c = _Env(n, board_offset, seed, flags, _p(self.board), _p(self.meta), _p(self.ep),
-                       None, None, 0, None)
+                       None, None, 0)
         if reset:
             self.reset()
 
-    def attach_episode_log(self, capacity: int):
-        """Append one EPISODE_DTYPE record per finished episode (g2048_env_set_episode_log)."""
-        self.log = np.zeros(capacity, EPISODE_DTYPE)
-        self.log_count = np.zeros(1, np.uint64)
+    def attach_episode_log(self, slots: int):
+        """One EPISODE_DTYPE record per finished episode in per-board slot rings [n][slots]
+        (g2048_env_set_episode_log)."""
+        self.log = np.zeros((self.n, slots), EPISODE_DTYPE)
         self.qsum = np.zeros(self.n, np.float64)
-        self._c.qsum, self._c.log = _p(self.qsum), self.log.ctypes.data
-        self._c.log_cap, self._c.log_count = capacity, _p(self.log_count)
+        self._c.qsum, self._c.log, self._c.log_slots = _p(self.qsum), self.log.ctypes.data, slots
+        self._log_read = np.zeros(self.n, np.int64)
 
     def episodes(self):
-        """Logged records so far (ring order = append order), as a structured array."""
-        n = int(self.log_count[0])
-        cap = len(self.log)
-        if n <= cap:
-            return self.log[:n].copy()
-        k = n % cap
-        return np.concatenate([self.log[k:], self.log[:k]])
+        """Records of the episodes finished since the last call, sorted by (step, board)."""
+        now = self.ep[:, 0].astype(np.int64)
+        S = self.log.shape[1]
+        if (now - self._log_read > S).any():
+            raise RuntimeError("oracle episode log overflow")
+        out = [self.log[b, e % S] for b in range(self.n) for e in range(self._log_read[b], now[b])]
+        self._log_read = now
+        r = np.array(out, EPISODE_DTYPE)
+        return r[np.lexsort((r["board"], r["step"]))] if len(r) else r
 
     def reset(self, mask=None):
         m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)

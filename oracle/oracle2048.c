@@ -303,7 +303,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             uint8_t mx = 0;
             for (int k = 0; k < 16; ++k) if (b[k] > mx) mx = b[k];
             if (e->log) {  /* experiments.py:112-122 add_episode, one record per episode */
-                o2048_episode* rec = e->log + (int64_t)(*e->log_count % (uint64_t)e->log_cap);
+                o2048_episode* rec = e->log + i * e->log_slots + (int64_t)(ep[0] % (uint32_t)e->log_slots);
                 rec->step = t;
                 rec->q_sum = qs;
                 rec->board = (uint32_t)gid;
@@ -312,7 +312,6 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
                 rec->moves = m[1];
                 rec->max_exp = mx;
                 rec->reserved = 0;
-                *e->log_count += 1;
             }
             qs = 0.0;
             ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;

@@ -53,9 +53,8 @@ typedef struct {
     uint32_t* meta;          /* [n][4]  */
     uint32_t* ep;            /* [n][4]  */
     double* qsum;            /* [n] running max-Q sum, or NULL (episode log off) */
-    o2048_episode* log;      /* episode log ring, appended in board order, or NULL */
-    int64_t log_cap;
-    uint64_t* log_count;
+    o2048_episode* log;      /* [n][log_slots]: board i's episode e at i*S + e%S, or NULL */
+    int64_t log_slots;
 } o2048_env;
 
 typedef struct {

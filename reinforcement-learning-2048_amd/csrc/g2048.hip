@@ -7,8 +7,9 @@
 //   meta  u32[N][4]   {score, moves, steps_lo, steps_hi}
 //   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (touched on done only)
 // Replay ring (capacity C): s u8[C][16], s2 u8[C][16], a u8[C], r i32[C], d u8[C], count u64.
-// Optional episode log (g2048_env_set_episode_log): ring of g2048_episode records appended on
-// every terminal step + qsum f64[N] (running sum of max_a Q over the board's episode).
+// Optional episode log (g2048_env_set_episode_log): g2048_episode records [N][S], board i's
+// episode e in slot i*S + e%S, written on its terminal step + qsum f64[N] (running sum of
+// max_a Q over the board's episode).
 //
 // One lane owns one board for the whole launch: load board + meta (2 x dwordx4), do the
 // legal-mask / select / slide / spawn / reset arithmetic in VGPRs (g2048_board.hpp), store them
@@ -69,10 +70,9 @@ struct StepArgs {
     ReplayDev rb;
     int k_steps;
     long long* reward_sum;
-    g2048_episode* log;  // episode log ring (NULL = off)
-    int64_t log_cap;
-    unsigned long long* log_count;
-    double* qsum;  // per-board running sum of max Q (NULL = off)
+    g2048_episode* log;  // per-board episode slot rings [n][log_slots] (NULL = off)
+    int64_t log_slots;
+    double* qsum;        // per-board running sum of max Q (NULL = off)
 };
 
 __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v.y, v.z, v.w}; }
@@ -142,28 +142,41 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         A.rb.d[slot] = (uint8_t)done;
     }
 
+    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
+    uint32_t ep_idx = 0u, mx = 0u, fin_score = 0u, fin_moves = 0u;
     if (done) {
         const uint4 e0 = A.ep[i];
-        const uint32_t mx = max_exp(b);
+        mx = max_exp(b);
         A.ep[i] = make_uint4(e0.x + 1u, m.x, m.y, mx);
-        if (A.log) {  // Experiment.add_episode (src/experiments.py:112-122), one record per episode
-            const unsigned long long k = atomicAdd(A.log_count, 1ull);
-            g2048_episode rec;
-            rec.step = t;
-            rec.q_sum = qs;
-            rec.board = (uint32_t)gid;
-            rec.episode = e0.x;
-            rec.score = m.x;
-            rec.moves = m.y;
-            rec.max_exp = mx;
-            rec.reserved = 0u;
-            A.log[(int64_t)(k % (unsigned long long)A.log_cap)] = rec;
+        ep_idx = e0.x;
+        fin_score = m.x;
+        fin_moves = m.y;
+        if constexpr (!kGreedy) {  // non-greedy steps add 0 to the sum: touch it on done only
+            if (A.qsum) qs = A.qsum[i];
         }
-        qs = 0.0;
         if (!(A.flags & G2048_NO_AUTORESET)) {
             b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m.x = 0u;
             m.y = 0u;
+        }
+    }
+    if (done && A.log) {  // Experiment.add_episode (src/experiments.py:112-122): one record per
+                          // episode, in the board's own slot ring (no atomics, fixed order)
+        g2048_episode rec;
+        rec.step = t;
+        rec.q_sum = qs;
+        rec.board = (uint32_t)gid;
+        rec.episode = ep_idx;
+        rec.score = fin_score;
+        rec.moves = fin_moves;
+        rec.max_exp = mx;
+        rec.reserved = 0u;
+        A.log[i * A.log_slots + (int64_t)(ep_idx % (uint32_t)A.log_slots)] = rec;
+    }
+    if (done) {
+        qs = 0.0;
+        if constexpr (!kGreedy) {
+            if (A.qsum) A.qsum[i] = 0.0;
         }
     }
     const uint64_t t1 = t + 1u;
@@ -198,11 +211,12 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     }
     int32_t rew;
     uint32_t done, legal, act;
-    double qs = A.qsum ? A.qsum[i] : 0.0;
+    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
+    double qs = (kGreedy && A.qsum) ? A.qsum[i] : 0.0;  // other modes: step_one, on done only
     step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
-    if (A.qsum) A.qsum[i] = qs;
+    if (kGreedy && A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
     if (A.legal_out) A.legal_out[i] = (uint8_t)legal;
@@ -218,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     uint4 m = A.meta[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
     long long rsum = 0;
-    double qs = A.qsum ? A.qsum[i] : 0.0;
+    double qs = 0.0;  // random policy: the running sum is read / cleared on done only
     for (int s = 0; s < A.k_steps; ++s) {
         int32_t rew;
         uint32_t done, legal, act;
@@ -227,7 +241,6 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     }
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
-    if (A.qsum) A.qsum[i] = qs;
     if (A.reward_sum) A.reward_sum[i] += rsum;
     if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
 }
@@ -373,8 +386,7 @@ struct g2048_env {
     bool owns = false;
     uint32_t epoch = 0;
     g2048_episode* log = nullptr;
-    int64_t log_cap = 0;
-    unsigned long long* log_count = nullptr;
+    int64_t log_slots = 0;
     double* qsum = nullptr;
 };
 
@@ -423,8 +435,7 @@ int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
     A.flags = e->flags;
     A.err = e->err;
     A.log = e->log;
-    A.log_cap = e->log_cap;
-    A.log_count = e->log_count;
+    A.log_slots = e->log_slots;
     A.qsum = e->qsum;
     if (rb) {
         if (rb->device != e->device)
@@ -578,15 +589,15 @@ int g2048_env_set_epoch(g2048_env* e, uint32_t epoch) {
     return G2048_OK;
 }
 
-int g2048_env_set_episode_log(g2048_env* e, g2048_episode* log, int64_t capacity,
-                              uint64_t* count, double* qsum) {
+int g2048_env_set_episode_log(g2048_env* e, g2048_episode* log, int64_t slots_per_board,
+                              double* qsum) {
     if (!e) return fail(G2048_EINVAL, "env_set_episode_log: NULL env");
-    if (log && (capacity <= 0 || !count || !qsum || ((uintptr_t)log & 7u) || ((uintptr_t)qsum & 7u)))
+    if (log && (slots_per_board <= 0 || slots_per_board > (1 << 20) || !qsum ||
+                ((uintptr_t)log & 7u) || ((uintptr_t)qsum & 7u)))
         return fail(G2048_EINVAL,
-                    "env_set_episode_log: need capacity > 0, count and qsum, 8-byte alignment");
+                    "env_set_episode_log: need 0 < slots_per_board <= 2^20, qsum, 8-byte alignment");
     e->log = log;
-    e->log_cap = log ? capacity : 0;
-    e->log_count = log ? reinterpret_cast<unsigned long long*>(count) : nullptr;
+    e->log_slots = log ? slots_per_board : 0;
     e->qsum = log ? qsum : nullptr;
     return G2048_OK;
 }

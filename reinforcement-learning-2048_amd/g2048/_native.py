@@ -38,7 +38,7 @@ SIGNATURES = {
     "g2048_env_error_count": (_int, [_vp, C.POINTER(C.c_int64), _vp]),
     "g2048_env_get_epoch": (_int, [_vp, C.POINTER(C.c_uint32)]),
     "g2048_env_set_epoch": (_int, [_vp, _u32]),
-    "g2048_env_set_episode_log": (_int, [_vp, _vp, _i64, _vp, _vp]),
+    "g2048_env_set_episode_log": (_int, [_vp, _vp, _i64, _vp]),
     "g2048_env_legal_mask": (_int, [_vp, _vp, _vp]),
     "g2048_replay_create": (_int, [_pp, _i64, _int, _vp]),
     "g2048_replay_wrap": (_int, [_pp, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp]),

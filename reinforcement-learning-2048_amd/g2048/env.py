@@ -23,7 +23,7 @@ EPISODE_FIELDS = ("step", "q_sum", "board", "episode", "score", "moves", "max_ex
 
 def decode_episodes(raw: torch.Tensor) -> dict:
     """int64 [k, 5] records -> dict of int64 / float64 host tensors, sorted by (step, board)
-    (records of one launch are appended in arbitrary order)."""
+    (the completion order; ties within one step broken by board id)."""
     raw = raw.cpu()
     lo = raw[:, 2:5] & 0xFFFFFFFF
     hi = (raw[:, 2:5] >> 32) & 0xFFFFFFFF
@@ -35,42 +35,54 @@ def decode_episodes(raw: torch.Tensor) -> dict:
 
 
 class EpisodeLog:
-    """Device ring of finished-episode records, appended by the step kernels themselves
-    (g2048_env_set_episode_log) -- the per-episode bookkeeping of training_loop
-    (src/dqn_lib.py:184-213) and Experiment.add_episode (src/experiments.py:112-122) without a
-    host round trip per step.  `read()` returns the records appended since the last read."""
+    """Per-board rings of finished-episode records, written by the step kernels themselves
+    (g2048_env_set_episode_log: board i's episode e lands in slot i*S + e%S) -- the per-episode
+    bookkeeping of training_loop (src/dqn_lib.py:184-213) and Experiment.add_episode
+    (src/experiments.py:112-122) with no host round trip and no atomics per step.  `read()`
+    gathers the records of episodes finished since the last read, using the env's own per-board
+    episode counters (ep[:, 0])."""
 
-    def __init__(self, env: "VecEnv2048", capacity: int):
+    def __init__(self, env: "VecEnv2048", slots_per_board: int = 8):
         self.env = env
-        self.capacity = int(capacity)
+        self.slots = int(slots_per_board)
         kw = dict(device=env.device)
-        self.raw = torch.zeros((self.capacity, 5), dtype=torch.int64, **kw)
-        self.count = torch.zeros(1, dtype=torch.int64, **kw)
+        self.raw = torch.zeros((env.n, self.slots, 5), dtype=torch.int64, **kw)
         self.qsum = torch.zeros(env.n, dtype=torch.float64, **kw)
-        self.read_upto = 0
-        N.check(N.load().g2048_env_set_episode_log(env.handle, N.ptr(self.raw), self.capacity,
-                                                   N.ptr(self.count), N.ptr(self.qsum)),
-                "g2048_env_set_episode_log")
+        self.read_ep = env.ep[:, 0].to(torch.int64)   # episodes already accounted for
+        self.ep0 = self.read_ep.clone()               # at attach time
+        N.check(N.load().g2048_env_set_episode_log(env.handle, N.ptr(self.raw), self.slots,
+                                                   N.ptr(self.qsum)), "g2048_env_set_episode_log")
 
     def detach(self) -> None:
-        N.check(N.load().g2048_env_set_episode_log(self.env.handle, None, 0, None, None),
+        N.check(N.load().g2048_env_set_episode_log(self.env.handle, None, 0, None),
                 "g2048_env_set_episode_log")
 
-    def total(self) -> int:  # host sync
-        return int(self.count.item())
+    def total(self) -> int:
+        """Episodes finished since the log was attached (host sync)."""
+        return int((self.env.ep[:, 0].to(torch.int64) - self.ep0).sum())
 
     def read(self, strict: bool = True) -> dict:
-        """Records appended since the last read (host sync).  strict: raise if the ring wrapped
-        past unread records (raise the capacity or read more often)."""
-        n = self.total()
-        lost = n - self.read_upto - self.capacity
-        if lost > 0:
+        """Records of the episodes finished since the last read, sorted by (step, board) (host
+        sync).  strict: raise if a board finished more than `slots` episodes since the last read
+        (older records were overwritten; read more often or attach more slots)."""
+        now = self.env.ep[:, 0].to(torch.int64)
+        cnt = now - self.read_ep
+        over = int(cnt.max()) - self.slots if cnt.numel() else 0
+        if over > 0:
             if strict:
-                raise RuntimeError(f"episode log overflow: {lost} records lost")
-            self.read_upto = n - self.capacity
-        idx = torch.arange(self.read_upto, n, device=self.raw.device) % self.capacity
-        self.read_upto = n
-        return decode_episodes(self.raw[idx])
+                raise RuntimeError(f"episode log overflow: a board finished {over} episodes more "
+                                   f"than its {self.slots} slots since the last read")
+            cnt = cnt.clamp(max=self.slots)
+        first = now - cnt
+        self.read_ep = now
+        total = int(cnt.sum())
+        if total == 0:
+            return decode_episodes(self.raw.new_zeros((0, 5)))
+        boards = torch.repeat_interleave(torch.arange(self.env.n, device=cnt.device), cnt)
+        starts = torch.cumsum(cnt, 0) - cnt
+        k = torch.arange(total, device=cnt.device) - torch.repeat_interleave(starts, cnt)
+        ep = first[boards] + k
+        return decode_episodes(self.raw[boards, ep % self.slots])
 
 
 class VecEnv2048:
@@ -134,8 +146,8 @@ class VecEnv2048:
     def epoch(self, value: int) -> None:
         N.check(N.load().g2048_env_set_epoch(self._h, int(value)), "g2048_env_set_epoch")
 
-    def attach_episode_log(self, capacity: int = 1 << 20) -> EpisodeLog:
-        self.episode_log = EpisodeLog(self, capacity)
+    def attach_episode_log(self, slots_per_board: int = 8) -> EpisodeLog:
+        self.episode_log = EpisodeLog(self, slots_per_board)
         return self.episode_log
 
     def legal_mask(self, out: torch.Tensor | None = None) -> torch.Tensor:

@@ -264,7 +264,7 @@ class Trainer:
     def __init__(self, env: VecEnv2048, replay: ReplayBuffer, learner: DQNLearner,
                  updates_per_step: int = 1, min_fill: int | None = None,
                  eps_decay_episodes: float = 1000.0, min_epsilon: float = 0.01,
-                 episode_log_capacity: int = 1 << 20, track_boards: int = 0,
+                 episode_log_slots: int = 8, track_boards: int = 0,
                  history_len: int = 4096):
         self.env, self.replay, self.learner = env, replay, learner
         self.updates_per_step = int(updates_per_step)
@@ -272,7 +272,7 @@ class Trainer:
         self.eps_decay = float(eps_decay_episodes)
         self.min_eps = float(min_epsilon)
         self.steps = 0
-        self.log = env.attach_episode_log(episode_log_capacity) if episode_log_capacity else None
+        self.log = env.attach_episode_log(episode_log_slots) if episode_log_slots else None
         self.track = int(min(track_boards, env.n))
         self.history_len = int(history_len)
         if self.track:
@@ -398,9 +398,9 @@ class Trainer:
                          "r": cpu(rb.r), "d": cpu(rb.d), "count": cpu(rb.count)},
               "learner": self.learner.state_dict()}
         if self.log is not None:
-            st["episode_log"] = {"capacity": self.log.capacity, "raw": cpu(self.log.raw),
-                                 "count": cpu(self.log.count), "qsum": cpu(self.log.qsum),
-                                 "read_upto": self.log.read_upto}
+            st["episode_log"] = {"slots": self.log.slots, "raw": cpu(self.log.raw),
+                                 "qsum": cpu(self.log.qsum), "read_ep": cpu(self.log.read_ep),
+                                 "ep0": cpu(self.log.ep0)}
         return st
 
     @torch.no_grad()
@@ -420,12 +420,12 @@ class Trainer:
             getattr(rb, k).copy_(st["replay"][k])
         if self.log is not None and "episode_log" in st:
             lg = st["episode_log"]
-            if lg["capacity"] != self.log.capacity:
-                raise ValueError("checkpoint episode-log capacity differs")
+            if lg["slots"] != self.log.slots:
+                raise ValueError("checkpoint episode-log slots differ")
             self.log.raw.copy_(lg["raw"])
-            self.log.count.copy_(lg["count"])
             self.log.qsum.copy_(lg["qsum"])
-            self.log.read_upto = int(lg["read_upto"])
+            self.log.read_ep.copy_(lg["read_ep"])
+            self.log.ep0.copy_(lg["ep0"])
         t = st["trainer"]
         self.steps = int(t["steps"])
         self.updates_per_step, self.min_fill = int(t["updates_per_step"]), int(t["min_fill"])

@@ -29,7 +29,7 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
                   use_double_dqn: bool = True, target_sync_every: int = 100,
                   no_episodes_to_reach_epsilon: float = 1000.0, min_epsilon: float = 0.01,
                   updates_per_step: int = 1, min_fill: int | None = None, seed: int = 0,
-                  device="cuda:0", track_boards: int = 1, episode_log_capacity: int = 1 << 20,
+                  device="cuda:0", track_boards: int = 1, episode_log_slots: int = 8,
                   graph: bool = True, board_offset: int = 0, process_group=None) -> Trainer:
     cap = max(n_boards, (replay_buffer_length // n_boards) * n_boards)  # multiple of n
     env = VecEnv2048(n_boards, seed=0x2048 + seed, device=device, board_offset=board_offset)
@@ -40,7 +40,7 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
                          graph=graph, seed=seed, process_group=process_group)
     return Trainer(env, replay, learner, updates_per_step=updates_per_step, min_fill=min_fill,
                    eps_decay_episodes=no_episodes_to_reach_epsilon, min_epsilon=min_epsilon,
-                   episode_log_capacity=episode_log_capacity, track_boards=track_boards)
+                   episode_log_slots=episode_log_slots, track_boards=track_boards)
 
 
 def hyperparameters(trainer: Trainer, no_episodes: int, snapshot_game_every_n_episodes: int):
@@ -115,7 +115,7 @@ def resume(folder_name: str, root: str = ".", **build_kwargs):
     e = state["env"]
     tr = build_trainer(n_boards=e["n"], seed=e["seed"] - 0x2048, board_offset=e["board_offset"],
                        replay_buffer_length=state["replay"]["capacity"],
-                       episode_log_capacity=state.get("episode_log", {}).get("capacity", 1 << 20),
+                       episode_log_slots=state.get("episode_log", {}).get("slots", 8),
                        **build_kwargs)
     tr.load_state_dict(state)
     exp.model = tr.learner.model

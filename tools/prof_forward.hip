@@ -47,6 +47,29 @@ __global__ __launch_bounds__(256) void k_mfma_cal(float* out, unsigned long long
                 v4 = fmaf(v4, 1.0001f, 0.25f);
             }
             a += v0 + v1 + v2 + v3 + v4;
+        } else if (chains >= 5) {  // 16x16x4 on 4 accumulators (x2 count: same FLOPs); 6: + 1 VALU
+            f32x4 d0 = f32x4{0}, d1 = d0, d2 = d0, d3 = d0;
+            float v0 = a, v1 = b, v2 = a + b, v3 = a - b;
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
+                if (chains == 6) v0 = fmaf(v0, 1.0001f, 0.5f);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
+                if (chains == 6) v1 = fmaf(v1, 1.0001f, 0.5f);
+                d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, d2, 0, 0, 0);
+                if (chains == 6) v2 = fmaf(v2, 1.0001f, 0.5f);
+                d3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, d3, 0, 0, 0);
+                if (chains == 6) v3 = fmaf(v3, 1.0001f, 0.5f);
+                d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
+                if (chains == 6) v0 = fmaf(v0, 1.0001f, 0.5f);
+                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
+                if (chains == 6) v1 = fmaf(v1, 1.0001f, 0.5f);
+                d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, d2, 0, 0, 0);
+                if (chains == 6) v2 = fmaf(v2, 1.0001f, 0.5f);
+                d3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, d3, 0, 0, 0);
+                if (chains == 6) v3 = fmaf(v3, 1.0001f, 0.5f);
+            }
+            for (int i = 0; i < 4; ++i) c0[i] = d0[i] + d1[i] + d2[i] + d3[i] + v0 + v1 + v2 + v3;
         } else {
 #pragma unroll
             for (int j = 0; j < 32; ++j) {
@@ -70,7 +93,7 @@ int main(int argc, char** argv) {
         unsigned long long* cyc;
         (void)hipMalloc(&o, 256 * 256 * 4);
         (void)hipMalloc(&cyc, 64);
-        for (int chains = 2; chains <= 4; ++chains) {
+        for (int chains = 2; chains <= 6; ++chains) {
             hipEvent_t e0, e1;
             (void)hipEventCreate(&e0);
             (void)hipEventCreate(&e1);
@@ -83,7 +106,7 @@ int main(int argc, char** argv) {
             (void)hipEventElapsedTime(&ms, e0, e1);
             unsigned long long h[4];
             (void)hipMemcpy(h, cyc, 32, hipMemcpyDeviceToHost);
-            printf("mfma cal chains=%d: 2048 MFMAs/wave: memtime %llu %llu %llu %llu, %.2f us "
+            printf("mfma cal mode=%d: 2048 32x32x2-equiv/wave: memtime %llu %llu %llu %llu, %.2f us "
                    "(%.1f TF)\n", chains, h[0], h[1], h[2], h[3], ms * 1e3,
                    256.0 * 4 * 2048 * 4096 / (ms * 1e-3) / 1e12);
         }

@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Fused eps-greedy step variants at 64k boards (events over a 200-launch graph): scalar eps,
+per-board schedule, schedule + episode log."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "reinforcement-learning-2048_amd")]
+import torch  # noqa: E402
+
+import g2048  # noqa: E402
+
+DEV = "cuda:0"
+N = 65536
+
+
+def run(variant, steps=200):
+    env = g2048.VecEnv2048(N, seed=1, device=DEV)
+    rb = g2048.ReplayBuffer(16 * N, device=DEV)
+    if variant == "log":
+        env.attach_episode_log(8)
+    q = torch.randn((N, 4), device=DEV)
+    kw = dict(eps_schedule=(1000.0, 0.01)) if variant != "scalar" else {}
+    outs = (torch.empty(N, dtype=torch.int32, device=DEV), torch.empty(N, dtype=torch.uint8, device=DEV),
+            torch.empty(N, dtype=torch.uint8, device=DEV))
+    def step():
+        env.step_egreedy(q, 0.1, replay=rb, reward=outs[0], done=outs[1], action=outs[2], **kw)
+    for _ in range(20):
+        step()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(steps):
+                step()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    g.replay()
+    a.record()
+    for _ in range(5):
+        g.replay()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) * 1e3 / (5 * steps)
+
+
+print(json.dumps({v: round(run(v), 3) for v in ("scalar", "schedule", "log")}))
