@@ -178,6 +178,23 @@ def bench_env(args, world, rank, dev):
     return dict(wall=wall_max, ev_s=ev_s, single_launch_s=single, n=n, G=G)
 
 
+def launch_floor(n: int, dev, G: int = 100, reps: int = 20) -> float:
+    """Per-launch time of a graph-replayed device copy of the step's board + meta bytes (32 B in,
+    32 B out per board): the floor any one-launch-per-step kernel over n boards pays here."""
+    src = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    g = capture(lambda: dst.copy_(src), G)
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        g.replay()
+    b.record()
+    b.synchronize()
+    return a.elapsed_time(b) / 1e3 / (G * reps)
+
+
 def bench_rollout(args, world, rank, dev):
     """K random steps per launch with fused replay append (replay pre-fill path)."""
     import g2048
@@ -288,6 +305,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args)
     traffic, traffic_src = pmc_traffic("k_step", r["n"])
+    floor_s = launch_floor(r["n"], dev)
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -313,7 +331,10 @@ def main():
                          "kernel": "k_step<MODE_RANDOM>",
                          "bytes_per_launch": STEP_BYTES * r["n"],
                          "launch_us_graph": per_step_s * 1e6,
-                         "launch_us_single_eager": r["single_launch_s"] * 1e6},
+                         "launch_us_single_eager": r["single_launch_s"] * 1e6,
+                         # at 64k boards the step is bound by the launch floor, not by HBM:
+                         "launch_floor_us": floor_s * 1e6,
+                         "floor_frac": floor_s / per_step_s},
             "cpu_baseline": cpu,
         }
         if ro:

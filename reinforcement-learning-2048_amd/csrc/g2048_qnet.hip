@@ -237,40 +237,40 @@ __global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Persistent variant for large n (the rollout's Q over all boards): a workgroup stages both big
-// weight matrices once (W2, fc1_w: 130 KB of LDS) and loops over tiles of 16 boards.
+// Persistent variant for large n (the rollout's Q over all boards): 256 workgroups (one per CU)
+// stage W2 once and loop over tiles of 16 boards; each wave keeps its 16-unit slice of fc1_w in
+// 64 VGPRs (fc1's B operand), which leaves LDS room for h1.
 //
-// On gfx950 f32 MFMA runs at the f32 VALU rate and VALU issued between MFMAs mostly adds to their
-// time, so the layout minimises VALU in the MFMA stream:
+// On gfx950 a VALU op between f32 MFMAs is not hidden (tools/prof_forward.hip: +4 cycles per op,
+// ~12 when the ops form dependent chains), so the MFMA loops carry no VALU at all:
+//  * conv1 runs as its own phase: thread (channel c = t&63, board group t>>6) computes its
+//    channel at the 9 positions of 4 boards -- 36 independent fma chains -- into
+//    h1[c][board*9 + pos] (channel stride 145 = 17 mod 64: conflict-free writes and reads);
 //  * conv2 is split by ROWS: wave w owns boards 4w..4w+3 (16 rows (s, q)) x all 64 channels as
-//    four 16x16x4 tiles sharing one A operand.  Lane group g = lane>>4 is conv2's tap
-//    (kh, kw) = (g>>1, g&1) and step c is conv1's channel, so k = 4c + g is exactly conv2's
-//    flat weight index.  The A value (conv1 output of channel c at the lane's position) is
-//    recomputed in registers from the lane's four input cells -- two channels per packed
-//    v_pk_fma_f32 chain, ~0.75 VALU per MFMA -- and feeds four MFMAs.
-//  * B comes as one ds_read_b128 per step (the lane's four N-tiles are adjacent in W2s).
-//  * fc1 reads A (h2) and B (fc1_w) as ds_read_b128 along k; fc2 uses all 256 threads.
-// Reduction order differs from the tile kernel (fp32 rounding only; same math).
+//    four 16x16x4 tiles.  Lane group g = lane>>4 is the tap (kh, kw) = (g>>1, g&1) and step c is
+//    the input channel, so k = 4c + g is conv2's flat weight index.  Per step: one ds_read_b32
+//    of h1 (A, shared by the four tiles) + one ds_read_b128 of W2 (B) -> 4 MFMAs;
+//  * fc1: A = h2 read along k as ds_read_b128, B = the wave's fc1_w slice in registers;
+//  * fc2 uses all 256 threads.
+// The summation order equals the tile kernel's per-row order (fp32 rounding identical per op).
 namespace persist {
 constexpr int S = 16;
+constexpr int H1S = 145;  // floats per channel of h1: [c][board*9 + pos], 16*9 = 144 used
 constexpr int H2S = 260;  // h2[s][k'], k' = q*64 + n (fc1's input index permuted)
-constexpr int WF1S = 260;  // WF1s[j][k']
 constexpr int FS = 68;    // fa[s][j] (16-byte aligned rows for fc2's b128 reads)
 constexpr int WF2S = 68;  // swf2[a][j]
 constexpr int OFF_X = 0;                          // [S][16]
-constexpr int OFF_W1T = OFF_X + S * 16;           // w1t[t][c]  (t = 2*ty + tx)
-constexpr int OFF_B1 = OFF_W1T + 256;             // 64
-constexpr int OFF_B2 = OFF_B1 + 64;               // 64
+constexpr int OFF_B2 = OFF_X + S * 16;            // 64
 constexpr int OFF_BF1 = OFF_B2 + 64;              // 64
 constexpr int OFF_WF2 = OFF_BF1 + 64;             // [4][WF2S]
 constexpr int OFF_BF2 = OFF_WF2 + 4 * WF2S;       // 4
 constexpr int OFF_W2 = OFF_BF2 + 4;               // W2s[k][16 x 4] swizzled, see w2s_index
-constexpr int OFF_WF1 = OFF_W2 + 256 * 64;
-constexpr int OFF_H2 = OFF_WF1 + 64 * WF1S;
+constexpr int OFF_H1 = OFF_W2 + 256 * 64;
+constexpr int OFF_H2 = (OFF_H1 + 64 * H1S + 3) & ~3;  // 16-byte aligned
 constexpr int OFF_F = OFF_H2 + S * H2S;
 constexpr int FLOATS = OFF_F + S * FS;
-static_assert(OFF_W2 % 4 == 0 && OFF_WF1 % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 &&
-                  OFF_WF2 % 4 == 0 && OFF_W1T % 4 == 0 && OFF_B1 % 4 == 0,
+static_assert(OFF_W2 % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 && OFF_WF2 % 4 == 0 &&
+                  OFF_X % 4 == 0,
               "b128 alignment");
 static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget (persistent forward)");
 // W2s row k holds w2[16nt + j][k] at 4*(j ^ (k & 15)) + nt: a lane group reads 16 distinct
@@ -281,7 +281,7 @@ __device__ __forceinline__ int w2s_index(int k, int j, int nt) {
 }  // namespace persist
 
 #ifdef G2048_PHASE_PROF
-__device__ unsigned long long g_phase[4][8];
+__device__ unsigned long long g_phase[4][10];
 #define PHASE(k)                                                          \
     do {                                                                  \
         const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
@@ -292,48 +292,57 @@ __device__ unsigned long long g_phase[4][8];
 #define PHASE(k) do {} while (0)
 #endif
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
     namespace P = persist;
 #ifdef G2048_PHASE_PROF
-    unsigned long long ph[8] = {0}, ph_last = __builtin_amdgcn_s_memtime();
+    unsigned long long ph[10] = {0}, ph_last = __builtin_amdgcn_s_memtime();
 #endif
     __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
     float* xs = lds + P::OFF_X;
-    float* w1t = lds + P::OFF_W1T;
-    float* sb1 = lds + P::OFF_B1;
     float* sb2 = lds + P::OFF_B2;
     float* sbf1 = lds + P::OFF_BF1;
     float* swf2 = lds + P::OFF_WF2;
     float* sbf2 = lds + P::OFF_BF2;
     float* w2s = lds + P::OFF_W2;
-    float* wf1s = lds + P::OFF_WF1;
+    float* h1 = lds + P::OFF_H1;
     float* h2 = lds + P::OFF_H2;
     float* fa = lds + P::OFF_F;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
 
-    // ---- stage everything once (coalesced global reads)
-    w1t[(t & 3) * 64 + (t >> 2)] = A.w1[t];  // w1[c][0][ty][tx], t = 4c + 2ty + tx
+    // ---- stage W2 and the small tensors once (coalesced global reads); registers for the rest
     if (t < 64) {
-        sb1[t] = A.b1[t];
         sb2[t] = A.b2[t];
         sbf1[t] = A.bf1[t];
     }
     swf2[(t >> 6) * P::WF2S + (t & 63)] = A.wf2[t];
     if (t < 4) sbf2[t] = A.bf2[t];
 #pragma unroll 4
-    for (int i = 0; i < 64; ++i) {
-        // w2[n][k] (n = i, k = t) -> W2s;  fc1_w[j][c'*4 + q] (j = i) -> WF1s[j][q*64 + c']
-        w2s[P::w2s_index(t, i & 15, i >> 4)] = A.w2[i * NT + t];
-        wf1s[i * P::WF1S + (t & 3) * 64 + (t >> 2)] = A.wf1[i * NT + t];
+    for (int i = 0; i < 64; ++i) w2s[P::w2s_index(t, i & 15, i >> 4)] = A.w2[i * NT + t];
+    const int cc = t & 63;  // this thread's conv1 channel
+    const float4 w1c = make_float4(A.w1[4 * cc], A.w1[4 * cc + 1], A.w1[4 * cc + 2], A.w1[4 * cc + 3]);
+    const float b1c = A.b1[cc];
+    // fc1_w slice: wf[kk] = fc1_w[16*wave + l16][kk*4 + g] (k' = 64g + kk <-> orig kk*4 + g),
+    // through LDS (the h1 area is still free): two halves of 32 rows, coalesced global reads,
+    // row stride 260 (= 4 mod 64) so the stride-4 register gather is conflict-free
+    float wf[64];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        float* st = h1;
+#pragma unroll 4
+        for (int i = 0; i < 32; ++i) st[i * 260 + t] = A.wf1[(32 * half + i) * NT + t];
+        __syncthreads();
+        if ((wave >> 1) == half) {
+            const float* src = st + (16 * (wave & 1) + l16) * 260 + g;
+#pragma unroll
+            for (int kk = 0; kk < 64; ++kk) wf[kk] = src[4 * kk];
+        }
+        __syncthreads();
     }
-
     const int64_t ntiles = (A.n + P::S - 1) / P::S;
-    // conv2 lane geometry: row r = l16 -> board s = 4*wave + (r >> 2), position q = r & 3;
-    // tap g = (kh, kw); conv1 output position (pr, pc) = (qh + kh, qw + kw)
+    // conv2 lane geometry: row l16 -> board s = 4*wave + (l16 >> 2), position q = l16 & 3; tap g
     const int s_r = 4 * wave + (l16 >> 2), q_r = l16 & 3;
-    const int pr = (q_r >> 1) + (g >> 1), pc = (q_r & 1) + (g & 1);
+    const int pos_r = ((q_r >> 1) + (g >> 1)) * 3 + (q_r & 1) + (g & 1);
+    const float* abase = h1 + s_r * 9 + pos_r;
     auto load_word = [&](int64_t tile) -> uint32_t {  // thread t < 64: word t&3 of board t>>2
         const int64_t b = tile * P::S + (t >> 2);
         if (t >= P::S * 4 || tile >= ntiles || b >= A.n) return 0u;
@@ -343,7 +352,7 @@ __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
     PHASE(7);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * P::S;
-        __syncthreads();  // previous tile's xs / h2 / fa fully consumed (and staging done)
+        __syncthreads();  // previous tile's xs / h1 / h2 / fa fully consumed (and staging done)
         PHASE(0);
         if (t < P::S * 4) {
             const uint32_t v = next_word;
@@ -354,78 +363,70 @@ __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
             dst[3] = (float)(v >> 24);
         }
         __syncthreads();
-        PHASE(1);
+        PHASE(8);
         next_word = load_word(tile + gridDim.x);  // in flight during this tile
-        // ---- conv2 (conv1 recomputed in the A operand), 8 chunks of 8 channels, software
-        //      pipelined: iteration ch reads chunk ch+1's B rows and chunk ch+2's conv1 weights,
-        //      computes chunk ch+1's conv1 and runs chunk ch's 32 MFMAs.
+        // ---- conv1 -> h1: channel cc at the 9 positions of boards 4*wave .. 4*wave+3: the 64
+        //      input cells are read at once (one LDS round trip), then 36 independent fma chains
         {
-            const float* x = xs + s_r * 16 + pr * 4 + pc;
-            const f32x2 a0 = {x[0], x[0]}, a1 = {x[1], x[1]}, a2 = {x[4], x[4]}, a3 = {x[5], x[5]};
-            f32x4 acc[4] = {f32x4{0}, f32x4{0}, f32x4{0}, f32x4{0}};
-            float hv[2][8];
-            f32x4 bb[2][8];
-            f32x4 wq[2][8], bq[2][2];  // wq[buf][4*half + tap] = w1t[tap][c0 + 4*half .. +3]
-            const int jsw = l16;
-            auto load_w = [&](int chunk, int buf) {
+            float x[4][16];
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
+            for (int bb = 0; bb < 4; ++bb)
 #pragma unroll
-                    for (int tp = 0; tp < 4; ++tp)
-                        wq[buf][4 * h + tp] =
-                            *reinterpret_cast<const f32x4*>(w1t + tp * 64 + chunk * 8 + 4 * h);
-                    bq[buf][h] = *reinterpret_cast<const f32x4*>(sb1 + chunk * 8 + 4 * h);
+                for (int r = 0; r < 4; ++r) {
+                    const float4 v = *reinterpret_cast<const float4*>(xs + (4 * wave + bb) * 16 + 4 * r);
+                    x[bb][4 * r] = v.x;
+                    x[bb][4 * r + 1] = v.y;
+                    x[bb][4 * r + 2] = v.z;
+                    x[bb][4 * r + 3] = v.w;
                 }
-            };
-            auto load_b = [&](int chunk, int buf) {
+            const float wt[4] = {w1c.x, w1c.y, w1c.z, w1c.w};
+            float v[4][9];
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                for (int p = 0; p < 9; ++p) v[bb][p] = b1c;
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                    for (int p = 0; p < 9; ++p) {
+                        const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
+                        v[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], v[bb][p]);
+                    }
+            float* dst = h1 + cc * P::H1S + 4 * wave * 9;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                for (int p = 0; p < 9; ++p) dst[bb * 9 + p] = fmaxf(v[bb][p], 0.f);
+        }
+        __syncthreads();
+        PHASE(1);
+        // ---- conv2: 64 steps x (A from h1, B from W2s) -> 4 MFMAs, chunks of 8 steps with the
+        //      next chunk's LDS reads in flight
+        {
+            f32x4 acc[4] = {f32x4{0}, f32x4{0}, f32x4{0}, f32x4{0}};
+            float av[2][8];
+            f32x4 bv[2][8];
+            auto load = [&](int chunk, int buf) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int k = 4 * (chunk * 8 + j) + g;
-                    bb[buf][j] = *reinterpret_cast<const f32x4*>(w2s + P::w2s_index(k, jsw, 0));
+                    const int c = chunk * 8 + j;
+                    av[buf][j] = abase[c * P::H1S];
+                    bv[buf][j] = *reinterpret_cast<const f32x4*>(w2s + P::w2s_index(4 * c + g, l16, 0));
                 }
             };
-            auto conv1 = [&](int buf) {  // hv[buf][0..7] = relu(conv1) of the chunk's 8 channels
-#pragma unroll
-                for (int pq = 0; pq < 4; ++pq) {  // channel pair (2pq, 2pq+1)
-                    const int h = pq >> 1, o = (pq & 1) * 2;
-                    const f32x4 bv = bq[buf][h];
-                    f32x2 v = {bv[o], bv[o + 1]};
-                    const f32x4 w0 = wq[buf][4 * h + 0], w1 = wq[buf][4 * h + 1];
-                    const f32x4 w2 = wq[buf][4 * h + 2], w3 = wq[buf][4 * h + 3];
-                    v = __builtin_elementwise_fma(f32x2{w0[o], w0[o + 1]}, a0, v);
-                    v = __builtin_elementwise_fma(f32x2{w1[o], w1[o + 1]}, a1, v);
-                    v = __builtin_elementwise_fma(f32x2{w2[o], w2[o + 1]}, a2, v);
-                    v = __builtin_elementwise_fma(f32x2{w3[o], w3[o + 1]}, a3, v);
-                    hv[buf][2 * pq] = fmaxf(v[0], 0.f);
-                    hv[buf][2 * pq + 1] = fmaxf(v[1], 0.f);
-                }
-            };
-            load_w(0, 0);
-            load_w(1, 1);
-            load_b(0, 0);
-            conv1(0);
-            __builtin_amdgcn_sched_barrier(0);
+            load(0, 0);
 #pragma unroll
             for (int ch = 0; ch < 8; ++ch) {
-                const int cur = ch & 1, nxt = cur ^ 1;
-                if (ch < 7) load_b(ch + 1, nxt);
-                if (ch < 6) load_w(ch + 2, cur);
-                __builtin_amdgcn_sched_barrier(0);
-                if (ch < 7) conv1(nxt);
+                const int cur = ch & 1;
+                if (ch < 7) load(ch + 1, cur ^ 1);
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
 #pragma unroll
                     for (int nt = 0; nt < 4; ++nt)
-                        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[cur][j], bb[cur][j][nt],
+                        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][j], bv[cur][j][nt],
                                                                        acc[nt], 0, 0, 0);
-                if (ch < 7) {
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // 2 MFMA
-                        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
             }
             PHASE(2);
             // C: row 4g + i of the wave's 16 -> board 4*wave + g, q = i; col n = 16nt + l16
@@ -441,22 +442,19 @@ __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
         __syncthreads();
         PHASE(3);
         // ---- fc1 (16x16x4): [16 boards x 256] @ [256 x 64]; wave w: units 16w .. 16w+15.
-        //      Lane group g covers k' in [64g, 64g+64), read 4 steps at a time as b128.
+        //      Lane group g covers k' in [64g, 64g+64): A read 4 steps at a time, B in registers.
         {
             f32x4 c0 = f32x4{0}, c1 = f32x4{0};
             const int jc = wave * 16 + l16;
             const float* ap = h2 + l16 * P::H2S + 64 * g;
-            const float* bp = wf1s + jc * P::WF1S + 64 * g;
 #pragma unroll
             for (int kk = 0; kk < 64; kk += 8) {
                 const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
-                const f32x4 bv0 = *reinterpret_cast<const f32x4*>(bp + kk);
                 const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
-                const f32x4 bv1 = *reinterpret_cast<const f32x4*>(bp + kk + 4);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv0[e], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv1[e], c1, 0, 0, 0);
+                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], wf[kk + e], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], wf[kk + 4 + e], c1, 0, 0, 0);
                 }
             }
 #pragma unroll
@@ -487,7 +485,7 @@ __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
     }
 #ifdef G2048_PHASE_PROF
     if (blockIdx.x == 0 && lane == 0)
-        for (int k = 0; k < 8; ++k) g_phase[wave][k] = ph[k];
+        for (int k = 0; k < 10; ++k) g_phase[wave][k] = ph[k];
 #endif
 }
 #undef PHASE

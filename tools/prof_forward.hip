@@ -17,74 +17,85 @@ extern "C" int g2048_replay_views(g2048_replay*, uint8_t**, uint8_t**, uint8_t**
                                   uint64_t**) {
     return -1;
 }
-// calibration: 16 x 128 f32 32x32x2 MFMAs on two accumulator chains, register operands
-__global__ __launch_bounds__(256) void k_mfma_cal(float* out, unsigned long long* cyc, int chains) {
+// calibration (compile-time modes): 2048 32x32x2-equivalents per wave, register operands
+//   0: 32x32x2, 2 chains   1: 32x32x2, 4 chains   2: 32x32x2, 2 chains + 5 VALU per MFMA
+//   3: 16x16x4, 4 chains   4: 16x16x4, 4 chains + 1 VALU per MFMA   5: 16x16x4, 2 chains
+template <int MODE>
+__global__ __launch_bounds__(256) void k_mfma_cal(float* out, unsigned long long* cyc) {
     float a = threadIdx.x * 1e-3f, b = 1.0f - threadIdx.x * 1e-4f;
     f32x16 c0 = f32x16{0}, c1 = f32x16{0}, c2 = f32x16{0}, c3 = f32x16{0};
+    f32x4 d0 = f32x4{0}, d1 = d0, d2 = d0, d3 = d0;
+    float v0 = a, v1 = b, v2 = a + b, v3 = a - b, v4 = a * b;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     for (int it = 0; it < 16; ++it) {
-        if (chains == 2) {
 #pragma unroll
-            for (int j = 0; j < 64; ++j) {
+        for (int j = 0; j < 32; ++j) {
+            if constexpr (MODE == 0 || MODE == 2) {
                 c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
+                if constexpr (MODE == 2) {
+                    v0 = fmaf(v0, 1.0001f, 0.5f); v1 = fmaf(v1, 1.0001f, 0.5f);
+                    v2 = fmaf(v2, 1.0001f, 0.5f); v3 = fmaf(v3, 1.0001f, 0.5f);
+                    v4 = fmaf(v4, 1.0001f, 0.5f);
+                }
                 c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
-            }
-        } else if (chains == 3) {  // 2 chains + 5 independent VALU FMAs per MFMA
-            float v0 = a, v1 = b, v2 = a + b, v3 = a - b, v4 = a * b;
-#pragma unroll
-            for (int j = 0; j < 64; ++j) {
-                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
-                v0 = fmaf(v0, 1.0001f, 0.5f);
-                v1 = fmaf(v1, 1.0001f, 0.5f);
-                v2 = fmaf(v2, 1.0001f, 0.5f);
-                v3 = fmaf(v3, 1.0001f, 0.5f);
-                v4 = fmaf(v4, 1.0001f, 0.5f);
-                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
-                v0 = fmaf(v0, 1.0001f, 0.25f);
-                v1 = fmaf(v1, 1.0001f, 0.25f);
-                v2 = fmaf(v2, 1.0001f, 0.25f);
-                v3 = fmaf(v3, 1.0001f, 0.25f);
-                v4 = fmaf(v4, 1.0001f, 0.25f);
-            }
-            a += v0 + v1 + v2 + v3 + v4;
-        } else if (chains >= 5) {  // 16x16x4 on 4 accumulators (x2 count: same FLOPs); 6: + 1 VALU
-            f32x4 d0 = f32x4{0}, d1 = d0, d2 = d0, d3 = d0;
-            float v0 = a, v1 = b, v2 = a + b, v3 = a - b;
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
-                if (chains == 6) v0 = fmaf(v0, 1.0001f, 0.5f);
-                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
-                if (chains == 6) v1 = fmaf(v1, 1.0001f, 0.5f);
-                d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, d2, 0, 0, 0);
-                if (chains == 6) v2 = fmaf(v2, 1.0001f, 0.5f);
-                d3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, d3, 0, 0, 0);
-                if (chains == 6) v3 = fmaf(v3, 1.0001f, 0.5f);
-                d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
-                if (chains == 6) v0 = fmaf(v0, 1.0001f, 0.5f);
-                d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
-                if (chains == 6) v1 = fmaf(v1, 1.0001f, 0.5f);
-                d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, d2, 0, 0, 0);
-                if (chains == 6) v2 = fmaf(v2, 1.0001f, 0.5f);
-                d3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, d3, 0, 0, 0);
-                if (chains == 6) v3 = fmaf(v3, 1.0001f, 0.5f);
-            }
-            for (int i = 0; i < 4; ++i) c0[i] = d0[i] + d1[i] + d2[i] + d3[i] + v0 + v1 + v2 + v3;
-        } else {
-#pragma unroll
-            for (int j = 0; j < 32; ++j) {
+                if constexpr (MODE == 2) {
+                    v0 = fmaf(v0, 1.0001f, 0.25f); v1 = fmaf(v1, 1.0001f, 0.25f);
+                    v2 = fmaf(v2, 1.0001f, 0.25f); v3 = fmaf(v3, 1.0001f, 0.25f);
+                    v4 = fmaf(v4, 1.0001f, 0.25f);
+                }
+                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, b, c1, 0, 0, 0);
+            } else if constexpr (MODE == 1) {
                 c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c0, 0, 0, 0);
                 c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, a, c1, 0, 0, 0);
                 c2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, c2, 0, 0, 0);
                 c3 = __builtin_amdgcn_mfma_f32_32x32x2f32(b, b, c3, 0, 0, 0);
+            } else if constexpr (MODE == 5) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, d0, 0, 0, 0);
+                    if constexpr (MODE == 4) v0 = fmaf(v0, 1.0001f, 0.5f);
+                    d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, a, d1, 0, 0, 0);
+                    if constexpr (MODE == 4) v1 = fmaf(v1, 1.0001f, 0.5f);
+                    d2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, a, d2, 0, 0, 0);
+                    if constexpr (MODE == 4) v2 = fmaf(v2, 1.0001f, 0.5f);
+                    d3 = __builtin_amdgcn_mfma_f32_16x16x4f32(b, b, d3, 0, 0, 0);
+                    if constexpr (MODE == 4) v3 = fmaf(v3, 1.0001f, 0.5f);
+                }
             }
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-    float s = 0;
+    float s = v0 + v1 + v2 + v3 + v4;
     for (int i = 0; i < 16; ++i) s += c0[i] + c1[i] + c2[i] + c3[i];
+    for (int i = 0; i < 4; ++i) s += d0[i] + d1[i] + d2[i] + d3[i];
     out[blockIdx.x * 256 + threadIdx.x] = s;
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) cyc[threadIdx.x >> 6] = t1 - t0;
+}
+
+template <int MODE>
+void run_cal(float* o, unsigned long long* cyc, const char* what) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_mfma_cal<MODE>, dim3(256), dim3(256), 0, nullptr, o, cyc);
+    (void)hipEventRecord(e0, nullptr);
+    hipLaunchKernelGGL(k_mfma_cal<MODE>, dim3(256), dim3(256), 0, nullptr, o, cyc);
+    (void)hipEventRecord(e1, nullptr);
+    (void)hipEventSynchronize(e1);
+    float ms;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    unsigned long long h[4];
+    (void)hipMemcpy(h, cyc, 32, hipMemcpyDeviceToHost);
+    // 16 x 32 x 4 = 2048 32x32x2-equivalents (4096 16x16x4) per wave
+    printf("cal %d %-34s ticks/32x32x2-equiv %.1f  %.2f us  %.1f TF\n", MODE, what, h[0] / 2048.0,
+           ms * 1e3, 256.0 * 4 * 2048 * 4096 / (ms * 1e-3) / 1e12);
 }
 
 int main(int argc, char** argv) {
@@ -93,23 +104,12 @@ int main(int argc, char** argv) {
         unsigned long long* cyc;
         (void)hipMalloc(&o, 256 * 256 * 4);
         (void)hipMalloc(&cyc, 64);
-        for (int chains = 2; chains <= 6; ++chains) {
-            hipEvent_t e0, e1;
-            (void)hipEventCreate(&e0);
-            (void)hipEventCreate(&e1);
-            hipLaunchKernelGGL(k_mfma_cal, dim3(256), dim3(256), 0, nullptr, o, cyc, chains);
-            (void)hipEventRecord(e0, nullptr);
-            hipLaunchKernelGGL(k_mfma_cal, dim3(256), dim3(256), 0, nullptr, o, cyc, chains);
-            (void)hipEventRecord(e1, nullptr);
-            (void)hipEventSynchronize(e1);
-            float ms;
-            (void)hipEventElapsedTime(&ms, e0, e1);
-            unsigned long long h[4];
-            (void)hipMemcpy(h, cyc, 32, hipMemcpyDeviceToHost);
-            printf("mfma cal mode=%d: 2048 32x32x2-equiv/wave: memtime %llu %llu %llu %llu, %.2f us "
-                   "(%.1f TF)\n", chains, h[0], h[1], h[2], h[3], ms * 1e3,
-                   256.0 * 4 * 2048 * 4096 / (ms * 1e-3) / 1e12);
-        }
+        run_cal<0>(o, cyc, "32x32x2, 2 chains");
+        run_cal<1>(o, cyc, "32x32x2, 4 chains");
+        run_cal<2>(o, cyc, "32x32x2, 2 chains, 5 VALU/MFMA");
+        run_cal<3>(o, cyc, "16x16x4, 4 chains");
+        run_cal<4>(o, cyc, "16x16x4, 4 chains, 1 VALU/MFMA");
+        run_cal<5>(o, cyc, "16x16x4, 2 chains");
     }
     const long n = argc > 1 ? atol(argv[1]) : 65536;
     const int sizes[8] = {256, 64, 16384, 64, 16384, 64, 256, 4};
@@ -138,12 +138,12 @@ int main(int argc, char** argv) {
     (void)hipEventSynchronize(b);
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
-    unsigned long long ph[4][8];
+    unsigned long long ph[4][10];
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
     printf("n=%ld  %.2f us/launch\n", n, ms * 1e3 / 20);
-    const char* names[8] = {"top_sync", "stage+sync", "conv2", "h2+sync", "fc1", "sync",
-                            "fc2", "weights"};
-    for (int k = 0; k < 8; ++k) {
+    const char* names[10] = {"top_sync", "conv1+sync", "conv2", "h2+sync", "fc1", "sync",
+                             "fc2", "weights", "stage+sync", "-"};
+    for (int k = 0; k < 9; ++k) {
         printf("%-11s", names[k]);
         for (int wv = 0; wv < 4; ++wv) printf(" %9llu", ph[wv][k]);
         printf("\n");
