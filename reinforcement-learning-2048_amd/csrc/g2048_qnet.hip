@@ -237,258 +237,267 @@ __global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Persistent variant for large n (the rollout's Q over all boards): 256 workgroups (one per CU)
-// stage W2 once and loop over tiles of 16 boards; each wave keeps its 16-unit slice of fc1_w in
-// 64 VGPRs (fc1's B operand), which leaves LDS room for h1.
+// ---------------------------------------------------------------------------------------------
+// Persistent kernels (rollout forward for large n, Double-DQN targets): a workgroup stages a
+// net's W2 once (LDS) and its fc1_w once (registers: each wave keeps its 16-unit slice in 64
+// VGPRs, fc1's B operand), then runs 16-board tiles.
 //
 // On gfx950 a VALU op between f32 MFMAs is not hidden (tools/prof_forward.hip: +4 cycles per op,
 // ~12 when the ops form dependent chains), so the MFMA loops carry no VALU at all:
-//  * conv1 runs as its own phase: thread (channel c = t&63, board group t>>6) computes its
-//    channel at the 9 positions of 4 boards -- 36 independent fma chains -- into
-//    h1[c][board*9 + pos] (channel stride 145 = 17 mod 64: conflict-free writes and reads);
+//  * conv1 runs as its own phase: thread (channel c = t&63, board group t>>6) reads its 4
+//    boards' 64 cells at once and runs 36 independent fma chains into h1[c][board*9 + pos]
+//    (channel stride 145 = 17 mod 64: conflict-free writes and reads);
 //  * conv2 is split by ROWS: wave w owns boards 4w..4w+3 (16 rows (s, q)) x all 64 channels as
 //    four 16x16x4 tiles.  Lane group g = lane>>4 is the tap (kh, kw) = (g>>1, g&1) and step c is
 //    the input channel, so k = 4c + g is conv2's flat weight index.  Per step: one ds_read_b32
 //    of h1 (A, shared by the four tiles) + one ds_read_b128 of W2 (B) -> 4 MFMAs;
 //  * fc1: A = h2 read along k as ds_read_b128, B = the wave's fc1_w slice in registers;
-//  * fc2 uses all 256 threads.
-// The summation order equals the tile kernel's per-row order (fp32 rounding identical per op).
+//  * fc2 uses all 256 threads and leaves Q[16][4] in LDS.
 namespace persist {
 constexpr int S = 16;
+constexpr int TMAX = 8;   // tiles per workgroup in the targets kernel
 constexpr int H1S = 145;  // floats per channel of h1: [c][board*9 + pos], 16*9 = 144 used
 constexpr int H2S = 260;  // h2[s][k'], k' = q*64 + n (fc1's input index permuted)
 constexpr int FS = 68;    // fa[s][j] (16-byte aligned rows for fc2's b128 reads)
 constexpr int WF2S = 68;  // swf2[a][j]
-constexpr int OFF_X = 0;                          // [S][16]
-constexpr int OFF_B2 = OFF_X + S * 16;            // 64
+constexpr int OFF_X = 0;                          // [TMAX][S][16] boards (exponents as floats)
+constexpr int OFF_B2 = OFF_X + TMAX * S * 16;     // 64
 constexpr int OFF_BF1 = OFF_B2 + 64;              // 64
 constexpr int OFF_WF2 = OFF_BF1 + 64;             // [4][WF2S]
 constexpr int OFF_BF2 = OFF_WF2 + 4 * WF2S;       // 4
 constexpr int OFF_W2 = OFF_BF2 + 4;               // W2s[k][16 x 4] swizzled, see w2s_index
-constexpr int OFF_H1 = OFF_W2 + 256 * 64;
-constexpr int OFF_H2 = (OFF_H1 + 64 * H1S + 3) & ~3;  // 16-byte aligned
+constexpr int OFF_H1 = OFF_W2 + 256 * 64;         // also the fc1_w staging area (32 x 260)
+constexpr int OFF_H2 = (OFF_H1 + 64 * H1S + 3) & ~3;
 constexpr int OFF_F = OFF_H2 + S * H2S;
-constexpr int FLOATS = OFF_F + S * FS;
+constexpr int OFF_Q = OFF_F + S * FS;             // [TMAX + 1][S][4] Q of a tile
+constexpr int FLOATS = OFF_Q + (TMAX + 1) * S * 4;
 static_assert(OFF_W2 % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 && OFF_WF2 % 4 == 0 &&
-                  OFF_X % 4 == 0,
+                  OFF_Q % 4 == 0,
               "b128 alignment");
-static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget (persistent forward)");
+static_assert(64 * H1S >= 32 * 260, "fc1_w staging must fit in the h1 area");
+static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget (persistent kernels)");
 // W2s row k holds w2[16nt + j][k] at 4*(j ^ (k & 15)) + nt: a lane group reads 16 distinct
 // 16-byte slots of one row (conflict-free b128) and the staging writes spread over 16 banks.
 __device__ __forceinline__ int w2s_index(int k, int j, int nt) {
     return k * 64 + 4 * (j ^ (k & 15)) + nt;
 }
-}  // namespace persist
 
-#ifdef G2048_PHASE_PROF
-__device__ unsigned long long g_phase[4][10];
-#define PHASE(k)                                                          \
-    do {                                                                  \
-        const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
-        ph[k] += now_ - ph_last;                                          \
-        ph_last = now_;                                                   \
-    } while (0)
-#else
-#define PHASE(k) do {} while (0)
-#endif
+struct Regs {  // per-thread weights held in registers
+    float4 w1c;    // conv1 weights of channel t & 63
+    float b1c;
+    float wf[64];  // fc1_w[16*wave + l16][kk*4 + g]  (k' = 64g + kk <-> orig kk*4 + g)
+};
 
-__global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
-    namespace P = persist;
-#ifdef G2048_PHASE_PROF
-    unsigned long long ph[10] = {0}, ph_last = __builtin_amdgcn_s_memtime();
-#endif
-    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
-    float* xs = lds + P::OFF_X;
-    float* sb2 = lds + P::OFF_B2;
-    float* sbf1 = lds + P::OFF_BF1;
-    float* swf2 = lds + P::OFF_WF2;
-    float* sbf2 = lds + P::OFF_BF2;
-    float* w2s = lds + P::OFF_W2;
-    float* h1 = lds + P::OFF_H1;
-    float* h2 = lds + P::OFF_H2;
-    float* fa = lds + P::OFF_F;
+// Stage net W: W2 + small tensors into LDS, conv1 channel + fc1_w slice into registers.  All
+// global loads (W2 and both fc1_w halves) are issued before the first LDS store: one memory
+// round trip.  Starts and ends with __syncthreads().
+__device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
-
-    // ---- stage W2 and the small tensors once (coalesced global reads); registers for the rest
-    if (t < 64) {
-        sb2[t] = A.b2[t];
-        sbf1[t] = A.bf1[t];
-    }
-    swf2[(t >> 6) * P::WF2S + (t & 63)] = A.wf2[t];
-    if (t < 4) sbf2[t] = A.bf2[t];
-#pragma unroll 4
-    for (int i = 0; i < 64; ++i) w2s[P::w2s_index(t, i & 15, i >> 4)] = A.w2[i * NT + t];
-    const int cc = t & 63;  // this thread's conv1 channel
-    const float4 w1c = make_float4(A.w1[4 * cc], A.w1[4 * cc + 1], A.w1[4 * cc + 2], A.w1[4 * cc + 3]);
-    const float b1c = A.b1[cc];
-    // fc1_w slice: wf[kk] = fc1_w[16*wave + l16][kk*4 + g] (k' = 64g + kk <-> orig kk*4 + g),
-    // through LDS (the h1 area is still free): two halves of 32 rows, coalesced global reads,
-    // row stride 260 (= 4 mod 64) so the stride-4 register gather is conflict-free
-    float wf[64];
+    float v2[64], f[2][32];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        float* st = h1;
-#pragma unroll 4
-        for (int i = 0; i < 32; ++i) st[i * 260 + t] = A.wf1[(32 * half + i) * NT + t];
+    for (int i = 0; i < 64; ++i) v2[i] = W.w2[i * NT + t];  // w2[n = i][k = t]
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) f[h][i] = W.wf1[(32 * h + i) * NT + t];
+    const int cc = t & 63;
+    R.w1c = make_float4(W.w1[4 * cc], W.w1[4 * cc + 1], W.w1[4 * cc + 2], W.w1[4 * cc + 3]);
+    R.b1c = W.b1[cc];
+    const float b2 = t < 64 ? W.b2[t] : 0.f, bf1 = t < 64 ? W.bf1[t] : 0.f;
+    const float wf2 = W.wf2[t], bf2 = t < 4 ? W.bf2[t] : 0.f;
+    __syncthreads();  // previous users of W2s / the h1 area are done
+    float* w2s = lds + OFF_W2;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) w2s[w2s_index(t, i & 15, i >> 4)] = v2[i];
+    if (t < 64) {
+        lds[OFF_B2 + t] = b2;
+        lds[OFF_BF1 + t] = bf1;
+    }
+    lds[OFF_WF2 + (t >> 6) * WF2S + (t & 63)] = wf2;
+    if (t < 4) lds[OFF_BF2 + t] = bf2;
+    // fc1_w through the h1 area in two halves of 32 rows (row stride 260 = 4 mod 64, so the
+    // stride-4 register gather is conflict-free)
+    float* st = lds + OFF_H1;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) st[i * 260 + t] = f[h][i];
         __syncthreads();
-        if ((wave >> 1) == half) {
+        if ((wave >> 1) == h) {
             const float* src = st + (16 * (wave & 1) + l16) * 260 + g;
 #pragma unroll
-            for (int kk = 0; kk < 64; ++kk) wf[kk] = src[4 * kk];
+            for (int kk = 0; kk < 64; ++kk) R.wf[kk] = src[4 * kk];
         }
         __syncthreads();
     }
+}
+
+// Q[16][4] of the 16 boards in xs (exponents as floats, visible to all threads) -> qs (LDS).
+// Ends with __syncthreads() (qs visible; h1 / h2 / fa free for the next tile).
+__device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R, float* qs) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
+    const float* w2s = lds + OFF_W2;
+    float* h1 = lds + OFF_H1;
+    float* h2 = lds + OFF_H2;
+    float* fa = lds + OFF_F;
+    // ---- conv1 -> h1: channel cc at the 9 positions of boards 4*wave .. 4*wave+3: the 64
+    //      input cells are read at once (one LDS round trip), then 36 independent fma chains
+    {
+        const int cc = t & 63;
+        float x[4][16];
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float4 v = *reinterpret_cast<const float4*>(xs + (4 * wave + bb) * 16 + 4 * r);
+                x[bb][4 * r] = v.x;
+                x[bb][4 * r + 1] = v.y;
+                x[bb][4 * r + 2] = v.z;
+                x[bb][4 * r + 3] = v.w;
+            }
+        const float wt[4] = {R.w1c.x, R.w1c.y, R.w1c.z, R.w1c.w};
+        float v[4][9];
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int p = 0; p < 9; ++p) v[bb][p] = R.b1c;
+#pragma unroll
+        for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+                for (int p = 0; p < 9; ++p) {
+                    const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
+                    v[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], v[bb][p]);
+                }
+        float* dst = h1 + cc * H1S + 4 * wave * 9;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+#pragma unroll
+            for (int p = 0; p < 9; ++p) dst[bb * 9 + p] = fmaxf(v[bb][p], 0.f);
+    }
+    __syncthreads();
+    // ---- conv2: 64 steps x (A from h1, B from W2s) -> 4 MFMAs, chunks of 8 steps with the next
+    //      chunk's LDS reads in flight
+    {
+        const int s_r = 4 * wave + (l16 >> 2), q_r = l16 & 3;
+        const int pos_r = ((q_r >> 1) + (g >> 1)) * 3 + (q_r & 1) + (g & 1);
+        const float* abase = h1 + s_r * 9 + pos_r;
+        f32x4 acc[4] = {f32x4{0}, f32x4{0}, f32x4{0}, f32x4{0}};
+        float av[2][8];
+        f32x4 bv[2][8];
+        auto load = [&](int chunk, int buf) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = chunk * 8 + j;
+                av[buf][j] = abase[c * H1S];
+                bv[buf][j] = *reinterpret_cast<const f32x4*>(w2s + w2s_index(4 * c + g, l16, 0));
+            }
+        };
+        load(0, 0);
+#pragma unroll
+        for (int ch = 0; ch < 8; ++ch) {
+            const int cur = ch & 1;
+            if (ch < 7) load(ch + 1, cur ^ 1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int nt = 0; nt < 4; ++nt)
+                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][j], bv[cur][j][nt],
+                                                                   acc[nt], 0, 0, 0);
+        }
+        // C: row 4g + i of the wave's 16 -> board 4*wave + g, q = i; col n = 16nt + l16
+        const float* sb2 = lds + OFF_B2;
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+            const int n = 16 * nt + l16;
+            const float bn = sb2[n];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                h2[(4 * wave + g) * H2S + i * 64 + n] = fmaxf(acc[nt][i] + bn, 0.f);
+        }
+    }
+    __syncthreads();
+    // ---- fc1 (16x16x4): [16 boards x 256] @ [256 x 64]; wave w: units 16w .. 16w+15.
+    //      Lane group g covers k' in [64g, 64g+64): A read 4 steps at a time, B in registers.
+    {
+        f32x4 c0 = f32x4{0}, c1 = f32x4{0};
+        const int jc = wave * 16 + l16;
+        const float* ap = h2 + l16 * H2S + 64 * g;
+#pragma unroll
+        for (int kk = 0; kk < 64; kk += 8) {
+            const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
+            const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], R.wf[kk + e], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], R.wf[kk + 4 + e], c1, 0, 0, 0);
+            }
+        }
+        const float* sbf1 = lds + OFF_BF1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            fa[(4 * g + i) * FS + jc] = fmaxf((c0[i] + c1[i]) + sbf1[jc], 0.f);
+    }
+    __syncthreads();
+    // ---- fc2: output o = t >> 2 (board o >> 2, action o & 3), part p = t & 3 sums 16 units
+    {
+        const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
+        const f32x4* fr = reinterpret_cast<const f32x4*>(fa + s * FS + 16 * p);
+        const f32x4* wr = reinterpret_cast<const f32x4*>(lds + OFF_WF2 + a * WF2S + 16 * p);
+        f32x4 pv = f32x4{0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const f32x4 f = fr[j], w = wr[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
+        }
+        float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+        v += __shfl_xor(v, 1);
+        v += __shfl_xor(v, 2);
+        if (p == 0) qs[o] = v + lds[OFF_BF2 + a];
+    }
+    __syncthreads();
+}
+
+// One board word (t < 64: word t&3 of board t>>2) -> 4 exponent floats in xs.
+__device__ __forceinline__ void put_word(float* xs, int t, uint32_t v) {
+    float* dst = xs + (t >> 2) * 16 + (t & 3) * 4;
+    dst[0] = (float)(v & 0xFFu);
+    dst[1] = (float)((v >> 8) & 0xFFu);
+    dst[2] = (float)((v >> 16) & 0xFFu);
+    dst[3] = (float)(v >> 24);
+}
+}  // namespace persist
+
+// The rollout's Q over all n boards (g2048_convnet_forward for n >= 16k): 256 workgroups stage
+// the net once and loop over 16-board tiles; the next tile's boards are loaded during the
+// current one.
+__global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
+    namespace P = persist;
+    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
+    const int t = threadIdx.x;
+    const NetW W{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2};
+    P::Regs R;
     const int64_t ntiles = (A.n + P::S - 1) / P::S;
-    // conv2 lane geometry: row l16 -> board s = 4*wave + (l16 >> 2), position q = l16 & 3; tap g
-    const int s_r = 4 * wave + (l16 >> 2), q_r = l16 & 3;
-    const int pos_r = ((q_r >> 1) + (g >> 1)) * 3 + (q_r & 1) + (g & 1);
-    const float* abase = h1 + s_r * 9 + pos_r;
-    auto load_word = [&](int64_t tile) -> uint32_t {  // thread t < 64: word t&3 of board t>>2
+    auto load_word = [&](int64_t tile) -> uint32_t {
         const int64_t b = tile * P::S + (t >> 2);
         if (t >= P::S * 4 || tile >= ntiles || b >= A.n) return 0u;
         return reinterpret_cast<const uint32_t*>(A.rows)[(A.idx ? A.idx[b] : b) * 4 + (t & 3)];
     };
     uint32_t next_word = load_word(blockIdx.x);
-    PHASE(7);
+    P::stage(W, lds, R);
+    float* xs = lds + P::OFF_X;
+    float* qs = lds + P::OFF_Q;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * P::S;
-        __syncthreads();  // previous tile's xs / h1 / h2 / fa fully consumed (and staging done)
-        PHASE(0);
-        if (t < P::S * 4) {
-            const uint32_t v = next_word;
-            float* dst = xs + (t >> 2) * 16 + (t & 3) * 4;
-            dst[0] = (float)(v & 0xFFu);
-            dst[1] = (float)((v >> 8) & 0xFFu);
-            dst[2] = (float)((v >> 16) & 0xFFu);
-            dst[3] = (float)(v >> 24);
-        }
+        if (t < P::S * 4) P::put_word(xs, t, next_word);
         __syncthreads();
-        PHASE(8);
         next_word = load_word(tile + gridDim.x);  // in flight during this tile
-        // ---- conv1 -> h1: channel cc at the 9 positions of boards 4*wave .. 4*wave+3: the 64
-        //      input cells are read at once (one LDS round trip), then 36 independent fma chains
-        {
-            float x[4][16];
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float4 v = *reinterpret_cast<const float4*>(xs + (4 * wave + bb) * 16 + 4 * r);
-                    x[bb][4 * r] = v.x;
-                    x[bb][4 * r + 1] = v.y;
-                    x[bb][4 * r + 2] = v.z;
-                    x[bb][4 * r + 3] = v.w;
-                }
-            const float wt[4] = {w1c.x, w1c.y, w1c.z, w1c.w};
-            float v[4][9];
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                for (int p = 0; p < 9; ++p) v[bb][p] = b1c;
-#pragma unroll
-            for (int tap = 0; tap < 4; ++tap)
-#pragma unroll
-                for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                    for (int p = 0; p < 9; ++p) {
-                        const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
-                        v[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], v[bb][p]);
-                    }
-            float* dst = h1 + cc * P::H1S + 4 * wave * 9;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                for (int p = 0; p < 9; ++p) dst[bb * 9 + p] = fmaxf(v[bb][p], 0.f);
-        }
-        __syncthreads();
-        PHASE(1);
-        // ---- conv2: 64 steps x (A from h1, B from W2s) -> 4 MFMAs, chunks of 8 steps with the
-        //      next chunk's LDS reads in flight
-        {
-            f32x4 acc[4] = {f32x4{0}, f32x4{0}, f32x4{0}, f32x4{0}};
-            float av[2][8];
-            f32x4 bv[2][8];
-            auto load = [&](int chunk, int buf) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int c = chunk * 8 + j;
-                    av[buf][j] = abase[c * P::H1S];
-                    bv[buf][j] = *reinterpret_cast<const f32x4*>(w2s + P::w2s_index(4 * c + g, l16, 0));
-                }
-            };
-            load(0, 0);
-#pragma unroll
-            for (int ch = 0; ch < 8; ++ch) {
-                const int cur = ch & 1;
-                if (ch < 7) load(ch + 1, cur ^ 1);
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-#pragma unroll
-                    for (int nt = 0; nt < 4; ++nt)
-                        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][j], bv[cur][j][nt],
-                                                                       acc[nt], 0, 0, 0);
-            }
-            PHASE(2);
-            // C: row 4g + i of the wave's 16 -> board 4*wave + g, q = i; col n = 16nt + l16
-#pragma unroll
-            for (int nt = 0; nt < 4; ++nt) {
-                const int n = 16 * nt + l16;
-                const float bn = sb2[n];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    h2[(4 * wave + g) * P::H2S + i * 64 + n] = fmaxf(acc[nt][i] + bn, 0.f);
-            }
-        }
-        __syncthreads();
-        PHASE(3);
-        // ---- fc1 (16x16x4): [16 boards x 256] @ [256 x 64]; wave w: units 16w .. 16w+15.
-        //      Lane group g covers k' in [64g, 64g+64): A read 4 steps at a time, B in registers.
-        {
-            f32x4 c0 = f32x4{0}, c1 = f32x4{0};
-            const int jc = wave * 16 + l16;
-            const float* ap = h2 + l16 * P::H2S + 64 * g;
-#pragma unroll
-            for (int kk = 0; kk < 64; kk += 8) {
-                const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
-                const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], wf[kk + e], c0, 0, 0, 0);
-                    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], wf[kk + 4 + e], c1, 0, 0, 0);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                fa[(4 * g + i) * P::FS + jc] = fmaxf((c0[i] + c1[i]) + sbf1[jc], 0.f);
-        }
-        PHASE(4);
-        __syncthreads();
-        PHASE(5);
-        // ---- fc2: output o = t >> 2 (board o >> 2, action o & 3), part p = t & 3 sums 16 units
-        {
-            const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
-            const f32x4* fr = reinterpret_cast<const f32x4*>(fa + s * P::FS + 16 * p);
-            const f32x4* wr = reinterpret_cast<const f32x4*>(swf2 + a * P::WF2S + 16 * p);
-            f32x4 pv = f32x4{0};
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f32x4 f = fr[j], w = wr[j];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
-            }
-            float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
-            v += __shfl_xor(v, 1);
-            v += __shfl_xor(v, 2);
-            if (p == 0 && b0 + s < A.n) A.q[b0 * 4 + o] = v + sbf2[a];
-        }
-        PHASE(6);
+        P::tile(xs, lds, R, qs);
+        if (t < P::S * 4 && b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = qs[t];
     }
-#ifdef G2048_PHASE_PROF
-    if (blockIdx.x == 0 && lane == 0)
-        for (int k = 0; k < 10; ++k) g_phase[wave][k] = ph[k];
-#endif
 }
-#undef PHASE
 
 // Double-DQN targets for a minibatch (src/dqn_lib.py:67-68,125-132), one launch:
 //   idx_b = uniform row of the ring (Philox, epoch = the learner's update counter) or idx_in,
@@ -510,53 +519,91 @@ struct TargetArgs {
     float* y;
 };
 
-__global__ __launch_bounds__(NT) void k_conv_targets(TargetArgs A) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-    __shared__ float qon[S * 4], qtg[S * 4];
-    __shared__ int64_t sidx[S];
+// Each workgroup owns up to TMAX 16-sample tiles (tile = blockIdx.x + k*gridDim.x): it draws
+// their indices and loads their s' rows once, runs them through the online net (Q kept in
+// LDS), stages the target net and runs them again, then writes y.
+__global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
+    namespace P = persist;
+    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
+    __shared__ int64_t sidx[P::TMAX * P::S];
     const int t = threadIdx.x;
-    const int64_t b0 = (int64_t)blockIdx.x * S;
-    if (t < S) {
-        const int64_t b = b0 + t;
-        int64_t j = 0;
-        if (b < A.batch) {
-            if (A.idx_in) {
-                j = A.idx_in[b];
-            } else {  // same draw as k_sample / o2048_replay_sample_f64 (domain 3)
-                const unsigned long long ep = *A.epoch;
-                const uint4 u = g2048::philox10(
-                    make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
-                               (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
-                    A.seed_lo, A.seed_hi);
-                const unsigned long long x = ((unsigned long long)u.y << 32) | u.x;
-                j = (int64_t)__umul64hi(x, *A.count);
-            }
-            A.idx_out[b] = j;
-        }
-        sidx[t] = j;
+    const int64_t ntiles = (A.batch + P::S - 1) / P::S;
+    int T = 0;
+    for (int64_t tl = blockIdx.x; tl < ntiles && T < P::TMAX; tl += gridDim.x) ++T;
+    // sampler: thread t < 64 owns word t&3 of sample t>>2 of every tile; it draws the sample's
+    // ring row itself (same draw as k_sample / o2048_replay_sample_f64, domain 3; the four
+    // threads of a sample agree) and loads that word of s' at once
+    int32_t rv[P::TMAX];  // r and d of sample t>>2 of every tile (threads t < 64, t&3 == 0)
+    uint32_t dv[P::TMAX];
+#pragma unroll
+    for (int k = 0; k < P::TMAX; ++k) {
+        rv[k] = 0;
+        dv[k] = 0u;
     }
-    __syncthreads();
-    stage_boards(lds + OFF_X, A.s2, sidx, 0, S);  // rows of this tile (padding rows -> row 0)
-    __syncthreads();
-    conv_forward_tile(A.on, lds, qon);
-    conv_forward_tile(A.tg, lds, qtg);
-    if (t < S && b0 + t < A.batch) {
-#pragma clang fp contract(off)
-        const float* qo = qon + t * 4;
-        const float* qt = qtg + t * 4;
-        float next;
-        if (A.double_dqn) {
-            int a = 0;
-            float best = qo[0];
-            for (int k = 1; k < 4; ++k)
-                if (qo[k] > best) { best = qo[k]; a = k; }
-            next = qt[a];
-        } else {
-            next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+    if (t < P::S * 4) {
+        const int s = t >> 2;
+        const unsigned long long ep = A.idx_in ? 0ull : *A.epoch;
+        const unsigned long long cnt = A.idx_in ? 0ull : *A.count;
+        uint32_t w[P::TMAX];
+#pragma unroll
+        for (int k = 0; k < P::TMAX; ++k) {
+            w[k] = 0u;
+            if (k >= T) continue;
+            const int64_t b = (blockIdx.x + (int64_t)k * gridDim.x) * P::S + s;
+            int64_t j = 0;
+            if (b < A.batch) {
+                if (A.idx_in) {
+                    j = A.idx_in[b];
+                } else {
+                    const uint4 u = g2048::philox10(
+                        make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
+                                   (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
+                        A.seed_lo, A.seed_hi);
+                    const unsigned long long x = ((unsigned long long)u.y << 32) | u.x;
+                    j = (int64_t)__umul64hi(x, cnt);
+                }
+                if ((t & 3) == 0) A.idx_out[b] = j;
+            }
+            if ((t & 3) == 0) {
+                sidx[k * P::S + s] = j;
+                rv[k] = A.r[j];
+                dv[k] = A.d[j];
+            }
+            w[k] = reinterpret_cast<const uint32_t*>(A.s2)[j * 4 + (t & 3)];
         }
-        const int64_t j = sidx[t];
-        const float disc = (float)(1 - (int)A.d[j]) * A.gamma;
-        A.y[b0 + t] = (float)A.r[j] + disc * next;
+#pragma unroll
+        for (int k = 0; k < P::TMAX; ++k)
+            if (k < T) P::put_word(lds + P::OFF_X + k * P::S * 16, t, w[k]);
+    }
+    P::Regs R;
+    float* qon = lds + P::OFF_Q;               // [TMAX][16][4]
+    float* qtg = qon + P::TMAX * P::S * 4;     // [16][4]
+    P::stage(A.on, lds, R);  // (starts with __syncthreads: the s' boards are visible)
+    for (int k = 0; k < T; ++k)
+        P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qon + k * P::S * 4);
+    P::stage(A.tg, lds, R);
+    for (int k = 0; k < T; ++k) {
+        P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qtg);
+        const int sm = t >> 2;  // sample of this thread (t < 64, t & 3 == 0)
+        const int64_t b = (blockIdx.x + (int64_t)k * gridDim.x) * P::S + sm;
+        if (t < P::S * 4 && (t & 3) == 0 && b < A.batch) {
+#pragma clang fp contract(off)
+            const float* qo = qon + (k * P::S + sm) * 4;
+            const float* qt = qtg + sm * 4;
+            float next;
+            if (A.double_dqn) {
+                int a = 0;
+                float best = qo[0];
+                for (int e = 1; e < 4; ++e)
+                    if (qo[e] > best) { best = qo[e]; a = e; }
+                next = qt[a];
+            } else {
+                next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+            }
+            const float disc = (float)(1 - (int)dv[k]) * A.gamma;
+            A.y[b] = (float)rv[k] + disc * next;
+        }
+        // qtg is rewritten by the next tile only after that tile's internal barriers
     }
 }
 
@@ -627,7 +674,10 @@ extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* onlin
     A.double_dqn = double_dqn;
     A.idx_out = idx_out;
     A.y = y_out;
-    hipLaunchKernelGGL(k_conv_targets, dim3((unsigned)((batch + S - 1) / S)), dim3(NT), 0,
+    const int64_t ntiles = (batch + persist::S - 1) / persist::S;
+    int64_t grid = ntiles < 256 ? ntiles : 256;
+    if (grid * persist::TMAX < ntiles) grid = (ntiles + persist::TMAX - 1) / persist::TMAX;
+    hipLaunchKernelGGL(k_conv_targets_persist, dim3((unsigned)grid), dim3(NT), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK

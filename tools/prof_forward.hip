@@ -1,5 +1,4 @@
-// Phase timing of k_conv_forward_persist (s_memtime deltas of block 0, per wave), built only
-// for kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip
+// f32 MFMA / VALU calibration and k_conv_forward_persist timing, built only for kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip
 #define G2048_PHASE_PROF 1
 #include <cstdarg>
 #include <cstdio>
@@ -138,15 +137,6 @@ int main(int argc, char** argv) {
     (void)hipEventSynchronize(b);
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
-    unsigned long long ph[4][10];
-    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_phase), sizeof(ph));
     printf("n=%ld  %.2f us/launch\n", n, ms * 1e3 / 20);
-    const char* names[10] = {"top_sync", "conv1+sync", "conv2", "h2+sync", "fc1", "sync",
-                             "fc2", "weights", "stage+sync", "-"};
-    for (int k = 0; k < 9; ++k) {
-        printf("%-11s", names[k]);
-        for (int wv = 0; wv < 4; ++wv) printf(" %9llu", ph[wv][k]);
-        printf("\n");
-    }
     return 0;
 }
