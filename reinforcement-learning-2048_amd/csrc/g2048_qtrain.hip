@@ -133,6 +133,15 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
     float accw1[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}}, accb1[2] = {0, 0};
     float accWf2 = 0.f, accBf2 = 0.f, accBf1 = 0.f, accB2 = 0.f, accLoss = 0.f;
 
+    // W2 and fc1_w columns of this thread (w2[i][t], wf1[i][t], i < 64), loaded once in one
+    // batch; the four per-tile LDS layouts below are stored from these registers
+    float vW2[64], vF[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+        vW2[i] = A.w2[i * NT + t];
+        vF[i] = A.wf1[i * NT + t];
+    }
+
     const int64_t ntiles = (A.batch + S - 1) / S;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * S;
@@ -156,8 +165,8 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             sy[t] = ok ? A.y[b] : 0.f;
             sg[t] = ok ? 1.f : 0.f;  // validity, replaced by dq in phase E
         }
-#pragma unroll 4
-        for (int i = 0; i < 64; ++i) w[t * WT_STRIDE + i] = A.w2[i * NT + t];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) w[t * WT_STRIDE + i] = vW2[i];
         __syncthreads();
 
         // ---- B: conv2 forward.  rows r = 32*wave + l32 (board s = r>>2, position q = r&3)
@@ -182,8 +191,8 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
         }
         __syncthreads();
         // ---- C: Wf1 transposed into w[k'][j], k' = q*64 + c' (h2's order), m = c'*4 + q
-#pragma unroll 4
-        for (int i = 0; i < 64; ++i) w[((t & 3) * 64 + (t >> 2)) * WT_STRIDE + i] = A.wf1[i * NT + t];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) w[((t & 3) * 64 + (t >> 2)) * WT_STRIDE + i] = vF[i];
         __syncthreads();
         // ---- D: fc1 forward (16x16x4) -> f
         {
@@ -231,8 +240,8 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             if (j == 0) accBf2 += gb;
         }
         // w[j][k'] (stride 257) = wf1[j][m], k' = q*64 + c', m = c'*4 + q
-#pragma unroll 4
-        for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + (t & 3) * 64 + (t >> 2)] = A.wf1[i * NT + t];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + (t & 3) * 64 + (t >> 2)] = vF[i];
         __syncthreads();
         // ---- G: df = dq * Wf2[a] * relu'(f), in place over f
         {
@@ -291,8 +300,8 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             }
         }
         // stage W2 row-major w[c'][k] (stride 257) for dP
-#pragma unroll 4
-        for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + t] = A.w2[i * NT + t];
+#pragma unroll
+        for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + t] = vW2[i];
         __syncthreads();
         // ---- J: db2; dW2^T += P^T @ dh2 (persistent; A = recomputed conv1 patches)
         if (t < 64) {

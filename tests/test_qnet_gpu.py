@@ -225,3 +225,38 @@ def test_dense64_train_grad_matches_autograd(G, B):
         g, r = grad[off:off + p.numel()].double(), ref[off:off + p.numel()]
         assert float((g - r).norm()) <= 1e-4 * float(r.norm()) + 1e-6, p.shape
         off += p.numel()
+
+
+@pytest.mark.parametrize("B", [32, 1000, 8192])
+def test_fused_learner_kernels_are_deterministic(G, B):
+    """Bitwise-identical results across repeated launches on the same inputs: the conv / dense64
+    forward, targets and train-gradient kernels (the gradient reduction is fixed-order; a race
+    shows up here even when it stays inside the parity tolerances)."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    rb = _filled_ring(G, 5 + B)
+    torch.manual_seed(B)
+    idx = torch.randint(0, rb.capacity, (B,), device=DEV)
+    y = (torch.randn(B, device=DEV) * 20 + 30).float()
+    epoch = torch.tensor([3], dtype=torch.int64, device=DEV)
+    for kind in ("conv", "dense64"):
+        m = det_init(make_net(kind, torch.float32, DEV), 0.4)
+        tgt = det_init(make_net(kind, torch.float32, DEV), 0.9)
+        po, pt = qnet.net_params(m), qnet.net_params(tgt)
+        tg = qnet.TrainGrad(m, B)
+        outs = []
+        for _ in range(6):
+            grad = torch.full((tg.n_params,), float("nan"), device=DEV)
+            loss = torch.zeros((), device=DEV)
+            tg(rb.s, rb.a, idx, y, grad, loss)
+            q = qnet.forward(m, rb.s, idx)
+            io = torch.empty(B, dtype=torch.int64, device=DEV)
+            yo = torch.empty(B, dtype=torch.float32, device=DEV)
+            qnet.targets(kind, po, pt, rb, B, io, yo, seed=7, epoch=epoch)
+            outs.append((grad, loss, q, io, yo))
+        torch.cuda.synchronize()
+        assert torch.isfinite(outs[0][0]).all()
+        for o in outs[1:]:
+            for a, b in zip(o, outs[0]):
+                assert torch.equal(a, b), kind
