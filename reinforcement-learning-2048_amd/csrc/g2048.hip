@@ -194,10 +194,12 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
     atomicMax(A.rb.count, (unsigned long long)c);
 }
 
-template <int MODE>
+// kFull: every block is full (n % kBlock == 0), so there is no bounds test and every kernel
+// argument load can be issued at once (with the test, the pointer loads wait for n's round trip).
+template <int MODE, bool kFull>
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= A.n) return;
+    if (!kFull && i >= A.n) return;
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
     double eps = 0.0;
@@ -458,8 +460,12 @@ int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
 template <int MODE>
 int launch_step(g2048_env* e, const StepArgs& A, void* stream) {
     DeviceGuard g(e->device);
-    hipLaunchKernelGGL(k_step<MODE>, dim3(grid_for(e->n)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), A);
+    if (e->n % kBlock == 0)
+        hipLaunchKernelGGL((k_step<MODE, true>), dim3(grid_for(e->n)), dim3(kBlock), 0,
+                           reinterpret_cast<hipStream_t>(stream), A);
+    else
+        hipLaunchKernelGGL((k_step<MODE, false>), dim3(grid_for(e->n)), dim3(kBlock), 0,
+                           reinterpret_cast<hipStream_t>(stream), A);
     G_HIP(hipGetLastError());
     return G2048_OK;
 }

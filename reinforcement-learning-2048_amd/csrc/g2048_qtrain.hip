@@ -91,7 +91,22 @@ __device__ __forceinline__ int acc_row32(int i, int lane) {  // 32x32 C/D row of
     return (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
 }
 
+#ifdef G2048_PHASE_PROF
+__device__ unsigned long long g_tphase[4][16];
+#define TPHASE(k)                                                         \
+    do {                                                                  \
+        const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+        ph[k] += now_ - ph_last;                                          \
+        ph_last = now_;                                                   \
+    } while (0)
+#else
+#define TPHASE(k) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
+#ifdef G2048_PHASE_PROF
+    unsigned long long ph[16] = {0}, ph_last = __builtin_amdgcn_s_memtime();
+#endif
     __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
     float* xs = lds + OFF_X;
     float* sw1 = lds + OFF_W1;
@@ -146,6 +161,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * S;
         __syncthreads();  // previous tile fully consumed
+        TPHASE(0);
         // ---- A: boards, actions, targets; W2 transposed into w[k][n]
         if (t < S * 4) {
             const int s = t >> 2, wd = t & 3;
@@ -169,6 +185,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
         for (int i = 0; i < 64; ++i) w[t * WT_STRIDE + i] = vW2[i];
         __syncthreads();
 
+        TPHASE(1);
         // ---- B: conv2 forward.  rows r = 32*wave + l32 (board s = r>>2, position q = r&3)
         {
             f32x16 c0 = f32x16{0}, c1 = f32x16{0};
@@ -190,10 +207,12 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             }
         }
         __syncthreads();
+        TPHASE(2);
         // ---- C: Wf1 transposed into w[k'][j], k' = q*64 + c' (h2's order), m = c'*4 + q
 #pragma unroll
         for (int i = 0; i < 64; ++i) w[((t & 3) * 64 + (t >> 2)) * WT_STRIDE + i] = vF[i];
         __syncthreads();
+        TPHASE(3);
         // ---- D: fc1 forward (16x16x4) -> f
         {
             const int mt = wave & 1, nt0 = (wave >> 1) * 2, arow = mt * 16 + (lane & 15);
@@ -215,6 +234,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             }
         }
         __syncthreads();
+        TPHASE(4);
         // ---- E: fc2 at the taken action, loss, dq = 2 (q - y)
         if (t < S) {
             const int a = (int)sa[t];
@@ -226,6 +246,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             sg[t] = 2.f * d;
         }
         __syncthreads();
+        TPHASE(5);
         // ---- F: dWf2 / dbf2 (thread = (action a, unit j)); stage Wf1 row-major, permuted columns
         {
             const int a = t >> 6, j = t & 63;
@@ -243,6 +264,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + (t & 3) * 64 + (t >> 2)] = vF[i];
         __syncthreads();
+        TPHASE(6);
         // ---- G: df = dq * Wf2[a] * relu'(f), in place over f
         {
             const int s = t >> 3, j0 = (t & 7) * 8;
@@ -256,6 +278,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             }
         }
         __syncthreads();
+        TPHASE(7);
         // ---- H: dbf1; dWf1 += df^T @ h2 (persistent); dh2_pre = df @ Wf1p
         if (t < 64) {
             float v = 0.f;
@@ -287,6 +310,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             }
         }
         __syncthreads();  // every read of h2 (dWf1) and of Wf1p is done
+        TPHASE(8);
         // ---- I: dh2 = dh2_pre * relu'(h2), in place over h2
         {
             const int nt0 = wave * 2;
@@ -303,6 +327,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) w[i * WR_STRIDE + t] = vW2[i];
         __syncthreads();
+        TPHASE(9);
         // ---- J: db2; dW2^T += P^T @ dh2 (persistent; A = recomputed conv1 patches)
         if (t < 64) {
             float v = 0.f;
@@ -340,6 +365,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
                 accW2[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, g1, accW2[3], 0, 0, 0);
             }
         }
+        TPHASE(10);
         // ---- K: dP = dh2 @ W2 per (m-tile, k-tile); epilogue folds col2im + relu'(h1) into
         //         per-lane dW1 / db1 sums.  Lane col k = kt*32 + l32 (kt = 2*wave + u).
 #pragma unroll
@@ -376,6 +402,7 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
     }
     __syncthreads();
 
+    TPHASE(11);
     // ---- write this workgroup's partial gradient slab (coalesced, kernel order)
     float* slab = A.slab + (int64_t)blockIdx.x * SLAB;
 #pragma unroll
@@ -426,7 +453,13 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
         for (int i = 0; i < S; ++i) v += red[i];
         slab[SL_LOSS] = v;
     }
+    TPHASE(12);
+#ifdef G2048_PHASE_PROF
+    if (blockIdx.x == 0 && (t & 63) == 0)
+        for (int k = 0; k < 16; ++k) g_tphase[t >> 6][k] = ph[k];
+#endif
 }
+#undef TPHASE
 
 // slab position -> torch flat parameter index
 __device__ __forceinline__ int slab_to_param(int pos) {
