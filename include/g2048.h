@@ -239,6 +239,20 @@ typedef struct {
     const float *w2, *b2; /* Linear(64, 4)  */
 } g2048_dense64_params;
 
+/* play_one_step of every board with the dense 16-64-4 Q-network (BASELINE configs[2]) fused in:
+ * each board's Q(s) is computed inside the step kernel (same fp32 summation order as
+ * g2048_dense64_forward, so the actions are bitwise those of forward + g2048_env_step_egreedy),
+ * then the eps-greedy step / replay append.  eps_decay_episodes > 0 selects the per-board
+ * schedule (as g2048_env_step_egreedy_schedule); else eps_dev (device f64) or eps.
+ * q_out f32[n][4] (16-byte aligned) receives Q, or NULL.  */
+G2048_API int g2048_env_step_egreedy_dense64(g2048_env* env, const g2048_dense64_params* params,
+                                             const double* eps_dev, double eps,
+                                             double eps_decay_episodes, double eps_min,
+                                             int32_t* reward_dev, uint8_t* done_dev,
+                                             uint8_t* action_dev, g2048_replay* rb,
+                                             float* q_out_dev, void* stream);
+
+
 G2048_API int g2048_dense64_forward(const g2048_dense64_params* params, const uint8_t* rows_dev,
                                     const int64_t* idx_dev, int64_t n, float* q_out_dev,
                                     void* stream);
@@ -253,6 +267,25 @@ G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* params,
                                        const int64_t* idx_dev, const float* y_dev, int64_t batch,
                                        float* workspace_dev, float* grad_out_dev,
                                        float* loss_out_dev, uint64_t* step_dev, void* stream);
+
+/* One whole Double-DQN update of the dense net in two launches (train_step, src/dqn_lib.py:116-165,
+ * intended zero_grad -> backward -> step order): per 32-row tile the sampler (idx_in, or the
+ * Philox draw of g2048_dense64_targets with epoch *step_dev), Q_target(s') / Q_online(s') -> y,
+ * Q_online(s) -> MSE(sum) -> gradient slab; then the fixed-order slab reduction, which with
+ * exp_avg / exp_avg_sq non-NULL applies torch Adam (lr, betas, eps; t = *step_dev + 1) to the
+ * ONLINE parameters in place.  *step_dev is incremented once.  grad_out (f32[1348], nullable with
+ * Adam) receives the summed gradient -- for a data-parallel all-reduce, pass NULL Adam state here
+ * and call g2048_adam_step afterwards.  idx_out / y_out receive the rows and targets; loss_out the
+ * loss (nullable).  workspace: f32[g2048_dense64_update_workspace(batch)]. */
+G2048_API int64_t g2048_dense64_update_workspace(int64_t batch);
+G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
+                                   const g2048_dense64_params* target, g2048_replay* rb,
+                                   const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                   uint64_t* step_dev, float gamma, int double_dqn,
+                                   int64_t* idx_out_dev, float* y_out_dev, float* workspace_dev,
+                                   float* grad_out_dev, float* loss_out_dev, float* exp_avg_dev,
+                                   float* exp_avg_sq_dev, double lr, double beta1, double beta2,
+                                   double eps, void* stream);
 
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);

@@ -32,7 +32,14 @@ using namespace g2048;
 namespace {
 
 constexpr int kBlock = 256;
-enum : int { MODE_ACTIONS = 0, MODE_RANDOM = 1, MODE_EG_F32 = 2, MODE_EG_F64 = 3, MODE_INJECT = 4 };
+enum : int {
+    MODE_ACTIONS = 0,
+    MODE_RANDOM = 1,
+    MODE_EG_F32 = 2,
+    MODE_EG_F64 = 3,
+    MODE_INJECT = 4,
+    MODE_EG_REG = 5  // eps-greedy over f32 Q computed in-kernel (passed in registers)
+};
 
 struct ReplayDev {
     uint4* s;
@@ -83,7 +90,7 @@ template <int MODE>
 __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, Board& b,
                                          uint4& m, double eps, double& qs, int32_t& rew_out,
                                          uint32_t& done_out, uint32_t& legal_out,
-                                         uint32_t& act_out) {
+                                         uint32_t& act_out, float4 qreg = float4{0, 0, 0, 0}) {
     const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
     const uint4 u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
     const uint32_t legal = legal_mask(b);
@@ -100,8 +107,10 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         if (explore) {
             const uint32_t nl = __popc(legal);
             act = (fixed && nl) ? kth_bit4(legal, __umulhi(u.x, nl)) : (u.x >> 30);
-        } else if constexpr (MODE == MODE_EG_F32) {
-            const float4 q = reinterpret_cast<const float4*>(A.q)[i];
+        } else if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_REG) {
+            float4 q;
+            if constexpr (MODE == MODE_EG_REG) q = qreg;
+            else q = reinterpret_cast<const float4*>(A.q)[i];
             act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
                         : greedy_compat(q.x, q.y, q.z, q.w, legal);
             qs += (double)fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w));  // torch.max(Q) (:29)
@@ -142,7 +151,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         A.rb.d[slot] = (uint8_t)done;
     }
 
-    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
+    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG;
     uint32_t ep_idx = 0u, mx = 0u, fin_score = 0u, fin_moves = 0u;
     if (done) {
         const uint4 e0 = A.ep[i];
@@ -222,6 +231,86 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
     if (A.legal_out) A.legal_out[i] = (uint8_t)legal;
+    if (A.action_out) A.action_out[i] = (uint8_t)act;
+    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+}
+
+// The fused rollout step of the dense 16-64-4 net (BASELINE configs[2]): each lane evaluates
+// Q(s) of its own board (h = relu(W1 x + b1), Q = W2 h + b2 in the summation order of
+// k_mlp_forward, so Q and the chosen actions are bitwise those of forward +
+// g2048_env_step_egreedy) and then takes the eps-greedy step.  1 280 FMA per lane as 640
+// v_pk_fma_f32 with SGPR weight operands.  At 64k boards (1 wave per SIMD) the MLP phase is
+// bound by exposed scalar-load latency (~12k cycles, measured with s_memtime; an LDS-staged
+// variant hit the same time, bound by LDS broadcast bandwidth).
+
+template <bool kFull>
+__global__ __launch_bounds__(kBlock) void k_step_dense64(StepArgs A, const float* __restrict__ w1,
+                                                         const float* __restrict__ b1,
+                                                         const float* __restrict__ w2,
+                                                         const float* __restrict__ b2,
+                                                         float* q_out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (!kFull && i >= A.n) return;
+    Board b = load_board(A.board[i]);
+    uint4 m = A.meta[i];
+    double eps;
+    if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board
+        const double e = (double)reinterpret_cast<const uint32_t*>(A.ep)[4 * i];
+        eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
+    } else {
+        eps = A.eps_dev ? *A.eps_dev : A.eps;
+    }
+    float x[16];
+    const uint32_t rw[4] = {b.r0, b.r1, b.r2, b.r3};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[4 * r + c] = (float)((rw[r] >> (8 * c)) & 0xFFu);
+    // h_j = (p0 + p1) + (p2 + p3) with p_r the partial sum over k = r (mod 4) (bias in p0) and
+    // Q_a = e + o over even / odd j (bias in e) -- the order of forward_tile in g2048_mlp.hip.
+    // An adjacent pair of the natural [j][k] / [a][j] weights is then the SGPR-pair operand of
+    // one v_pk_fma_f32 (uniform read-only loads -> s_load): 2 packed chains per hidden unit, 4
+    // units per iteration, no LDS.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2* w1p = reinterpret_cast<const f2*>(w1);  // [j][k/2]
+    const f2* w2p = reinterpret_cast<const f2*>(w2);  // [a][j/2]
+    f2 xp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xp[u] = f2{x[2 * u], x[2 * u + 1]};
+    f2 acc2[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc2[a] = f2{b2[a], 0.f};
+#pragma unroll 2
+    for (int jj = 0; jj < 32; ++jj) {
+        float hv[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int j = 2 * jj + e;
+            f2 pa = f2{b1[j], 0.f}, pb = f2{0.f, 0.f};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                pa = __builtin_elementwise_fma(w1p[j * 8 + 2 * u], xp[2 * u], pa);
+                pb = __builtin_elementwise_fma(w1p[j * 8 + 2 * u + 1], xp[2 * u + 1], pb);
+            }
+            hv[e] = fmaxf((pa.x + pa.y) + (pb.x + pb.y), 0.f);
+        }
+        const f2 hp = f2{hv[0], hv[1]};
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc2[a] = __builtin_elementwise_fma(w2p[a * 32 + jj], hp, acc2[a]);
+    }
+    const float4 q = make_float4(acc2[0].x + acc2[0].y, acc2[1].x + acc2[1].y,
+                                 acc2[2].x + acc2[2].y, acc2[3].x + acc2[3].y);
+    if (q_out) reinterpret_cast<float4*>(q_out)[i] = q;
+    int32_t rew;
+    uint32_t done, legal, act;
+    double qs = A.qsum ? A.qsum[i] : 0.0;
+    step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act,
+                          q);
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (A.qsum) A.qsum[i] = qs;
+    if (A.reward) A.reward[i] = rew;
+    if (A.done) A.done[i] = (uint8_t)done;
     if (A.action_out) A.action_out[i] = (uint8_t)act;
     if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
 }
@@ -669,6 +758,37 @@ static int g2048_env_step_egreedy_impl(g2048_env* e, const void* q, int q_dtype,
     A.action_out = action_out;
     return q_dtype == G2048_F32 ? launch_step<MODE_EG_F32>(e, A, stream)
                                 : launch_step<MODE_EG_F64>(e, A, stream);
+}
+
+int g2048_env_step_egreedy_dense64(g2048_env* e, const g2048_dense64_params* p,
+                                   const double* eps_dev, double eps, double eps_decay_episodes,
+                                   double eps_min, int32_t* reward, uint8_t* done,
+                                   uint8_t* action_out, g2048_replay* rb, float* q_out,
+                                   void* stream) {
+    if (!e || !p || !p->w1 || !p->b1 || !p->w2 || !p->b2)
+        return fail(G2048_EINVAL, "env_step_egreedy_dense64: NULL env or parameter");
+    if (q_out && !aligned16(q_out))
+        return fail(G2048_EINVAL, "env_step_egreedy_dense64: q_out must be 16-byte aligned");
+    StepArgs A;
+    int rc = make_args(e, rb, A);
+    if (rc) return rc;
+    A.eps_dev = eps_dev;
+    A.eps = eps;
+    A.eps_decay = eps_decay_episodes > 0.0 ? eps_decay_episodes : 0.0;
+    A.eps_min = eps_min;
+    A.reward = reward;
+    A.done = done;
+    A.action_out = action_out;
+    DeviceGuard g(e->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (e->n % kBlock == 0)
+        hipLaunchKernelGGL((k_step_dense64<true>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A,
+                           p->w1, p->b1, p->w2, p->b2, q_out);
+    else
+        hipLaunchKernelGGL((k_step_dense64<false>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A,
+                           p->w1, p->b1, p->w2, p->b2, q_out);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
 }
 
 int g2048_env_step_inject(g2048_env* e, const uint8_t* actions, const int8_t* spawn_idx,

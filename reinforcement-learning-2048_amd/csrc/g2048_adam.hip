@@ -36,19 +36,8 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
 #pragma unroll
     for (int j = 1; j < kMaxTensors; ++j) k += (j < A.nt && i >= A.off[j]) ? 1 : 0;
     float* p = A.p[k] + (i - A.off[k]);
-    const double t = (double)*A.step;
-    const float step_size = (float)(A.lr / (1.0 - pow(A.b1, t)));
-    const float bc2_sqrt = (float)sqrt(1.0 - pow(A.b2, t));
-    const float w1 = (float)(1.0 - A.b1), b2 = (float)A.b2, w2 = (float)(1.0 - A.b2);
-    const float eps = (float)A.eps;
-    const float g = A.g[i];
-    float m = A.m[i];
-    m = m + w1 * (g - m);                          // lerp(m, g, 1 - b1), weight < 0.5 branch
-    const float v = A.v[i] * b2 + w2 * g * g;      // mul_(b2).addcmul_(g, g, 1 - b2)
-    A.m[i] = m;
-    A.v[i] = v;
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    *p = *p + (-step_size) * (m / denom);          // addcdiv_(m, denom, value=-step_size)
+    const g2048::AdamCoef c = g2048::adam_coef((double)*A.step, A.lr, A.b1, A.b2, A.eps);
+    *p = g2048::adam_apply(c, A.g[i], A.m + i, A.v + i, *p);
 }
 
 }  // namespace

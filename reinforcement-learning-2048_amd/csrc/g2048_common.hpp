@@ -3,3 +3,43 @@
 
 // Record a printf-style message for g2048_last_error() and return `code` (hidden symbol).
 int g2048_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#ifdef __HIPCC__
+#include <hip/hip_runtime.h>
+
+namespace g2048 {
+
+// torch.optim.Adam (single-tensor, amsgrad off, no weight decay) for one element; the scalar
+// factors are evaluated in double and rounded to f32 like torch's Python-side scalars.  Shared by
+// k_adam (g2048_adam.hip) and the dense-net reduce+Adam (g2048_mlp.hip) so both apply the same
+// float sequence.
+struct AdamCoef {
+    float step_size, bc2_sqrt, w1, b2, w2, eps;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(double t, double lr, double b1, double b2,
+                                              double eps) {
+    AdamCoef c;
+    c.step_size = (float)(lr / (1.0 - pow(b1, t)));
+    c.bc2_sqrt = (float)sqrt(1.0 - pow(b2, t));
+    c.w1 = (float)(1.0 - b1);
+    c.b2 = (float)b2;
+    c.w2 = (float)(1.0 - b2);
+    c.eps = (float)eps;
+    return c;
+}
+
+// returns the updated parameter; m / v updated in place
+__device__ __forceinline__ float adam_apply(const AdamCoef& c, float g, float* m_, float* v_,
+                                            float p) {
+    float m = *m_;
+    m = m + c.w1 * (g - m);                      // lerp(m, g, 1 - b1), weight < 0.5 branch
+    const float v = *v_ * c.b2 + c.w2 * g * g;   // mul_(b2).addcmul_(g, g, 1 - b2)
+    *m_ = m;
+    *v_ = v;
+    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    return p + (-c.step_size) * (m / denom);     // addcdiv_(m, denom, value=-step_size)
+}
+
+}  // namespace g2048
+#endif

@@ -19,28 +19,35 @@
 
 namespace {
 
-constexpr int S = 64, NT = 256, H = 64;
+constexpr int NT = 256, H = 64;
 constexpr int XS = 17, W1S = 17, HS = 65, W2S = 65;
+constexpr int S_FWD = 64;  // boards per tile: forward / targets / train_grad launches
+constexpr int S_UPD = 32;  // the fused update (batch 8192 -> 256 tiles = one per CU)
 // torch order: 0.weight [64][16], 0.bias [64], 2.weight [4][64], 2.bias [4]
 constexpr int P_W1 = 0, P_B1 = 1024, P_W2 = 1088, P_B2 = 1344, P_N = 1348;
 constexpr int SLAB = 1352;  // params + loss, padded
+constexpr int MAX_SLABS = 256;
 
 struct MlpW {
     const float *w1, *b1, *w2, *b2;
 };
 
-struct Lds {
-    float x[S * XS];
+struct LW {  // one net's weights in LDS
     float w1[H * W1S];
     float b1[H];
     float w2[4 * W2S];
     float b2[4];
+};
+
+template <int S>
+struct Tile {  // one tile of S boards
+    float x[S * XS];
     float h[S * HS];
     float q[S * 4];
     float a[S], y[S], g[S];
 };
 
-__device__ __forceinline__ void stage_weights(const MlpW& W, Lds& L) {
+__device__ __forceinline__ void stage_weights(const MlpW& W, LW& L) {
     const int t = threadIdx.x;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -52,14 +59,16 @@ __device__ __forceinline__ void stage_weights(const MlpW& W, Lds& L) {
     if (t < 4) L.b2[t] = W.b2[t];
 }
 
-__device__ __forceinline__ void stage_boards(Lds& L, const uint8_t* rows, const int64_t* idx,
+template <int S>
+__device__ __forceinline__ void stage_boards(Tile<S>& T, const uint8_t* rows, const int64_t* idx,
                                              int64_t b0, int64_t n) {
-    const int t = threadIdx.x;  // 64 boards x 4 words
+    const int t = threadIdx.x;  // S boards x 4 words
+    if (t >= 4 * S) return;
     const int s = t >> 2, w = t & 3;
     const int64_t b = b0 + s;
     uint32_t v = 0;
     if (b < n) v = reinterpret_cast<const uint32_t*>(rows)[(idx ? idx[b] : b) * 4 + w];
-    float* dst = L.x + s * XS + w * 4;
+    float* dst = T.x + s * XS + w * 4;
     dst[0] = (float)(v & 0xFFu);
     dst[1] = (float)((v >> 8) & 0xFFu);
     dst[2] = (float)((v >> 16) & 0xFFu);
@@ -67,32 +76,148 @@ __device__ __forceinline__ void stage_boards(Lds& L, const uint8_t* rows, const 
 }
 
 // weights + boards staged (caller syncs); leaves h (post-ReLU) and q in LDS, ends with a sync
-__device__ __forceinline__ void forward_tile(Lds& L) {
+template <int S>
+__device__ __forceinline__ void forward_tile(Tile<S>& T, const LW& W) {
     const int t = threadIdx.x;
     {
-        const int j = t & 63, s0 = (t >> 6) * 16;
+        constexpr int SPT = S / 4;  // boards per thread
+        const int j = t & 63, s0 = (t >> 6) * SPT;
         float w[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = L.w1[j * W1S + i];
-        const float bb = L.b1[j];
+        for (int i = 0; i < 16; ++i) w[i] = W.w1[j * W1S + i];
+        const float bb = W.b1[j];
+        // h = (p0 + p1) + (p2 + p3), p_r summing i = r (mod 4) with the bias in p0: the order
+        // of the packed (v_pk_fma_f32) Q evaluation inside the fused step kernel (g2048.hip
+        // k_step_dense64), so the two agree bit for bit
 #pragma unroll 4
-        for (int ss = 0; ss < 16; ++ss) {
+        for (int ss = 0; ss < SPT; ++ss) {
             const int s = s0 + ss;
-            float v = bb;
+            float p[4] = {bb, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) v = fmaf(w[i], L.x[s * XS + i], v);
-            L.h[s * HS + j] = fmaxf(v, 0.f);
+            for (int i = 0; i < 16; ++i) p[i & 3] = fmaf(w[i], T.x[s * XS + i], p[i & 3]);
+            T.h[s * HS + j] = fmaxf((p[0] + p[1]) + (p[2] + p[3]), 0.f);
         }
     }
     __syncthreads();
-    {
+    if (t < 4 * S) {
         const int s = t >> 2, a = t & 3;
-        float v = L.b2[a];
+        float e = W.b2[a], o = 0.f;  // even / odd j, same order as k_step_dense64
 #pragma unroll 16
-        for (int j = 0; j < H; ++j) v = fmaf(L.w2[a * W2S + j], L.h[s * HS + j], v);
-        L.q[t] = v;
+        for (int j = 0; j < H; j += 2) {
+            e = fmaf(W.w2[a * W2S + j], T.h[s * HS + j], e);
+            o = fmaf(W.w2[a * W2S + j + 1], T.h[s * HS + j + 1], o);
+        }
+        T.q[t] = e + o;
     }
     __syncthreads();
+}
+
+// Double-DQN target of board t of the tile (src/dqn_lib.py:125-132): qo = Q_online(s'),
+// qt = Q_target(s') rows of this board
+__device__ __forceinline__ float bellman(const float* qo, const float* qt, int32_t r, uint8_t d,
+                                         float gamma, int double_dqn) {
+#pragma clang fp contract(off)
+    float next;
+    if (double_dqn) {
+        int a = 0;
+        float best = qo[0];
+        for (int k = 1; k < 4; ++k)
+            if (qo[k] > best) { best = qo[k]; a = k; }
+        next = qt[a];
+    } else {
+        next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+    }
+    const float disc = (float)(1 - (int)d) * gamma;
+    return (float)r + disc * next;
+}
+
+// uniform ring index of minibatch row b, the draw of k_sample (domain 3)
+__device__ __forceinline__ int64_t sample_row(int64_t b, unsigned long long ep,
+                                              unsigned long long count, uint32_t lo, uint32_t hi) {
+    const uint4 u = g2048::philox10(
+        make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
+                   (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
+        lo, hi);
+    return (int64_t)__umul64hi(((unsigned long long)u.y << 32) | u.x, count);
+}
+
+struct GradAcc {  // per-thread gradient accumulators, persistent across a workgroup's tiles
+    float w1[4] = {0.f, 0.f, 0.f, 0.f};
+    float b1 = 0.f, w2 = 0.f, b2 = 0.f, loss = 0.f;
+};
+
+// forward + MSE + backward of one staged tile (x, a, y and the validity mask g in LDS, synced)
+template <int S>
+__device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, GradAcc& G) {
+    const int t = threadIdx.x;
+    forward_tile<S>(T, W);
+    if (t < S) {  // loss and dq = 2 (q - y) at the taken action
+        const float d = (T.q[t * 4 + (int)T.a[t]] - T.y[t]) * T.g[t];
+        G.loss = fmaf(d, d, G.loss);
+        T.g[t] = 2.f * d;
+    }
+    __syncthreads();
+    {  // dW2[a][j] / db2[a]: thread (a = t>>6, j = t&63)
+        const int a = t >> 6, j = t & 63;
+        float gw = 0.f, gb = 0.f;
+#pragma unroll 8
+        for (int s = 0; s < S; ++s) {
+            const float g = (int)T.a[s] == a ? T.g[s] : 0.f;
+            gw = fmaf(g, T.h[s * HS + j], gw);
+            gb += g;
+        }
+        G.w2 += gw;
+        if (j == 0) G.b2 += gb;
+    }
+    __syncthreads();
+    {  // dh = dq * W2[a] * relu'(h), in place
+        constexpr int SPT = S / 4;
+        const int j = t & 63, s0 = (t >> 6) * SPT;
+#pragma unroll 4
+        for (int ss = 0; ss < SPT; ++ss) {
+            const int s = s0 + ss;
+            const float hv = T.h[s * HS + j];
+            T.h[s * HS + j] = hv > 0.f ? T.g[s] * W.w2[(int)T.a[s] * W2S + j] : 0.f;
+        }
+    }
+    __syncthreads();
+    {  // dW1[j][i0..i0+3]: thread (j = t>>2, i0 = 4*(t&3)); db1 by threads j < 64
+        const int j = t >> 2, i0 = (t & 3) * 4;
+#pragma unroll 8
+        for (int s = 0; s < S; ++s) {
+            const float dh = T.h[s * HS + j];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) G.w1[u] = fmaf(dh, T.x[s * XS + i0 + u], G.w1[u]);
+        }
+        if (t < H) {
+            float v = 0.f;
+#pragma unroll 8
+            for (int s = 0; s < S; ++s) v += T.h[s * HS + t];
+            G.b1 += v;
+        }
+    }
+}
+
+// the workgroup's gradient slab in torch parameter order + its loss (scratch: S*4 >= 64 floats)
+template <int S>
+__device__ __forceinline__ void write_slab(const GradAcc& G, Tile<S>& T, float* slab) {
+    const int t = threadIdx.x;
+    {
+        const int j = t >> 2, i0 = (t & 3) * 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) slab[P_W1 + j * 16 + i0 + u] = G.w1[u];
+    }
+    if (t < H) slab[P_B1 + t] = G.b1;
+    slab[P_W2 + t] = G.w2;  // t = a*64 + j
+    if ((t & 63) == 0) slab[P_B2 + (t >> 6)] = G.b2;
+    __syncthreads();
+    if (t < S) T.q[t] = G.loss;  // threads >= S hold 0
+    __syncthreads();
+    if (t == 0) {
+        float v = 0.f;
+        for (int i = 0; i < S; ++i) v += T.q[i];
+        slab[P_N] = v;
+    }
 }
 
 struct FwdArgs {
@@ -104,14 +229,16 @@ struct FwdArgs {
 };
 
 __global__ __launch_bounds__(NT) void k_mlp_forward(FwdArgs A) {
-    __shared__ Lds L;
+    constexpr int S = S_FWD;
+    __shared__ LW W;
+    __shared__ Tile<S> T;
     const int64_t b0 = (int64_t)blockIdx.x * S;
-    stage_weights(A.W, L);
-    stage_boards(L, A.rows, A.idx, b0, A.n);
+    stage_weights(A.W, W);
+    stage_boards<S>(T, A.rows, A.idx, b0, A.n);
     __syncthreads();
-    forward_tile(L);
+    forward_tile<S>(T, W);
     const int t = threadIdx.x;
-    if (b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = L.q[t];
+    if (b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = T.q[t];
 }
 
 struct TargetArgs {
@@ -131,7 +258,9 @@ struct TargetArgs {
 };
 
 __global__ __launch_bounds__(NT) void k_mlp_targets(TargetArgs A) {
-    __shared__ Lds L;
+    constexpr int S = S_FWD;
+    __shared__ LW W;
+    __shared__ Tile<S> T;
     __shared__ float qon[S * 4];
     __shared__ int64_t sidx[S];
     const int t = threadIdx.x;
@@ -140,46 +269,23 @@ __global__ __launch_bounds__(NT) void k_mlp_targets(TargetArgs A) {
         const int64_t b = b0 + t;
         int64_t j = 0;
         if (b < A.batch) {
-            if (A.idx_in) {
-                j = A.idx_in[b];
-            } else {  // same draw as k_sample (domain 3)
-                const unsigned long long ep = *A.epoch;
-                const uint4 u = g2048::philox10(
-                    make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
-                               (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
-                    A.seed_lo, A.seed_hi);
-                j = (int64_t)__umul64hi(((unsigned long long)u.y << 32) | u.x, *A.count);
-            }
+            j = A.idx_in ? A.idx_in[b] : sample_row(b, *A.epoch, *A.count, A.seed_lo, A.seed_hi);
             A.idx_out[b] = j;
         }
         sidx[t] = j;
     }
-    stage_weights(A.on, L);
+    stage_weights(A.on, W);
     __syncthreads();
-    stage_boards(L, A.s2, sidx, 0, S);
+    stage_boards<S>(T, A.s2, sidx, 0, S);
     __syncthreads();
-    forward_tile(L);
-    qon[t] = L.q[t];
-    stage_weights(A.tg, L);  // forward_tile ended with a sync: the online weights are dead
+    forward_tile<S>(T, W);
+    qon[t] = T.q[t];
+    stage_weights(A.tg, W);  // forward_tile ended with a sync: the online weights are dead
     __syncthreads();
-    forward_tile(L);
+    forward_tile<S>(T, W);
     if (t < S && b0 + t < A.batch) {
-#pragma clang fp contract(off)
-        const float* qo = qon + t * 4;
-        const float* qt = L.q + t * 4;
-        float next;
-        if (A.double_dqn) {
-            int a = 0;
-            float best = qo[0];
-            for (int k = 1; k < 4; ++k)
-                if (qo[k] > best) { best = qo[k]; a = k; }
-            next = qt[a];
-        } else {
-            next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
-        }
         const int64_t j = sidx[t];
-        const float disc = (float)(1 - (int)A.d[j]) * A.gamma;
-        A.y[b0 + t] = (float)A.r[j] + disc * next;
+        A.y[b0 + t] = bellman(qon + t * 4, T.q + t * 4, A.r[j], A.d[j], A.gamma, A.double_dqn);
     }
 }
 
@@ -195,117 +301,157 @@ struct TrainArgs {
 };
 
 __global__ __launch_bounds__(NT) void k_mlp_train(TrainArgs A) {
-    __shared__ Lds L;
+    constexpr int S = S_FWD;
+    __shared__ LW W;
+    __shared__ Tile<S> T;
     const int t = threadIdx.x;
     if (A.step && blockIdx.x == 0 && t == 0) *A.step += 1ull;
-    stage_weights(A.W, L);
-    float gW1[4] = {0, 0, 0, 0}, gB1 = 0.f, gW2 = 0.f, gB2 = 0.f, gLoss = 0.f;
+    stage_weights(A.W, W);
+    GradAcc G;
     const int64_t ntiles = (A.batch + S - 1) / S;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * S;
         __syncthreads();
-        stage_boards(L, A.rows, A.idx, b0, A.batch);
+        stage_boards<S>(T, A.rows, A.idx, b0, A.batch);
         if (t < S) {
             const int64_t b = b0 + t;
             const bool ok = b < A.batch;
-            L.a[t] = ok ? (float)A.actions[A.idx[b]] : 0.f;
-            L.y[t] = ok ? A.y[b] : 0.f;
-            L.g[t] = ok ? 1.f : 0.f;
+            T.a[t] = ok ? (float)A.actions[A.idx[b]] : 0.f;
+            T.y[t] = ok ? A.y[b] : 0.f;
+            T.g[t] = ok ? 1.f : 0.f;
         }
         __syncthreads();
-        forward_tile(L);
-        if (t < S) {  // loss and dq = 2 (q - y) at the taken action
-            const float d = (L.q[t * 4 + (int)L.a[t]] - L.y[t]) * L.g[t];
-            gLoss = fmaf(d, d, gLoss);
-            L.g[t] = 2.f * d;
-        }
-        __syncthreads();
-        {  // dW2[a][j] / db2[a]: thread (a = t>>6, j = t&63)
-            const int a = t >> 6, j = t & 63;
-            float gw = 0.f, gb = 0.f;
-#pragma unroll 8
-            for (int s = 0; s < S; ++s) {
-                const float g = (int)L.a[s] == a ? L.g[s] : 0.f;
-                gw = fmaf(g, L.h[s * HS + j], gw);
-                gb += g;
-            }
-            gW2 += gw;
-            if (j == 0) gB2 += gb;
-        }
-        __syncthreads();
-        {  // dh = dq * W2[a] * relu'(h), in place
-            const int j = t & 63, s0 = (t >> 6) * 16;
-#pragma unroll 4
-            for (int ss = 0; ss < 16; ++ss) {
-                const int s = s0 + ss;
-                const float hv = L.h[s * HS + j];
-                L.h[s * HS + j] = hv > 0.f ? L.g[s] * L.w2[(int)L.a[s] * W2S + j] : 0.f;
-            }
-        }
-        __syncthreads();
-        {  // dW1[j][i0..i0+3]: thread (j = t>>2, i0 = 4*(t&3)); db1 by threads j < 64
-            const int j = t >> 2, i0 = (t & 3) * 4;
-#pragma unroll 8
-            for (int s = 0; s < S; ++s) {
-                const float dh = L.h[s * HS + j];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) gW1[u] = fmaf(dh, L.x[s * XS + i0 + u], gW1[u]);
-            }
-            if (t < H) {
-                float v = 0.f;
-#pragma unroll 8
-                for (int s = 0; s < S; ++s) v += L.h[s * HS + t];
-                gB1 += v;
-            }
-        }
+        grad_tile<S>(T, W, G);
     }
-    float* slab = A.slab + (int64_t)blockIdx.x * SLAB;
-    {
-        const int j = t >> 2, i0 = (t & 3) * 4;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) slab[P_W1 + j * 16 + i0 + u] = gW1[u];
-    }
-    if (t < H) slab[P_B1 + t] = gB1;
-    slab[P_W2 + t] = gW2;  // t = a*64 + j
-    if ((t & 63) == 0) slab[P_B2 + (t >> 6)] = gB2;
-    __syncthreads();
-    L.q[t] = gLoss;  // reuse as scratch (threads >= 64 hold 0)
-    __syncthreads();
-    if (t == 0) {
-        float v = 0.f;
-        for (int i = 0; i < S; ++i) v += L.q[i];
-        slab[P_N] = v;
-    }
+    write_slab<S>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
 }
 
-// block = 64 slab positions x 4 waves (wave w sums slabs w, w+4, ...), fixed-order combine
-__global__ __launch_bounds__(256) void k_mlp_reduce(const float* slab, int nslab, float* grad,
-                                                    float* loss) {
+// The whole graded + target half of train_step in one launch (src/dqn_lib.py:116-161): per tile
+// of S_UPD minibatch rows, draw the ring rows, Q_target(s') and Q_online(s') -> y, then
+// Q_online(s) -> MSE -> gradient slab.  Both nets' weights are staged once per workgroup.
+// *step is the sampler epoch (read only here); block 0 publishes *step + 1 in *step_next, which
+// the reduction commits to *step (Adam's t) -- no block reads a value another block writes.
+struct UpdateArgs {
+    MlpW on, tg;
+    const uint8_t *s, *a, *s2, *d;
+    const int32_t* r;
+    const unsigned long long* count;
+    const unsigned long long* step;
+    const int64_t* idx_in;
+    int64_t batch;
+    uint32_t seed_lo, seed_hi;
+    float gamma;
+    int double_dqn;
+    int64_t* idx_out;
+    float* y_out;
+    float* slab;
+    unsigned long long* step_next;
+};
+
+__global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
+    constexpr int S = S_UPD;
+    __shared__ LW Won, Wtg;
+    __shared__ Tile<S> T;
+    __shared__ float qtg[S * 4];
+    __shared__ int64_t sidx[S];
+    const int t = threadIdx.x;
+    const unsigned long long ep = A.idx_in ? 0ull : *A.step;
+    const unsigned long long count = A.idx_in ? 0ull : *A.count;
+    if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
+    stage_weights(A.on, Won);
+    stage_weights(A.tg, Wtg);
+    GradAcc G;
+    const int64_t ntiles = (A.batch + S - 1) / S;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b0 = tile * S;
+        int32_t rj = 0;
+        uint8_t dj = 0;
+        __syncthreads();
+        if (t < S) {
+            const int64_t b = b0 + t;
+            const bool ok = b < A.batch;
+            int64_t j = 0;
+            if (ok) {
+                j = A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+                A.idx_out[b] = j;
+                rj = A.r[j];
+                dj = A.d[j];
+            }
+            sidx[t] = j;
+            T.a[t] = ok ? (float)A.a[j] : 0.f;
+            T.g[t] = ok ? 1.f : 0.f;
+        }
+        __syncthreads();
+        stage_boards<S>(T, A.s2, sidx, 0, S);
+        __syncthreads();
+        forward_tile<S>(T, Wtg);
+        if (t < 4 * S) qtg[t] = T.q[t];
+        forward_tile<S>(T, Won);
+        if (t < S) {
+            const float y = bellman(T.q + t * 4, qtg + t * 4, rj, dj, A.gamma, A.double_dqn);
+            T.y[t] = y;
+            if (b0 + t < A.batch) A.y_out[b0 + t] = y;
+        }
+        __syncthreads();  // T.x is restaged below; T.y visible to grad_tile
+        stage_boards<S>(T, A.s, sidx, 0, S);
+        __syncthreads();
+        grad_tile<S>(T, Won, G);
+    }
+    write_slab<S>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
+}
+
+// block = 64 slab positions x 4 waves (wave w sums slabs w, w+4, ...), fixed-order combine.
+// With `adam`, the summed gradient of each parameter is applied right here (torch Adam, t read
+// from *step_next) and *step_next is committed to *step.
+struct ReduceArgs {
+    const float* slab;
+    int nslab;
+    float* grad;
+    float* loss;
+    const unsigned long long* step_next;
+    unsigned long long* step;
+    float* p[4];  // w1, b1, w2, b2 (updated in place when adam)
+    float* m;
+    float* v;
+    double lr, b1, b2, eps;
+    int adam;
+};
+
+__global__ __launch_bounds__(256) void k_mlp_reduce(ReduceArgs A) {
     __shared__ float part[4][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
     float v = 0.f;
     if (pos <= P_N) {
         int g = wave;
-        for (; g + 28 < nslab; g += 32) {
+        for (; g + 28 < A.nslab; g += 32) {
             float r[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) r[u] = slab[(int64_t)(g + 4 * u) * SLAB + pos];
+            for (int u = 0; u < 8; ++u) r[u] = A.slab[(int64_t)(g + 4 * u) * SLAB + pos];
 #pragma unroll
             for (int u = 0; u < 8; ++u) v += r[u];
         }
-        for (; g < nslab; g += 4) v += slab[(int64_t)g * SLAB + pos];
+        for (; g < A.nslab; g += 4) v += A.slab[(int64_t)g * SLAB + pos];
     }
     part[wave][lane] = v;
     __syncthreads();
     if (wave == 0 && pos <= P_N) {
         const float sum = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
         if (pos == P_N) {
-            if (loss) *loss = sum;
+            if (A.loss) *A.loss = sum;
         } else {
-            grad[pos] = sum;
+            if (A.grad) A.grad[pos] = sum;
+            if (A.adam) {
+                const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
+                const int base[4] = {P_W1, P_B1, P_W2, P_B2};
+                float* p = A.p[k] + (pos - base[k]);
+                const g2048::AdamCoef c =
+                    g2048::adam_coef((double)*A.step_next, A.lr, A.b1, A.b2, A.eps);
+                *p = g2048::adam_apply(c, sum, A.m + pos, A.v + pos, *p);
+            }
         }
     }
+    if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
 }
 
 inline MlpW mlp_w(const g2048_dense64_params* p) { return MlpW{p->w1, p->b1, p->w2, p->b2}; }
@@ -321,7 +467,7 @@ extern "C" G2048_API int g2048_dense64_forward(const g2048_dense64_params* p, co
     if (!ok_params(p) || !rows || !q_out || n <= 0)
         return g2048_fail(G2048_EINVAL, "dense64_forward: NULL argument or n <= 0");
     FwdArgs A{mlp_w(p), rows, idx, n, q_out};
-    hipLaunchKernelGGL(k_mlp_forward, dim3((unsigned)((n + S - 1) / S)), dim3(NT), 0,
+    hipLaunchKernelGGL(k_mlp_forward, dim3((unsigned)((n + S_FWD - 1) / S_FWD)), dim3(NT), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "dense64_forward: %s", hipGetErrorString(e));
@@ -358,15 +504,15 @@ extern "C" G2048_API int g2048_dense64_targets(const g2048_dense64_params* onlin
     A.double_dqn = double_dqn;
     A.idx_out = idx_out;
     A.y = y_out;
-    hipLaunchKernelGGL(k_mlp_targets, dim3((unsigned)((batch + S - 1) / S)), dim3(NT), 0,
+    hipLaunchKernelGGL(k_mlp_targets, dim3((unsigned)((batch + S_FWD - 1) / S_FWD)), dim3(NT), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "dense64_targets: %s", hipGetErrorString(e));
 }
 
 extern "C" G2048_API int64_t g2048_dense64_train_workspace(int64_t batch) {
-    const int64_t ntiles = (batch + S - 1) / S;
-    return (ntiles < 256 ? ntiles : 256) * SLAB;
+    const int64_t ntiles = (batch + S_FWD - 1) / S_FWD;
+    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB;
 }
 
 extern "C" G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* p,
@@ -377,16 +523,95 @@ extern "C" G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* p,
                                                   void* stream) {
     if (!ok_params(p) || !rows || !actions || !idx || !y || !workspace || !grad_out || batch <= 0)
         return g2048_fail(G2048_EINVAL, "dense64_train_grad: NULL argument or batch <= 0");
-    const int64_t ntiles = (batch + S - 1) / S;
-    const int grid = (int)(ntiles < 256 ? ntiles : 256);
+    const int64_t ntiles = (batch + S_FWD - 1) / S_FWD;
+    const int grid = (int)(ntiles < MAX_SLABS ? ntiles : MAX_SLABS);
     TrainArgs A{mlp_w(p), rows, actions, idx, y, batch, workspace,
                 reinterpret_cast<unsigned long long*>(step_dev)};
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_mlp_train, dim3(grid), dim3(NT), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_mlp_train: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(256), 0, st, workspace, grid,
-                       grad_out, loss_out);
+    ReduceArgs R{};
+    R.slab = workspace;
+    R.nslab = grid;
+    R.grad = grad_out;
+    R.loss = loss_out;
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(256), 0, st, R);
+    e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int64_t g2048_dense64_update_workspace(int64_t batch) {
+    const int64_t ntiles = (batch + S_UPD - 1) / S_UPD;
+    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + 2;  // + the u64 step_next word
+}
+
+extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
+                                              const g2048_dense64_params* target,
+                                              g2048_replay* rb, const int64_t* idx_in,
+                                              int64_t batch, uint64_t seed, uint64_t* step_dev,
+                                              float gamma, int double_dqn, int64_t* idx_out,
+                                              float* y_out, float* workspace, float* grad_out,
+                                              float* loss_out, float* exp_avg, float* exp_avg_sq,
+                                              double lr, double beta1, double beta2, double eps,
+                                              void* stream) {
+    if (!ok_params(online) || !ok_params(target) || !rb || batch <= 0 || !step_dev || !idx_out ||
+        !y_out || !workspace)
+        return g2048_fail(G2048_EINVAL, "dense64_update: NULL argument or batch <= 0");
+    if ((exp_avg == nullptr) != (exp_avg_sq == nullptr) || (!exp_avg && !grad_out))
+        return g2048_fail(G2048_EINVAL,
+                          "dense64_update: need exp_avg and exp_avg_sq (Adam) or grad_out");
+    uint8_t *s = nullptr, *a = nullptr, *s2 = nullptr, *d = nullptr;
+    int32_t* r = nullptr;
+    uint64_t* count = nullptr;
+    if (g2048_replay_views(rb, &s, &s2, &a, &r, &d, &count) != G2048_OK) return G2048_EINVAL;
+    const int64_t ntiles = (batch + S_UPD - 1) / S_UPD;
+    const int grid = (int)(ntiles < MAX_SLABS ? ntiles : MAX_SLABS);
+    unsigned long long* step_next =
+        reinterpret_cast<unsigned long long*>(workspace + (int64_t)grid * SLAB);
+    UpdateArgs U;
+    U.on = mlp_w(online);
+    U.tg = mlp_w(target);
+    U.s = s;
+    U.a = a;
+    U.s2 = s2;
+    U.d = d;
+    U.r = r;
+    U.count = reinterpret_cast<const unsigned long long*>(count);
+    U.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    U.idx_in = idx_in;
+    U.batch = batch;
+    U.seed_lo = (uint32_t)seed;
+    U.seed_hi = (uint32_t)(seed >> 32);
+    U.gamma = gamma;
+    U.double_dqn = double_dqn;
+    U.idx_out = idx_out;
+    U.y_out = y_out;
+    U.slab = workspace;
+    U.step_next = step_next;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_mlp_update, dim3(grid), dim3(NT), 0, st, U);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_mlp_update: %s", hipGetErrorString(e));
+    ReduceArgs R{};
+    R.slab = workspace;
+    R.nslab = grid;
+    R.grad = grad_out;
+    R.loss = loss_out;
+    R.step_next = step_next;
+    R.step = reinterpret_cast<unsigned long long*>(step_dev);
+    R.adam = exp_avg != nullptr;
+    R.p[0] = const_cast<float*>(online->w1);
+    R.p[1] = const_cast<float*>(online->b1);
+    R.p[2] = const_cast<float*>(online->w2);
+    R.p[3] = const_cast<float*>(online->b2);
+    R.m = exp_avg;
+    R.v = exp_avg_sq;
+    R.lr = lr;
+    R.b1 = beta1;
+    R.b2 = beta2;
+    R.eps = eps;
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(256), 0, st, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
 }

@@ -40,6 +40,8 @@ SIGNATURES = {
     "g2048_env_set_epoch": (_int, [_vp, _u32]),
     "g2048_env_set_episode_log": (_int, [_vp, _vp, _i64, _vp]),
     "g2048_env_legal_mask": (_int, [_vp, _vp, _vp]),
+    "g2048_env_step_egreedy_dense64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp, _vp,
+                                              _vp, _vp]),
     "g2048_replay_create": (_int, [_pp, _i64, _int, _vp]),
     "g2048_replay_wrap": (_int, [_pp, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "g2048_replay_destroy": (None, [_vp]),
@@ -57,6 +59,9 @@ SIGNATURES = {
                                      _vp, _vp]),
     "g2048_dense64_train_workspace": (_i64, [_i64]),
     "g2048_dense64_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "g2048_dense64_update_workspace": (_i64, [_i64]),
+    "g2048_dense64_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
     "g2048_last_error": (C.c_char_p, []),
     "g2048_abi_version": (_int, []),
 }

@@ -112,6 +112,7 @@ class VecEnv2048:
         self.meta = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
         self.ep = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
         self._h = C.c_void_p()
+        self._destroy = lib.g2048_env_destroy
         with torch.cuda.device(self.device):
             N.check(lib.g2048_env_wrap(C.byref(self._h), self.n, self.seed, self.board_offset,
                                        self.device.index, self.flags, N.ptr(self.board),
@@ -119,9 +120,12 @@ class VecEnv2048:
                                        N.stream_of(self.device)), "g2048_env_wrap")
 
     def __del__(self):
+        # the destroy entry point is bound at construction: at interpreter exit the module
+        # globals this would otherwise go through may already be torn down
         h = getattr(self, "_h", None)
-        if h:
-            N.load().g2048_env_destroy(h)
+        destroy = getattr(self, "_destroy", None)
+        if h and destroy is not None:
+            destroy(h)
             self._h = None
 
     def __len__(self):
@@ -221,6 +225,31 @@ class VecEnv2048:
                                                 self._stream()), "g2048_env_step_egreedy")
         return action, reward, done
 
+    def step_egreedy_dense64(self, params, epsilon=0.0, replay: "ReplayBuffer | None" = None,
+                             reward=None, done=None, action=None, eps_schedule=None, q_out=None):
+        """play_one_step for every board with the dense 16-64-4 Q-net computed INSIDE the step
+        kernel (g2048_env_step_egreedy_dense64): params = qnet.net_params(model) of an fp32
+        dense64 net.  Same epsilon forms as step_egreedy.  Returns (action, reward, done)."""
+        if eps_schedule is not None:
+            eps_ptr, eps_val, dec, mn = None, 0.0, float(eps_schedule[0]), float(eps_schedule[1])
+        elif isinstance(epsilon, torch.Tensor):
+            if epsilon.dtype != torch.float64 or epsilon.device != self.device or epsilon.numel() != 1:
+                raise ValueError("epsilon tensor must be one float64 on the env device")
+            eps_ptr, eps_val, dec, mn = N.ptr(epsilon), 0.0, 0.0, 0.0
+        else:
+            eps_ptr, eps_val, dec, mn = None, float(epsilon), 0.0, 0.0
+        if q_out is not None and (q_out.shape != (self.n, 4) or q_out.dtype != torch.float32
+                                  or not q_out.is_contiguous()):
+            raise ValueError(f"q_out must be a contiguous float32 [{self.n}, 4] tensor")
+        reward = self._out(reward, torch.int32)
+        done = self._out(done, torch.uint8)
+        action = self._out(action, torch.uint8)
+        N.check(N.load().g2048_env_step_egreedy_dense64(
+            self._h, C.byref(params), eps_ptr, eps_val, dec, mn, N.ptr(reward), N.ptr(done),
+            N.ptr(action), replay.handle if replay is not None else None, N.ptr(q_out),
+            self._stream()), "g2048_env_step_egreedy_dense64")
+        return action, reward, done
+
     def step_inject(self, actions, spawn_idx, spawn_exp):
         """Test entry: the given actions with the given spawn cells (-1 = none) / exponents."""
         actions = self._u8(actions, "actions")
@@ -312,6 +341,7 @@ class ReplayBuffer:
         self.d = torch.zeros(self.capacity, dtype=torch.uint8, **kw)
         self.count = torch.zeros(1, dtype=torch.int64, **kw)
         self._h = C.c_void_p()
+        self._destroy = N.load().g2048_replay_destroy
         with torch.cuda.device(self.device):
             N.check(N.load().g2048_replay_wrap(C.byref(self._h), self.capacity, self.device.index,
                                                N.ptr(self.s), N.ptr(self.s2), N.ptr(self.a),
@@ -319,9 +349,12 @@ class ReplayBuffer:
                     "g2048_replay_wrap")
 
     def __del__(self):
+        # the destroy entry point is bound at construction: at interpreter exit the module
+        # globals this would otherwise go through may already be torn down
         h = getattr(self, "_h", None)
-        if h:
-            N.load().g2048_replay_destroy(h)
+        destroy = getattr(self, "_destroy", None)
+        if h and destroy is not None:
+            destroy(h)
             self._h = None
 
     @property

@@ -64,6 +64,7 @@ class DQNLearner:
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
         self.kind = qnet.kind_of(self.model)
         self.fused = self.kind is not None
+        self._upd = None
         if self.fused:
             self._p_on = qnet.net_params(self.model)
             self._p_tgt = qnet.net_params(self.target)
@@ -76,6 +77,11 @@ class DQNLearner:
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
             self._adam = FusedAdam(params, lr=lr)
+            # dense64: sampler + targets + gradient in ONE launch, and (single process) Adam
+            # folded into the gradient reduction -- 2 launches per update
+            self._upd = (qnet.Dense64Update(self.model, self.target, self.B,
+                                            adam=self._adam if self.world == 1 else None)
+                         if self.kind == "dense64" else None)
             rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
             self.sample_seed = (int(seed) * 0x9E3779B9 + 0x2048 + (rank << 40)) & ((1 << 64) - 1)
 
@@ -95,6 +101,11 @@ class DQNLearner:
         idx = None if self.fused else self._sample_idx()
         if self.fused:
             idx_in = self.sampler(self.B, self.replay) if self.sampler is not None else None
+            if self._upd is not None:
+                self._upd(self.replay, self._idx, self._y, self.step_dev, self.gamma,
+                          self.use_double_dqn, self.sample_seed, idx_in,
+                          grad_out=self.grad_flat, loss_out=self.last_loss)
+                return
             qnet.targets(self.kind, self._p_on, self._p_tgt, self.replay, self.B, self._idx,
                          self._y, self.gamma, self.use_double_dqn, self.sample_seed, self.step_dev,
                          idx_in)
@@ -113,6 +124,8 @@ class DQNLearner:
         self.bucket.allreduce_mean_(self.pg)
 
     def _apply(self):
+        if self._upd is not None and self._upd.adam is not None:
+            return  # applied inside the dense64 update's reduction
         if self.fused:
             self._adam.step(self.grad_flat, self.step_dev)
         else:
@@ -253,7 +266,8 @@ class Trainer:
     """Vectorised training_loop (src/dqn_lib.py:167-244).
 
     Per iteration: Q = online(boards) -> fused epsilon-greedy step of all N boards with replay
-    append -> `updates_per_step` learner updates once the ring holds `min_fill` transitions.
+    append (for the fp32 dense 16-64-4 net, Q is computed inside the step kernel itself) ->
+    `updates_per_step` learner updates once the ring holds `min_fill` transitions.
     epsilon_b = max((eps_decay_episodes - e_b) / eps_decay_episodes, min_epsilon) with e_b the
     number of episodes board b has finished -- the reference's per-episode schedule (:184-188)
     applied per board inside the fused step kernel.  Every finished episode is appended to the
@@ -297,12 +311,18 @@ class Trainer:
         self.steps += steps
 
     def step(self) -> None:
-        q = self.learner.q_values(self.env)
         if self.track:
             row = self.steps % self.history_len
             self.h_s[row].copy_(self.env.board[:self.track])
-        self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward, done=self._done,
-                              action=self._action, eps_schedule=(self.eps_decay, self.min_eps))
+        sched = (self.eps_decay, self.min_eps)
+        if self.learner.kind == "dense64":  # Q computed inside the step kernel (one launch)
+            self.env.step_egreedy_dense64(self.learner._p_on, replay=self.replay,
+                                          reward=self._reward, done=self._done,
+                                          action=self._action, eps_schedule=sched)
+        else:
+            q = self.learner.q_values(self.env)
+            self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward,
+                                  done=self._done, action=self._action, eps_schedule=sched)
         if self.track:
             self.h_a[row].copy_(self._action[:self.track])
             self.h_r[row].copy_(self._reward[:self.track])

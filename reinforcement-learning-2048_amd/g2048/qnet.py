@@ -7,6 +7,7 @@ g2048_mlp.hip), for the two fp32 fast-path nets:
 forward(model, rows, idx)   == model(board_as_*_tensor(rows[idx]))        one launch
 targets(...)                == sampler + Q_online(s') + Q_target(s') + Bellman target, one launch
 TrainGrad(model, B)(...)    == d/dtheta sum_b (Q(s_b)[a_b] - y_b)^2 into a flat bucket, 2 launches
+Dense64Update(...)()        == a whole dense64 train_step (sampler, targets, gradient, Adam), 2 launches
 """
 from __future__ import annotations
 
@@ -120,6 +121,40 @@ class TrainGrad:
 
 
 ConvTrainGrad = TrainGrad
+
+
+class Dense64Update:
+    """One whole Double-DQN update of an fp32 dense 16-64-4 net in two launches
+    (g2048_dense64_update): sampler + both target-side forwards + Bellman + MSE gradient per
+    32-row tile, then the fixed-order gradient reduction with Adam applied in place (adam given)
+    or the summed gradient left in grad_out (adam=None, for a data-parallel all-reduce followed by
+    FusedAdam.step).  step_dev: device u64 update counter (sampler epoch in, +1 out)."""
+
+    def __init__(self, model, target, batch: int, adam=None):
+        if kind_of(model) != "dense64" or kind_of(target) != "dense64":
+            raise TypeError("Dense64Update needs fp32 dense 16-64-4 online and target nets")
+        self.on, self.tg = net_params(model), net_params(target)
+        self.batch = int(batch)
+        self.adam = adam
+        dev = next(model.parameters()).device
+        n = N.load().g2048_dense64_update_workspace(self.batch)
+        self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
+                 idx_in=None, grad_out=None, loss_out=None):
+        if idx_out.numel() != self.batch or y_out.numel() != self.batch:
+            raise ValueError("idx_out / y_out must have `batch` elements")
+        if self.adam is None and grad_out is None:
+            raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        a = self.adam
+        m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
+        lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)
+        N.check(N.load().g2048_dense64_update(
+            C.byref(self.on), C.byref(self.tg), replay.handle, N.ptr(idx_in), self.batch,
+            int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)), N.ptr(idx_out),
+            N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(m),
+            N.ptr(v), float(lr), float(b1), float(b2), float(eps), N.stream_of(y_out.device)),
+            "g2048_dense64_update")
 
 
 def targets(kind: str, online, target, replay, batch: int, idx_out: torch.Tensor,

@@ -417,3 +417,38 @@ def test_epoch_roundtrip(g2048):
     a.reset()
     b.reset()
     np.testing.assert_array_equal(_np(a.board), _np(b.board))
+
+
+@pytest.mark.parametrize("mode", ["scalar", "schedule"])
+def test_fused_dense64_step_matches_forward_plus_step(g2048, mode):
+    """g2048_env_step_egreedy_dense64 (Q computed in the step kernel) == g2048_dense64_forward +
+    g2048_env_step_egreedy, bit for bit: Q, actions, boards, rewards, replay, episode log."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    n = 4096 + 77
+    m = det_init(make_net("dense64", torch.float32, DEV), 0.7)
+    p = qnet.net_params(m)
+    kw = dict(eps_schedule=(30.0, 0.05)) if mode == "schedule" else {}
+    envs, rbs, logs = [], [], []
+    for _ in range(2):
+        e = g2048.VecEnv2048(n, seed=9, device=DEV)
+        rbs.append(g2048.ReplayBuffer(8 * n, device=DEV))
+        logs.append(e.attach_episode_log(16))
+        e.rollout(30)
+        envs.append(e)
+    qf = torch.empty((n, 4), dtype=torch.float32, device=DEV)
+    for t in range(60):
+        a0, r0, d0 = envs[0].step_egreedy_dense64(p, 0.2, replay=rbs[0], q_out=qf, **kw)
+        q = qnet.forward(m, envs[1].board)
+        a1, r1, d1 = envs[1].step_egreedy(q, 0.2, replay=rbs[1], **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(qf, q), t
+        assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
+    for name in ("board", "meta", "ep"):
+        assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
+    for name in ("s", "s2", "a", "r", "d", "count"):
+        assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name
+    g0, g1 = logs[0].read(), logs[1].read()
+    for f in g0:
+        assert torch.equal(g0[f], g1[f]), f

@@ -227,6 +227,62 @@ def test_dense64_train_grad_matches_autograd(G, B):
         off += p.numel()
 
 
+@pytest.mark.parametrize("B,double_dqn,sampled", [(8192, True, True), (1000, False, True),
+                                                   (45, True, False), (20000, True, False)])
+def test_dense64_update_matches_pieces(G, B, double_dqn, sampled):
+    """g2048_dense64_update (sampler + targets + gradient in one launch, Adam in the reduction)
+    against targets -> train_grad -> FusedAdam: identical rows and targets (bitwise), the
+    gradient within fp32 summation-order tolerance (32- vs 64-row slabs), the same update
+    counter; and its grad-only mode + FusedAdam.step is bitwise its Adam-in-reduction mode."""
+    import copy
+
+    from g2048.nets import make_net
+    from g2048.optim import FusedAdam
+    from g2048.qnet import Dense64Update, TrainGrad, net_params, targets
+
+    rb = _filled_ring(G, B % 97)
+    torch.manual_seed(B)
+    on = make_net("dense64", torch.float32, DEV)
+    tg = make_net("dense64", torch.float32, DEV)
+    idx_in = None if sampled else torch.randint(0, rb.capacity, (B,), device=DEV)
+    seed = 0xABCDEF12345
+    nets = [copy.deepcopy(on) for _ in range(3)]
+    steps = [torch.full((1,), 11, dtype=torch.int64, device=DEV) for _ in range(3)]
+    outs = []
+    # (0) pieces: targets -> train_grad (bumps the counter) -> FusedAdam
+    io, y = torch.empty(B, dtype=torch.int64, device=DEV), torch.empty(B, device=DEV)
+    g0, l0 = torch.empty(1348, device=DEV), torch.zeros((), device=DEV)
+    targets("dense64", net_params(nets[0]), net_params(tg), rb, B, io, y, 0.8, double_dqn, seed,
+            steps[0], idx_in)
+    TrainGrad(nets[0], B)(rb.s, rb.a, io, y, g0, l0, steps[0])
+    FusedAdam(list(nets[0].parameters()), lr=1e-2).step(g0, steps[0])
+    outs.append((io, y, g0, l0))
+    # (1) fused update with Adam in the reduction; (2) fused, gradient only, then FusedAdam
+    for k, with_adam in ((1, True), (2, False)):
+        adam = FusedAdam(list(nets[k].parameters()), lr=1e-2)
+        io_k, y_k = torch.empty(B, dtype=torch.int64, device=DEV), torch.empty(B, device=DEV)
+        g_k, l_k = torch.full((1348,), float("nan"), device=DEV), torch.zeros((), device=DEV)
+        Dense64Update(nets[k], tg, B, adam=adam if with_adam else None)(
+            rb, io_k, y_k, steps[k], 0.8, double_dqn, seed, idx_in, grad_out=g_k, loss_out=l_k)
+        if not with_adam:
+            adam.step(g_k, steps[k])
+        outs.append((io_k, y_k, g_k, l_k))
+    torch.cuda.synchronize()
+    for k in (1, 2):
+        assert int(steps[k]) == 12 == int(steps[0])
+        assert torch.equal(outs[k][0], outs[0][0])
+        assert torch.equal(outs[k][1], outs[0][1])
+        torch.testing.assert_close(outs[k][2], outs[0][2], rtol=1e-4,
+                                   atol=1e-5 * float(outs[0][2].abs().max()))
+        assert float(outs[k][3]) == pytest.approx(float(outs[0][3]), rel=1e-5)
+    assert torch.equal(outs[1][2], outs[2][2]) and torch.equal(outs[1][3], outs[2][3])
+    for p1, p2, p0 in zip(nets[1].parameters(), nets[2].parameters(), nets[0].parameters()):
+        assert torch.equal(p1, p2)
+        torch.testing.assert_close(p1, p0, rtol=1e-4, atol=1e-5)  # ~lr*sign(g) first steps
+    if sampled:
+        assert int(outs[1][0].min()) >= 0 and int(outs[1][0].max()) < int(rb.count)
+
+
 @pytest.mark.parametrize("B", [32, 1000, 8192])
 def test_fused_learner_kernels_are_deterministic(G, B):
     """Bitwise-identical results across repeated launches on the same inputs: the conv / dense64
@@ -260,3 +316,21 @@ def test_fused_learner_kernels_are_deterministic(G, B):
         for o in outs[1:]:
             for a, b in zip(o, outs[0]):
                 assert torch.equal(a, b), kind
+    # the fused dense64 update (gradient-only mode, counter reset per launch)
+    m = det_init(make_net("dense64", torch.float32, DEV), 0.4)
+    tgt = det_init(make_net("dense64", torch.float32, DEV), 0.9)
+    upd = qnet.Dense64Update(m, tgt, B)
+    outs = []
+    for _ in range(6):
+        st = torch.tensor([3], dtype=torch.int64, device=DEV)
+        io = torch.empty(B, dtype=torch.int64, device=DEV)
+        yo = torch.empty(B, dtype=torch.float32, device=DEV)
+        grad = torch.full((1348,), float("nan"), device=DEV)
+        loss = torch.zeros((), device=DEV)
+        upd(rb, io, yo, st, seed=7, grad_out=grad, loss_out=loss)
+        outs.append((grad, loss, io, yo, st))
+    torch.cuda.synchronize()
+    assert torch.isfinite(outs[0][0]).all() and int(outs[0][4]) == 4
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert torch.equal(a, b), "dense64 update"

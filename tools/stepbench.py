@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fused eps-greedy step variants at 64k boards (events over a 200-launch graph): scalar eps,
-per-board schedule, schedule + episode log."""
+per-board schedule, schedule + episode log, and the dense 16-64-4 Q computed in the step."""
 import json
 import os
 import sys
@@ -18,14 +18,24 @@ N = 65536
 def run(variant, steps=200):
     env = g2048.VecEnv2048(N, seed=1, device=DEV)
     rb = g2048.ReplayBuffer(16 * N, device=DEV)
-    if variant == "log":
+    if variant in ("log", "dense64"):
         env.attach_episode_log(8)
     q = torch.randn((N, 4), device=DEV)
     kw = dict(eps_schedule=(1000.0, 0.01)) if variant != "scalar" else {}
     outs = (torch.empty(N, dtype=torch.int32, device=DEV), torch.empty(N, dtype=torch.uint8, device=DEV),
             torch.empty(N, dtype=torch.uint8, device=DEV))
-    def step():
-        env.step_egreedy(q, 0.1, replay=rb, reward=outs[0], done=outs[1], action=outs[2], **kw)
+    if variant == "dense64":
+        from g2048 import qnet
+        from g2048.nets import det_init, make_net
+        m = det_init(make_net("dense64", torch.float32, DEV), 0.3)
+        p = qnet.net_params(m)
+
+        def step():
+            env.step_egreedy_dense64(p, 0.1, replay=rb, reward=outs[0], done=outs[1],
+                                     action=outs[2], **kw)
+    else:
+        def step():
+            env.step_egreedy(q, 0.1, replay=rb, reward=outs[0], done=outs[1], action=outs[2], **kw)
     for _ in range(20):
         step()
     torch.cuda.synchronize()
@@ -46,4 +56,4 @@ def run(variant, steps=200):
     return a.elapsed_time(b) * 1e3 / (5 * steps)
 
 
-print(json.dumps({v: round(run(v), 3) for v in ("scalar", "schedule", "log")}))
+print(json.dumps({v: round(run(v), 3) for v in ("scalar", "schedule", "log", "dense64")}))
