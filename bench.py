@@ -233,6 +233,7 @@ def bench_train(args, world, rank, dev, net):
     T.prefill(C // n)  # replay pre-filled by random-policy rollout steps (one launch)
     for _ in range(5):
         T.step()
+    L.update()  # the learner's own graph (the Trainer may run a graphed loop): captured here
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     K = args.train_updates

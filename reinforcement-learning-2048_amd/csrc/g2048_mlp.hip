@@ -20,7 +20,8 @@
 namespace {
 
 constexpr int NT = 256, H = 64;
-constexpr int XS = 17, W1S = 17, HS = 65, W2S = 65;
+// rows of x / h / W2 are float4-aligned (b128 LDS reads); W1 rows odd-strided (b32, per-lane j)
+constexpr int XS = 20, W1S = 17, HS = 68, W2S = 68;
 constexpr int S_FWD = 64;  // boards per tile: forward / targets / train_grad launches
 constexpr int S_UPD = 32;  // the fused update (batch 8192 -> 256 tiles = one per CU)
 // torch order: 0.weight [64][16], 0.bias [64], 2.weight [4][64], 2.bias [4]
@@ -32,7 +33,7 @@ struct MlpW {
     const float *w1, *b1, *w2, *b2;
 };
 
-struct LW {  // one net's weights in LDS
+struct alignas(16) LW {  // one net's weights in LDS
     float w1[H * W1S];
     float b1[H];
     float w2[4 * W2S];
@@ -40,7 +41,7 @@ struct LW {  // one net's weights in LDS
 };
 
 template <int S>
-struct Tile {  // one tile of S boards
+struct alignas(16) Tile {  // one tile of S boards
     float x[S * XS];
     float h[S * HS];
     float q[S * 4];
@@ -59,6 +60,12 @@ __device__ __forceinline__ void stage_weights(const MlpW& W, LW& L) {
     if (t < 4) L.b2[t] = W.b2[t];
 }
 
+// one u32 board word (4 exponents) -> 4 floats of an x row
+__device__ __forceinline__ void put_word(float* dst, uint32_t v) {
+    *reinterpret_cast<float4*>(dst) = make_float4((float)(v & 0xFFu), (float)((v >> 8) & 0xFFu),
+                                                  (float)((v >> 16) & 0xFFu), (float)(v >> 24));
+}
+
 template <int S>
 __device__ __forceinline__ void stage_boards(Tile<S>& T, const uint8_t* rows, const int64_t* idx,
                                              int64_t b0, int64_t n) {
@@ -68,11 +75,7 @@ __device__ __forceinline__ void stage_boards(Tile<S>& T, const uint8_t* rows, co
     const int64_t b = b0 + s;
     uint32_t v = 0;
     if (b < n) v = reinterpret_cast<const uint32_t*>(rows)[(idx ? idx[b] : b) * 4 + w];
-    float* dst = T.x + s * XS + w * 4;
-    dst[0] = (float)(v & 0xFFu);
-    dst[1] = (float)((v >> 8) & 0xFFu);
-    dst[2] = (float)((v >> 16) & 0xFFu);
-    dst[3] = (float)(v >> 24);
+    put_word(T.x + s * XS + w * 4, v);
 }
 
 // weights + boards staged (caller syncs); leaves h (post-ReLU) and q in LDS, ends with a sync
@@ -92,20 +95,32 @@ __device__ __forceinline__ void forward_tile(Tile<S>& T, const LW& W) {
 #pragma unroll 4
         for (int ss = 0; ss < SPT; ++ss) {
             const int s = s0 + ss;
+            const float4* xr = reinterpret_cast<const float4*>(T.x + s * XS);  // broadcast
             float p[4] = {bb, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) p[i & 3] = fmaf(w[i], T.x[s * XS + i], p[i & 3]);
+            for (int u = 0; u < 4; ++u) {
+                const float4 xv = xr[u];
+                p[0] = fmaf(w[4 * u + 0], xv.x, p[0]);
+                p[1] = fmaf(w[4 * u + 1], xv.y, p[1]);
+                p[2] = fmaf(w[4 * u + 2], xv.z, p[2]);
+                p[3] = fmaf(w[4 * u + 3], xv.w, p[3]);
+            }
             T.h[s * HS + j] = fmaxf((p[0] + p[1]) + (p[2] + p[3]), 0.f);
         }
     }
     __syncthreads();
     if (t < 4 * S) {
         const int s = t >> 2, a = t & 3;
+        const float4* hr = reinterpret_cast<const float4*>(T.h + s * HS);
+        const float4* wr = reinterpret_cast<const float4*>(W.w2 + a * W2S);
         float e = W.b2[a], o = 0.f;  // even / odd j, same order as k_step_dense64
-#pragma unroll 16
-        for (int j = 0; j < H; j += 2) {
-            e = fmaf(W.w2[a * W2S + j], T.h[s * HS + j], e);
-            o = fmaf(W.w2[a * W2S + j + 1], T.h[s * HS + j + 1], o);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const float4 hv = hr[u], wv = wr[u];
+            e = fmaf(wv.x, hv.x, e);
+            o = fmaf(wv.y, hv.y, o);
+            e = fmaf(wv.z, hv.z, e);
+            o = fmaf(wv.w, hv.w, o);
         }
         T.q[t] = e + o;
     }
@@ -186,8 +201,11 @@ __device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, GradAcc& G) {
 #pragma unroll 8
         for (int s = 0; s < S; ++s) {
             const float dh = T.h[s * HS + j];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) G.w1[u] = fmaf(dh, T.x[s * XS + i0 + u], G.w1[u]);
+            const float4 xv = *reinterpret_cast<const float4*>(T.x + s * XS + i0);
+            G.w1[0] = fmaf(dh, xv.x, G.w1[0]);
+            G.w1[1] = fmaf(dh, xv.y, G.w1[1]);
+            G.w1[2] = fmaf(dh, xv.z, G.w1[2]);
+            G.w1[3] = fmaf(dh, xv.w, G.w1[3]);
         }
         if (t < H) {
             float v = 0.f;
@@ -346,14 +364,24 @@ struct UpdateArgs {
     float* y_out;
     float* slab;
     unsigned long long* step_next;
+#ifdef G2048_MLP_PHASE
+    long long* phase;
+#endif
 };
+
+#ifdef G2048_MLP_PHASE
+#define MPHASE(k) \
+    if (threadIdx.x == 0) A.phase[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime()
+#else
+#define MPHASE(k)
+#endif
 
 __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
     constexpr int S = S_UPD;
+    MPHASE(0);
     __shared__ LW Won, Wtg;
     __shared__ Tile<S> T;
     __shared__ float qtg[S * 4];
-    __shared__ int64_t sidx[S];
     const int t = threadIdx.x;
     const unsigned long long ep = A.idx_in ? 0ull : *A.step;
     const unsigned long long count = A.idx_in ? 0ull : *A.count;
@@ -362,47 +390,69 @@ __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
     stage_weights(A.tg, Wtg);
     GradAcc G;
     const int64_t ntiles = (A.batch + S - 1) / S;
+    const int sl = t >> 2, w = t & 3;  // threads t < 4S: board sl of the tile, word w
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * S;
+        // every thread of a board draws its row itself and fetches its s' and s words in the
+        // same round trip as a / r / d (no LDS hand-off of the indices)
+        const int64_t b = b0 + sl;
+        const bool ok = t < 4 * S && b < A.batch;
+        uint32_t s2w = 0, sw = 0;
         int32_t rj = 0;
-        uint8_t dj = 0;
-        __syncthreads();
-        if (t < S) {
-            const int64_t b = b0 + t;
-            const bool ok = b < A.batch;
-            int64_t j = 0;
-            if (ok) {
-                j = A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+        uint8_t dj = 0, aj = 0;
+        if (ok) {
+            const int64_t j =
+                A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+            s2w = reinterpret_cast<const uint32_t*>(A.s2)[j * 4 + w];
+            sw = reinterpret_cast<const uint32_t*>(A.s)[j * 4 + w];
+            if (w == 0) {
                 A.idx_out[b] = j;
                 rj = A.r[j];
                 dj = A.d[j];
+                aj = A.a[j];
             }
-            sidx[t] = j;
-            T.a[t] = ok ? (float)A.a[j] : 0.f;
-            T.g[t] = ok ? 1.f : 0.f;
+        }
+        __syncthreads();  // the previous tile's grad_tile is done with T
+        MPHASE(1);
+        if (t < 4 * S) {
+            put_word(T.x + sl * XS + w * 4, s2w);
+            if (w == 0) {
+                T.a[sl] = (float)aj;
+                T.g[sl] = ok ? 1.f : 0.f;
+            }
         }
         __syncthreads();
-        stage_boards<S>(T, A.s2, sidx, 0, S);
-        __syncthreads();
+        MPHASE(2);
         forward_tile<S>(T, Wtg);
         if (t < 4 * S) qtg[t] = T.q[t];
         forward_tile<S>(T, Won);
-        if (t < S) {
-            const float y = bellman(T.q + t * 4, qtg + t * 4, rj, dj, A.gamma, A.double_dqn);
-            T.y[t] = y;
-            if (b0 + t < A.batch) A.y_out[b0 + t] = y;
+        if (t < 4 * S && w == 0) {
+            const float y = bellman(T.q + sl * 4, qtg + sl * 4, rj, dj, A.gamma, A.double_dqn);
+            T.y[sl] = y;
+            if (ok) A.y_out[b] = y;
         }
         __syncthreads();  // T.x is restaged below; T.y visible to grad_tile
-        stage_boards<S>(T, A.s, sidx, 0, S);
+        MPHASE(3);
+        if (t < 4 * S) put_word(T.x + sl * XS + w * 4, sw);
         __syncthreads();
+        MPHASE(4);
         grad_tile<S>(T, Won, G);
+#ifdef G2048_MLP_PHASE
+        __syncthreads();
+#endif
+        MPHASE(5);
     }
     write_slab<S>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
+    MPHASE(6);
 }
 
-// block = 64 slab positions x 4 waves (wave w sums slabs w, w+4, ...), fixed-order combine.
-// With `adam`, the summed gradient of each parameter is applied right here (torch Adam, t read
-// from *step_next) and *step_next is committed to *step.
+// block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... (<= 16 loads, all in
+// flight at once), then a fixed-order combine of the 16 partials.  With `adam`, the summed
+// gradient of each parameter is applied right here (torch Adam, t read from *step_next) and
+// *step_next is committed to *step.
+constexpr int RW = 16;  // waves per reduction block
+static_assert(MAX_SLABS <= RW * 16, "reduction covers at most RW*16 slabs");
+
 struct ReduceArgs {
     const float* slab;
     int nslab;
@@ -417,26 +467,25 @@ struct ReduceArgs {
     int adam;
 };
 
-__global__ __launch_bounds__(256) void k_mlp_reduce(ReduceArgs A) {
-    __shared__ float part[4][64];
+__global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
+    __shared__ float part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
-    float v = 0.f;
-    if (pos <= P_N) {
-        int g = wave;
-        for (; g + 28 < A.nslab; g += 32) {
-            float r[8];
+    float r[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) r[u] = A.slab[(int64_t)(g + 4 * u) * SLAB + pos];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v += r[u];
-        }
-        for (; g < A.nslab; g += 4) v += A.slab[(int64_t)g * SLAB + pos];
+    for (int u = 0; u < 16; ++u) {
+        const int g = wave + RW * u;
+        r[u] = (pos <= P_N && g < A.nslab) ? A.slab[(int64_t)g * SLAB + pos] : 0.f;
     }
+    float v = r[0];
+#pragma unroll
+    for (int u = 1; u < 16; ++u) v += r[u];
     part[wave][lane] = v;
     __syncthreads();
     if (wave == 0 && pos <= P_N) {
-        const float sum = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        float sum = part[0][lane];
+#pragma unroll
+        for (int k = 1; k < RW; ++k) sum += part[k][lane];
         if (pos == P_N) {
             if (A.loss) *A.loss = sum;
         } else {
@@ -454,6 +503,9 @@ __global__ __launch_bounds__(256) void k_mlp_reduce(ReduceArgs A) {
     if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
 }
 
+}  // namespace
+
+namespace {
 inline MlpW mlp_w(const g2048_dense64_params* p) { return MlpW{p->w1, p->b1, p->w2, p->b2}; }
 inline bool ok_params(const g2048_dense64_params* p) {
     return p && p->w1 && p->b1 && p->w2 && p->b2;
@@ -536,13 +588,16 @@ extern "C" G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* p,
     R.nslab = grid;
     R.grad = grad_out;
     R.loss = loss_out;
-    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(256), 0, st, R);
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(64 * RW), 0, st, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
 }
 
 extern "C" G2048_API int64_t g2048_dense64_update_workspace(int64_t batch) {
     const int64_t ntiles = (batch + S_UPD - 1) / S_UPD;
+#ifdef G2048_MLP_PHASE
+    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + 2 + 2 * 8 * MAX_SLABS;
+#endif
     return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + 2;  // + the u64 step_next word
 }
 
@@ -589,6 +644,9 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
     U.y_out = y_out;
     U.slab = workspace;
     U.step_next = step_next;
+#ifdef G2048_MLP_PHASE
+    U.phase = reinterpret_cast<long long*>(step_next + 1);
+#endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_mlp_update, dim3(grid), dim3(NT), 0, st, U);
     hipError_t e = hipGetLastError();
@@ -611,7 +669,7 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
     R.b1 = beta1;
     R.b2 = beta2;
     R.eps = eps;
-    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(256), 0, st, R);
+    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(64 * RW), 0, st, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
 }

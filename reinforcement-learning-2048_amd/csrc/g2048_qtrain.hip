@@ -488,31 +488,31 @@ __device__ __forceinline__ int slab_to_param(int pos) {
     return P_BF2 + p3 - 704;
 }
 
-// Deterministic slab reduction: a block owns 64 slab positions; its 4 waves sum the slabs
-// g = wave, wave + 4, ... (8 independent loads in flight per lane), then the 4 partials are
-// added in a fixed order.  524 blocks keep enough loads in flight to stream the ~34 MB.
-__global__ __launch_bounds__(256) void k_reduce_slabs(const float* slab, int nslab, float* grad,
-                                                      float* loss) {
-    __shared__ float part[4][64];
+// Deterministic slab reduction: a block owns 64 slab positions; its 16 waves sum the slabs
+// g = wave, wave + 16, ... (<= 16 independent loads per lane, all issued at once: one memory
+// round trip for the ~34 MB instead of 8), then the 16 partials are added in a fixed order.
+constexpr int RW = 16;  // waves per reduction block
+
+__global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int nslab,
+                                                          float* grad, float* loss) {
+    __shared__ float part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
-    float v = 0.f;
-    if (pos <= SL_LOSS) {
-        const float* p = slab + pos;
-        int g = wave;
-        for (; g + 28 < nslab; g += 32) {
-            float r[8];
+    float r[16];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) r[u] = p[(int64_t)(g + 4 * u) * SLAB];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v += r[u];
-        }
-        for (; g < nslab; g += 4) v += p[(int64_t)g * SLAB];
+    for (int u = 0; u < 16; ++u) {
+        const int g = wave + RW * u;
+        r[u] = (pos <= SL_LOSS && g < nslab) ? slab[(int64_t)g * SLAB + pos] : 0.f;
     }
+    float v = r[0];
+#pragma unroll
+    for (int u = 1; u < 16; ++u) v += r[u];
     part[wave][lane] = v;
     __syncthreads();
     if (wave == 0 && pos <= SL_LOSS) {
-        const float s = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+        float s = part[0][lane];
+#pragma unroll
+        for (int k = 1; k < RW; ++k) s += part[k][lane];
         if (pos == SL_LOSS) {
             if (loss) *loss = s;
         } else {
@@ -559,8 +559,8 @@ extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
     hipLaunchKernelGGL(k_conv_train, dim3(grid), dim3(NT), 0, st, A);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(256), 0, st, workspace,
-                       grid, grad_out, loss_out);
+    hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, st,
+                       workspace, grid, grad_out, loss_out);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "k_reduce_slabs: %s", hipGetErrorString(e));

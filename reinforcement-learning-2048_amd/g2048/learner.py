@@ -279,8 +279,15 @@ class Trainer:
                  updates_per_step: int = 1, min_fill: int | None = None,
                  eps_decay_episodes: float = 1000.0, min_epsilon: float = 0.01,
                  episode_log_slots: int = 8, track_boards: int = 0,
-                 history_len: int = 4096):
+                 history_len: int = 4096, graph: bool | None = None):
         self.env, self.replay, self.learner = env, replay, learner
+        # graph: replay one captured hipGraph per iteration (fused step + updates) once the
+        # learner is updating; default on for the fused fp32 learners on one process
+        self.graph = (learner.fused and learner.graph and learner.world == 1) if graph is None \
+            else bool(graph)
+        if self.graph and not (learner.fused and learner.world == 1):
+            raise ValueError("the graphed loop needs a fused learner on one process")
+        self._loop_graph = None
         self.updates_per_step = int(updates_per_step)
         self.min_fill = int(min_fill if min_fill is not None else learner.B)
         self.eps_decay = float(eps_decay_episodes)
@@ -310,10 +317,8 @@ class Trainer:
         self.env.rollout(steps, replay=self.replay)
         self.steps += steps
 
-    def step(self) -> None:
-        if self.track:
-            row = self.steps % self.history_len
-            self.h_s[row].copy_(self.env.board[:self.track])
+    def _rollout_step(self) -> None:
+        """Device work of play_one_step for all boards (stream-ordered, capturable)."""
         sched = (self.eps_decay, self.min_eps)
         if self.learner.kind == "dense64":  # Q computed inside the step kernel (one launch)
             self.env.step_egreedy_dense64(self.learner._p_on, replay=self.replay,
@@ -323,12 +328,48 @@ class Trainer:
             q = self.learner.q_values(self.env)
             self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward,
                                   done=self._done, action=self._action, eps_schedule=sched)
+
+    def _graphed_iteration(self) -> None:
+        """One iteration as hipGraph replays: [step + first update], then [update] for each
+        further update, with the target sync checked between updates exactly as in
+        DQNLearner.update.  Capture records without executing, and every kernel of the fused
+        path reads its varying state (boards, ring position, update counter) from device memory,
+        so replay k equals eager iteration k bit for bit."""
+        L = self.learner
+        if self._loop_graph is None:
+            g1, g2 = torch.cuda.CUDAGraph(), None
+            with torch.cuda.graph(g1):
+                self._rollout_step()
+                L._compute_grads()
+                L._apply()
+            if self.updates_per_step > 1:
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2):
+                    L._compute_grads()
+                    L._apply()
+            self._loop_graph = (g1, g2)
+        g1, g2 = self._loop_graph
+        for u in range(self.updates_per_step):
+            (g1 if u == 0 else g2).replay()
+            L.updates += 1
+            if L.target_sync_every and L.updates % L.target_sync_every == 0:
+                dqn_lib.sync_target(L.model, L.target)
+
+    def step(self) -> None:
+        if self.track:
+            row = self.steps % self.history_len
+            self.h_s[row].copy_(self.env.board[:self.track])
+        updating = (self.steps + 1) * self.env.n >= self.min_fill
+        if self.graph and updating and self.updates_per_step > 0:
+            self._graphed_iteration()
+        else:
+            self._rollout_step()
         if self.track:
             self.h_a[row].copy_(self._action[:self.track])
             self.h_r[row].copy_(self._reward[:self.track])
             self.h_d[row].copy_(self._done[:self.track])
         self.steps += 1
-        if self.steps * self.env.n >= self.min_fill:
+        if not self.graph and self.steps * self.env.n >= self.min_fill:
             for _ in range(self.updates_per_step):
                 self.learner.update()
 
@@ -425,6 +466,7 @@ class Trainer:
 
     @torch.no_grad()
     def load_state_dict(self, st: dict) -> None:
+        self._loop_graph = None  # host-side env state (the reset epoch) is baked into a capture
         env, rb = self.env, self.replay
         e = st["env"]
         for k in ("n", "seed", "board_offset", "flags"):

@@ -30,7 +30,8 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
                   no_episodes_to_reach_epsilon: float = 1000.0, min_epsilon: float = 0.01,
                   updates_per_step: int = 1, min_fill: int | None = None, seed: int = 0,
                   device="cuda:0", track_boards: int = 1, episode_log_slots: int = 8,
-                  graph: bool = True, board_offset: int = 0, process_group=None) -> Trainer:
+                  graph: bool = True, board_offset: int = 0, process_group=None,
+                  loop_graph: bool | None = None) -> Trainer:
     cap = max(n_boards, (replay_buffer_length // n_boards) * n_boards)  # multiple of n
     env = VecEnv2048(n_boards, seed=0x2048 + seed, device=device, board_offset=board_offset)
     replay = ReplayBuffer(cap, device=device)
@@ -40,7 +41,8 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
                          graph=graph, seed=seed, process_group=process_group)
     return Trainer(env, replay, learner, updates_per_step=updates_per_step, min_fill=min_fill,
                    eps_decay_episodes=no_episodes_to_reach_epsilon, min_epsilon=min_epsilon,
-                   episode_log_slots=episode_log_slots, track_boards=track_boards)
+                   episode_log_slots=episode_log_slots, track_boards=track_boards,
+                   graph=loop_graph)
 
 
 def hyperparameters(trainer: Trainer, no_episodes: int, snapshot_game_every_n_episodes: int):

@@ -133,3 +133,29 @@ def test_training_loop_artefacts(G, tmp_path):
                          min_epsilon=0.05, device=DEV, track_boards=2)
     assert tr2.steps == tr.steps and len(exp2.episodes) == len(eps)
     assert torch.equal(tr2.env.board.cpu(), tr.env.board.cpu())
+
+
+@pytest.mark.parametrize("net", ["conv", "dense64"])
+def test_graphed_loop_equals_eager(G, net):
+    """Trainer(graph=True) replays one captured hipGraph per iteration (step + updates); the
+    trajectory must be bitwise the eager one: boards, episode counters, ring, episode log,
+    tracked-board histories, online and target weights, loss.  Covers the steps before
+    min_fill (no update), 2 updates per step and target syncs between replays."""
+    outs = []
+    for graph in (True, False):
+        tr = _small(G, net, min_fill=3 * 1024, target_sync_every=3, track_boards=3,
+                    updates_per_step=2, loop_graph=graph)
+        assert tr.graph is graph
+        for _ in range(11):
+            tr.step()
+        f = _fingerprint(tr)
+        f["h_s"], f["h_a"] = tr.h_s.cpu().clone(), tr.h_a.cpu().clone()
+        outs.append((f, tr.learner.updates))
+    (a, ua), (b, ub) = outs
+    assert ua == ub == 2 * 9
+    for k in a:
+        if k in ("params", "target"):
+            for x, y in zip(a[k], b[k]):
+                assert torch.equal(x, y), k
+        else:
+            assert torch.equal(a[k], b[k]), k
