@@ -86,11 +86,15 @@ __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v
 
 // One transition of board i (global id gid).  Mirrors o2048_env_step (oracle/oracle2048.c),
 // which restates src/dqn_lib.py:91-107 + src/board.py.
-template <int MODE>
+// kPre: the caller loaded ep (and qs, when a q-sum buffer is attached) together with the board.
+// Otherwise they are loaded here on done only -- 16 B less traffic per board, at the price of a
+// dependent memory round trip for every wave that holds a terminal board.
+template <int MODE, bool kPre = true>
 __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, Board& b,
                                          uint4& m, double eps, double& qs, int32_t& rew_out,
                                          uint32_t& done_out, uint32_t& legal_out,
-                                         uint32_t& act_out, float4 qreg = float4{0, 0, 0, 0}) {
+                                         uint32_t& act_out, uint4& ep,
+                                         float4 qreg = float4{0, 0, 0, 0}) {
     const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
     const uint4 u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
     const uint32_t legal = legal_mask(b);
@@ -154,15 +158,18 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG;
     uint32_t ep_idx = 0u, mx = 0u, fin_score = 0u, fin_moves = 0u;
     if (done) {
-        const uint4 e0 = A.ep[i];
+        if constexpr (!kPre) {
+            ep = A.ep[i];
+            if constexpr (!kGreedy) {  // non-greedy steps add 0 to the sum: read it on done
+                if (A.qsum) qs = A.qsum[i];
+            }
+        }
         mx = max_exp(b);
-        A.ep[i] = make_uint4(e0.x + 1u, m.x, m.y, mx);
-        ep_idx = e0.x;
+        ep_idx = ep.x;
+        ep = make_uint4(ep.x + 1u, m.x, m.y, mx);
+        A.ep[i] = ep;
         fin_score = m.x;
         fin_moves = m.y;
-        if constexpr (!kGreedy) {  // non-greedy steps add 0 to the sum: touch it on done only
-            if (A.qsum) qs = A.qsum[i];
-        }
         if (!(A.flags & G2048_NO_AUTORESET)) {
             b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m.x = 0u;
@@ -205,16 +212,17 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
 
 // kFull: every block is full (n % kBlock == 0), so there is no bounds test and every kernel
 // argument load can be issued at once (with the test, the pointer loads wait for n's round trip).
-template <int MODE, bool kFull>
+template <int MODE, bool kFull, bool kPre>
 __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (!kFull && i >= A.n) return;
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
+    uint4 ep = kPre ? A.ep[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
         if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board: ep = its episode count
-            const double e = (double)reinterpret_cast<const uint32_t*>(A.ep)[4 * i];
+            const double e = (double)(kPre ? ep.x : reinterpret_cast<const uint32_t*>(A.ep)[4 * i]);
             eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
         } else {
             eps = A.eps_dev ? *A.eps_dev : A.eps;
@@ -223,8 +231,9 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     int32_t rew;
     uint32_t done, legal, act;
     constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
-    double qs = (kGreedy && A.qsum) ? A.qsum[i] : 0.0;  // other modes: step_one, on done only
-    step_one<MODE>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act);
+    double qs = ((kPre || kGreedy) && A.qsum) ? A.qsum[i] : 0.0;
+    step_one<MODE, kPre>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act,
+                         ep);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
     if (kGreedy && A.qsum) A.qsum[i] = qs;
@@ -253,9 +262,10 @@ __global__ __launch_bounds__(kBlock) void k_step_dense64(StepArgs A, const float
     if (!kFull && i >= A.n) return;
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
+    uint4 ep = A.ep[i];
     double eps;
     if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board
-        const double e = (double)reinterpret_cast<const uint32_t*>(A.ep)[4 * i];
+        const double e = (double)ep.x;
         eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
     } else {
         eps = A.eps_dev ? *A.eps_dev : A.eps;
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_step_dense64(StepArgs A, const float
     uint32_t done, legal, act;
     double qs = A.qsum ? A.qsum[i] : 0.0;
     step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act,
-                          q);
+                          ep, q);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
     if (A.qsum) A.qsum[i] = qs;
@@ -321,13 +331,14 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     if (i >= A.n) return;
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
+    uint4 ep = A.ep[i];  // kept in registers across the K steps
     const uint64_t gid = A.board_offset + (uint64_t)i;
     long long rsum = 0;
-    double qs = 0.0;  // random policy: the running sum is read / cleared on done only
+    double qs = A.qsum ? A.qsum[i] : 0.0;  // random policy: written back (0) on done only
     for (int s = 0; s < A.k_steps; ++s) {
         int32_t rew;
         uint32_t done, legal, act;
-        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, qs, rew, done, legal, act);
+        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, qs, rew, done, legal, act, ep);
         rsum += rew;
     }
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
@@ -546,15 +557,28 @@ int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
     return G2048_OK;
 }
 
+// Prefetch the episode counters with the board (k_step's kPre) when the extra 16 B are nearly
+// free: the eps schedule reads the same 32 B sector anyway, a q-sum buffer is attached, or the
+// batch is small enough to be latency-bound (measured: 64k boards -1 %; 4M boards, HBM-bound,
+// +17 % per step with the prefetch).
+constexpr int64_t kPrefetchMaxBoards = 1 << 18;
+
+template <int MODE, bool kPre>
+void launch_step_k(g2048_env* e, const StepArgs& A, hipStream_t st) {
+    if (e->n % kBlock == 0)
+        hipLaunchKernelGGL((k_step<MODE, true, kPre>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+    else
+        hipLaunchKernelGGL((k_step<MODE, false, kPre>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+}
+
 template <int MODE>
 int launch_step(g2048_env* e, const StepArgs& A, void* stream) {
     DeviceGuard g(e->device);
-    if (e->n % kBlock == 0)
-        hipLaunchKernelGGL((k_step<MODE, true>), dim3(grid_for(e->n)), dim3(kBlock), 0,
-                           reinterpret_cast<hipStream_t>(stream), A);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (A.eps_decay > 0.0 || A.qsum || e->n <= kPrefetchMaxBoards)
+        launch_step_k<MODE, true>(e, A, st);
     else
-        hipLaunchKernelGGL((k_step<MODE, false>), dim3(grid_for(e->n)), dim3(kBlock), 0,
-                           reinterpret_cast<hipStream_t>(stream), A);
+        launch_step_k<MODE, false>(e, A, st);
     G_HIP(hipGetLastError());
     return G2048_OK;
 }
