@@ -232,6 +232,15 @@ G2048_API int g2048_adam_step(float* const* params_dev, const int64_t* numels, i
                               const float* grad_dev, float* exp_avg_dev, float* exp_avg_sq_dev,
                               const uint64_t* step_dev, double lr, double beta1, double beta2,
                               double eps, void* stream);
+/* The same, plus the target-network sync of training_loop (src/dqn_lib.py:227-228) decided on
+ * the device: when t % sync_every == 0, each updated parameter is also written to
+ * target_params (same tensor shapes/order), so graph replays need no host decision. */
+G2048_API int g2048_adam_step_sync(float* const* params_dev, const int64_t* numels, int n_tensors,
+                                   const float* grad_dev, float* exp_avg_dev,
+                                   float* exp_avg_sq_dev, const uint64_t* step_dev, double lr,
+                                   double beta1, double beta2, double eps,
+                                   float* const* target_params_dev, uint64_t sync_every,
+                                   void* stream);
 
 /* ---- dense 16 -> 64 -> 4 Q-net (BASELINE configs[2]): the same four entry points ---------- */
 typedef struct {
@@ -276,7 +285,9 @@ G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* params,
  * ONLINE parameters in place.  *step_dev is incremented once.  grad_out (f32[1348], nullable with
  * Adam) receives the summed gradient -- for a data-parallel all-reduce, pass NULL Adam state here
  * and call g2048_adam_step afterwards.  idx_out / y_out receive the rows and targets; loss_out the
- * loss (nullable).  workspace: f32[g2048_dense64_update_workspace(batch)]. */
+ * loss (nullable).  With Adam and sync_every > 0, the updated parameters are also written to the
+ * TARGET net when t % sync_every == 0 (the target sync of training_loop, decided on the device).
+ * workspace: f32[g2048_dense64_update_workspace(batch)]. */
 G2048_API int64_t g2048_dense64_update_workspace(int64_t batch);
 G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
                                    const g2048_dense64_params* target, g2048_replay* rb,
@@ -285,7 +296,7 @@ G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
                                    int64_t* idx_out_dev, float* y_out_dev, float* workspace_dev,
                                    float* grad_out_dev, float* loss_out_dev, float* exp_avg_dev,
                                    float* exp_avg_sq_dev, double lr, double beta1, double beta2,
-                                   double eps, void* stream);
+                                   double eps, uint64_t sync_every, void* stream);
 
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);

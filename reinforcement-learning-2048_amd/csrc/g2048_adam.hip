@@ -20,6 +20,8 @@ constexpr int kMaxTensors = 16;
 
 struct AdamArgs {
     float* p[kMaxTensors];
+    float* tp[kMaxTensors];  // target-net copies (nullable): written when t % sync_every == 0
+    unsigned long long sync_every;
     int64_t off[kMaxTensors + 1];
     int nt;
     const float* g;
@@ -36,27 +38,37 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
 #pragma unroll
     for (int j = 1; j < kMaxTensors; ++j) k += (j < A.nt && i >= A.off[j]) ? 1 : 0;
     float* p = A.p[k] + (i - A.off[k]);
-    const g2048::AdamCoef c = g2048::adam_coef((double)*A.step, A.lr, A.b1, A.b2, A.eps);
-    *p = g2048::adam_apply(c, A.g[i], A.m + i, A.v + i, *p);
+    const unsigned long long t = *A.step;
+    const g2048::AdamCoef c = g2048::adam_coef((double)t, A.lr, A.b1, A.b2, A.eps);
+    const float np = g2048::adam_apply(c, A.g[i], A.m + i, A.v + i, *p);
+    *p = np;
+    // target sync (src/dqn_lib.py:227-228 load_state_dict after the update) on the device
+    // counter, so an update that syncs needs no host decision between graph replays
+    if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][i - A.off[k]] = np;
 }
 
 }  // namespace
 
-extern "C" G2048_API int g2048_adam_step(float* const* params, const int64_t* numels,
-                                         int n_tensors, const float* grad, float* exp_avg,
-                                         float* exp_avg_sq, const uint64_t* step_dev, double lr,
-                                         double beta1, double beta2, double eps, void* stream) {
+static int adam_launch(float* const* params, const int64_t* numels, int n_tensors,
+                       const float* grad, float* exp_avg, float* exp_avg_sq,
+                       const uint64_t* step_dev, double lr, double beta1, double beta2,
+                       double eps, float* const* target_params, uint64_t sync_every,
+                       void* stream) {
     if (!params || !numels || n_tensors <= 0 || n_tensors > kMaxTensors || !grad || !exp_avg ||
         !exp_avg_sq || !step_dev)
         return g2048_fail(G2048_EINVAL, "adam_step: bad arguments (n_tensors <= %d)", kMaxTensors);
+    if (sync_every && !target_params)
+        return g2048_fail(G2048_EINVAL, "adam_step: sync_every > 0 needs target_params");
     AdamArgs A;
     A.nt = n_tensors;
     A.off[0] = 0;
     for (int j = 0; j < kMaxTensors; ++j) {
         A.p[j] = j < n_tensors ? params[j] : nullptr;
+        A.tp[j] = (sync_every && j < n_tensors) ? target_params[j] : nullptr;
         if (j < n_tensors) A.off[j + 1] = A.off[j] + numels[j];
     }
     for (int j = n_tensors + 1; j <= kMaxTensors; ++j) A.off[j] = A.off[n_tensors];
+    A.sync_every = sync_every;
     A.g = grad;
     A.m = exp_avg;
     A.v = exp_avg_sq;
@@ -70,4 +82,22 @@ extern "C" G2048_API int g2048_adam_step(float* const* params, const int64_t* nu
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "adam_step: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int g2048_adam_step(float* const* params, const int64_t* numels,
+                                         int n_tensors, const float* grad, float* exp_avg,
+                                         float* exp_avg_sq, const uint64_t* step_dev, double lr,
+                                         double beta1, double beta2, double eps, void* stream) {
+    return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
+                       beta2, eps, nullptr, 0, stream);
+}
+
+extern "C" G2048_API int g2048_adam_step_sync(float* const* params, const int64_t* numels,
+                                              int n_tensors, const float* grad, float* exp_avg,
+                                              float* exp_avg_sq, const uint64_t* step_dev,
+                                              double lr, double beta1, double beta2, double eps,
+                                              float* const* target_params, uint64_t sync_every,
+                                              void* stream) {
+    return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
+                       beta2, eps, target_params, sync_every, stream);
 }

@@ -460,7 +460,9 @@ struct ReduceArgs {
     float* loss;
     const unsigned long long* step_next;
     unsigned long long* step;
-    float* p[4];  // w1, b1, w2, b2 (updated in place when adam)
+    float* p[4];   // w1, b1, w2, b2 (updated in place when adam)
+    float* tp[4];  // target net: receives the new params when t % sync_every == 0
+    unsigned long long sync_every;
     float* m;
     float* v;
     double lr, b1, b2, eps;
@@ -494,9 +496,11 @@ __global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
                 const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
                 const int base[4] = {P_W1, P_B1, P_W2, P_B2};
                 float* p = A.p[k] + (pos - base[k]);
-                const g2048::AdamCoef c =
-                    g2048::adam_coef((double)*A.step_next, A.lr, A.b1, A.b2, A.eps);
-                *p = g2048::adam_apply(c, sum, A.m + pos, A.v + pos, *p);
+                const unsigned long long t = *A.step_next;
+                const g2048::AdamCoef c = g2048::adam_coef((double)t, A.lr, A.b1, A.b2, A.eps);
+                const float np = g2048::adam_apply(c, sum, A.m + pos, A.v + pos, *p);
+                *p = np;
+                if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
             }
         }
     }
@@ -609,7 +613,7 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
                                               float* y_out, float* workspace, float* grad_out,
                                               float* loss_out, float* exp_avg, float* exp_avg_sq,
                                               double lr, double beta1, double beta2, double eps,
-                                              void* stream) {
+                                              uint64_t sync_every, void* stream) {
     if (!ok_params(online) || !ok_params(target) || !rb || batch <= 0 || !step_dev || !idx_out ||
         !y_out || !workspace)
         return g2048_fail(G2048_EINVAL, "dense64_update: NULL argument or batch <= 0");
@@ -663,6 +667,11 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
     R.p[1] = const_cast<float*>(online->b1);
     R.p[2] = const_cast<float*>(online->w2);
     R.p[3] = const_cast<float*>(online->b2);
+    R.sync_every = exp_avg ? sync_every : 0;
+    R.tp[0] = const_cast<float*>(target->w1);
+    R.tp[1] = const_cast<float*>(target->b1);
+    R.tp[2] = const_cast<float*>(target->w2);
+    R.tp[3] = const_cast<float*>(target->b2);
     R.m = exp_avg;
     R.v = exp_avg_sq;
     R.lr = lr;

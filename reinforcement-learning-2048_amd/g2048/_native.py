@@ -54,6 +54,8 @@ SIGNATURES = {
     "g2048_convnet_targets": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
                                      _vp, _vp]),
     "g2048_adam_step": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+    "g2048_adam_step_sync": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
+                                    _vp, _u64, _vp]),
     "g2048_dense64_forward": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "g2048_dense64_targets": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
                                      _vp, _vp]),
@@ -61,7 +63,7 @@ SIGNATURES = {
     "g2048_dense64_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "g2048_dense64_update_workspace": (_i64, [_i64]),
     "g2048_dense64_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
-                                    _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),
+                                    _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
     "g2048_last_error": (C.c_char_p, []),
     "g2048_abi_version": (_int, []),
 }

@@ -77,6 +77,10 @@ class DQNLearner:
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
             self._adam = FusedAdam(params, lr=lr)
+            # the target sync (every target_sync_every updates) is done by the Adam launch on
+            # the device update counter: no host decision between graph replays
+            if self.target_sync_every:
+                self._adam.attach_target(list(self.target.parameters()), self.target_sync_every)
             # dense64: sampler + targets + gradient in ONE launch, and (single process) Adam
             # folded into the gradient reduction -- 2 launches per update
             self._upd = (qnet.Dense64Update(self.model, self.target, self.B,
@@ -135,6 +139,8 @@ class DQNLearner:
         # the warm-up below runs real updates; snapshot weights so capture leaves no trace
         params = list(self.model.parameters())
         snap = [p.detach().clone() for p in params]
+        tparams = list(self.target.parameters())  # the fused Adam may sync the target
+        tsnap = [p.detach().clone() for p in tparams]
         step0 = self.step_dev.clone() if self.fused else None
         loss0 = self.last_loss.clone()
         rng0 = torch.cuda.get_rng_state(self.device)  # the warm-up draws must not shift the stream
@@ -166,6 +172,8 @@ class DQNLearner:
         with torch.no_grad():  # restore in place (the graphs hold these addresses)
             for p, s in zip(params, snap):
                 p.copy_(s)
+            for p, s in zip(tparams, tsnap):
+                p.copy_(s)
             for p, st in self.opt.state.items():
                 prev = adam0.get(p, {}) if not self.fused else {}
                 for k, v in st.items():
@@ -196,7 +204,8 @@ class DQNLearner:
             self._allreduce()
             self._apply()
         self.updates += 1
-        if self.target_sync_every and self.updates % self.target_sync_every == 0:
+        if (not self.fused and self.target_sync_every
+                and self.updates % self.target_sync_every == 0):
             dqn_lib.sync_target(self.model, self.target)
         return self.last_loss
 
@@ -330,30 +339,22 @@ class Trainer:
                                   done=self._done, action=self._action, eps_schedule=sched)
 
     def _graphed_iteration(self) -> None:
-        """One iteration as hipGraph replays: [step + first update], then [update] for each
-        further update, with the target sync checked between updates exactly as in
-        DQNLearner.update.  Capture records without executing, and every kernel of the fused
-        path reads its varying state (boards, ring position, update counter) from device memory,
-        so replay k equals eager iteration k bit for bit."""
+        """One iteration (step + updates_per_step updates, target syncs included: the fused
+        Adam performs them on the device update counter) as ONE hipGraph replay.  Capture
+        records without executing, and every kernel of the fused path reads its varying state
+        (boards, ring position, update counter) from device memory, so replay k equals eager
+        iteration k bit for bit."""
         L = self.learner
         if self._loop_graph is None:
-            g1, g2 = torch.cuda.CUDAGraph(), None
-            with torch.cuda.graph(g1):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
                 self._rollout_step()
-                L._compute_grads()
-                L._apply()
-            if self.updates_per_step > 1:
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2):
+                for _ in range(self.updates_per_step):
                     L._compute_grads()
                     L._apply()
-            self._loop_graph = (g1, g2)
-        g1, g2 = self._loop_graph
-        for u in range(self.updates_per_step):
-            (g1 if u == 0 else g2).replay()
-            L.updates += 1
-            if L.target_sync_every and L.updates % L.target_sync_every == 0:
-                dqn_lib.sync_target(L.model, L.target)
+            self._loop_graph = g
+        self._loop_graph.replay()
+        L.updates += self.updates_per_step
 
     def step(self) -> None:
         if self.track:

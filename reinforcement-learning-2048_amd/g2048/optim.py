@@ -24,6 +24,20 @@ class FusedAdam:
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float32, device=dev)
         self._ptrs = (C.c_void_p * len(self.params))(*[p.data_ptr() for p in self.params])
         self._numel = (C.c_int64 * len(self.params))(*[p.numel() for p in self.params])
+        self._tptrs, self.sync_every = None, 0
+
+    def attach_target(self, target_params, sync_every: int) -> None:
+        """Also write the updated parameters into target_params whenever the device step
+        counter t is a multiple of sync_every (the target-net sync of training_loop, decided
+        on the device, so graph replays need no host decision)."""
+        tps = [t for t in target_params]
+        if len(tps) != len(self.params) or any(t.shape != p.shape or t.dtype != p.dtype
+                                               or not t.is_contiguous()
+                                               for t, p in zip(tps, self.params)):
+            raise ValueError("target params must match the optimised params")
+        self._target = tps
+        self._tptrs = (C.c_void_p * len(tps))(*[t.data_ptr() for t in tps])
+        self.sync_every = int(sync_every)
 
     def reset_state(self):
         self.exp_avg.zero_()
@@ -32,7 +46,8 @@ class FusedAdam:
     def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor):
         """grad_flat: fp32 gradients of self.params packed in order; step_counter: device u64
         holding t (>= 1) for this step's bias correction."""
-        N.check(N.load().g2048_adam_step(
+        N.check(N.load().g2048_adam_step_sync(
             self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
             N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
-            self.eps, N.stream_of(grad_flat.device)), "g2048_adam_step")
+            self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0,
+            N.stream_of(grad_flat.device)), "g2048_adam_step_sync")

@@ -128,7 +128,8 @@ class Dense64Update:
     (g2048_dense64_update): sampler + both target-side forwards + Bellman + MSE gradient per
     32-row tile, then the fixed-order gradient reduction with Adam applied in place (adam given)
     or the summed gradient left in grad_out (adam=None, for a data-parallel all-reduce followed by
-    FusedAdam.step).  step_dev: device u64 update counter (sampler epoch in, +1 out)."""
+    FusedAdam.step).  step_dev: device u64 update counter (sampler epoch in, +1 out).  An Adam
+    with attach_target(target params, K) also syncs the target net every K-th update."""
 
     def __init__(self, model, target, batch: int, adam=None):
         if kind_of(model) != "dense64" or kind_of(target) != "dense64":
@@ -153,7 +154,8 @@ class Dense64Update:
             C.byref(self.on), C.byref(self.tg), replay.handle, N.ptr(idx_in), self.batch,
             int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)), N.ptr(idx_out),
             N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(m),
-            N.ptr(v), float(lr), float(b1), float(b2), float(eps), N.stream_of(y_out.device)),
+            N.ptr(v), float(lr), float(b1), float(b2), float(eps),
+            int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
             "g2048_dense64_update")
 
 

@@ -165,3 +165,32 @@ def test_fused_graphed_learner_equals_eager(G, net):
     assert outs[0][2] == outs[1][2] == 7
     np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6)
     torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("net", ["dense64", "conv"])
+@pytest.mark.parametrize("graph", [True, False])
+def test_fused_target_sync_on_device(G, net, graph):
+    """The fused Adam syncs the target net when the device update counter hits a multiple of
+    target_sync_every (training_loop's `ep % 100 == 0` sync, src/dqn_lib.py:227-228): after
+    update 3 the target equals the online net bitwise; after update 4 it still holds the
+    update-3 weights."""
+    from g2048.learner import DQNLearner
+
+    n, C = 2048, 16 * 2048
+    env = G.VecEnv2048(n, device=DEV, seed=13)
+    rb = G.ReplayBuffer(C, device=DEV)
+    env.rollout(C // n, replay=rb)
+    L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=512, graph=graph, seed=2,
+                   target_sync_every=3)
+    t0 = [p.detach().clone() for p in L.target.parameters()]
+    flat = lambda m: torch.cat([p.detach().reshape(-1) for p in m.parameters()])  # noqa: E731
+    for k in range(1, 5):
+        L.update()
+        torch.cuda.synchronize()
+        if k < 3:
+            assert all(torch.equal(a, b) for a, b in zip(L.target.parameters(), t0)), k
+        if k == 3:
+            after3 = flat(L.model).clone()
+            assert torch.equal(flat(L.target), after3)
+    assert torch.equal(flat(L.target), after3) and not torch.equal(flat(L.model), after3)
+    assert int(L.step_dev) == 4 == L.updates
