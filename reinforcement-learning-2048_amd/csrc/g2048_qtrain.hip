@@ -191,13 +191,39 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
             f32x16 c0 = f32x16{0}, c1 = f32x16{0};
             const int r = wave * 32 + l32, s = r >> 2, q = r & 3, qh = q >> 1, qw = q & 1;
             const float* x = xs + s * 16;
-#pragma unroll 4
-            for (int kk = 0; kk < 128; ++kk) {
-                const int k = 2 * kk + half, c = k >> 2, kh = (k >> 1) & 1, kw = k & 1;
-                const float4 wc = *reinterpret_cast<const float4*>(sw1 + c * 4);
-                const float a = fmaxf(conv1_pre(x, qh + kh, qw + kw, wc, sb1[c]), 0.f);
-                c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w[k * WT_STRIDE + l32], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, w[k * WT_STRIDE + 32 + l32], c1, 0, 0, 0);
+            // k = 2kk + half: kw = half is fixed per lane and kh = kk & 1, so the lane only ever
+            // reads the 3x2 window xv[rr][cc] = x[qh + rr][qw + half + cc] -- in registers, the
+            // same products in the same order as conv1_pre
+            float xv[3][2];
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                for (int cc = 0; cc < 2; ++cc) xv[rr][cc] = x[(qh + rr) * 4 + qw + half + cc];
+            // chunks of 16 k-steps: the 16 conv1 operands as independent VALU chains first
+            // (full issue rate), then their 32 MFMAs with no VALU in between (a dependent conv1
+            // chain feeding every MFMA is not hidden at one wave per SIMD)
+#pragma unroll 1
+            for (int ch = 0; ch < 8; ++ch) {
+                float av[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int c = (ch * 32 + 2 * j) >> 2, kh = j & 1;
+                    const float4 wc = *reinterpret_cast<const float4*>(sw1 + c * 4);
+                    float pre = sb1[c];
+                    pre = fmaf(wc.x, xv[kh][0], pre);
+                    pre = fmaf(wc.y, xv[kh][1], pre);
+                    pre = fmaf(wc.z, xv[kh + 1][0], pre);
+                    pre = fmaf(wc.w, xv[kh + 1][1], pre);
+                    av[j] = fmaxf(pre, 0.f);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int k = 2 * (ch * 16 + j) + half;
+                    c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], w[k * WT_STRIDE + l32], c0, 0, 0, 0);
+                    c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], w[k * WT_STRIDE + 32 + l32], c1, 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
@@ -339,63 +365,112 @@ __global__ __launch_bounds__(NT) void k_conv_train(TrainArgs A) {
         }
         {
             // lane row k = kt*32 + l32 for kt in {2*wave, 2*wave+1}: c, kh, kw fixed per lane
-            int kc[2], kdh[2], kdw[2];
+            // (kh, kw the same for both kt).  Row m = 2kk + half: board kk >> 1, position
+            // (qh, qw) = (kk & 1, half).  Chunks of 8 k-steps: the 16 conv1 operands from a 3x2
+            // register window of each of the chunk's 4 boards (independent VALU chains, the
+            // products of conv1_pre in its order), then their 32 MFMAs.
+            const int kdh = (l32 >> 1) & 1, kdw = l32 & 1;
             float4 wc[2];
             float bc[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const int k = (2 * wave + u) * 32 + l32;
-                kc[u] = k >> 2;
-                kdh[u] = (k >> 1) & 1;
-                kdw[u] = k & 1;
-                wc[u] = *reinterpret_cast<const float4*>(sw1 + kc[u] * 4);
-                bc[u] = sb1[kc[u]];
+                const int c = ((2 * wave + u) * 32 + l32) >> 2;
+                wc[u] = *reinterpret_cast<const float4*>(sw1 + c * 4);
+                bc[u] = sb1[c];
             }
-#pragma unroll 2
-            for (int kk = 0; kk < 64; ++kk) {
-                const int m = 2 * kk + half, s = m >> 2, q = m & 3, qh = q >> 1, qw = q & 1;
-                const float* x = xs + s * 16;
-                const float a0 = fmaxf(conv1_pre(x, qh + kdh[0], qw + kdw[0], wc[0], bc[0]), 0.f);
-                const float a1 = fmaxf(conv1_pre(x, qh + kdh[1], qw + kdw[1], wc[1], bc[1]), 0.f);
-                const float g0 = h2[s * H2_STRIDE + q * 64 + l32];
-                const float g1 = h2[s * H2_STRIDE + q * 64 + 32 + l32];
-                accW2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, g0, accW2[0], 0, 0, 0);
-                accW2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, g1, accW2[1], 0, 0, 0);
-                accW2[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, g0, accW2[2], 0, 0, 0);
-                accW2[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, g1, accW2[3], 0, 0, 0);
+#pragma unroll 1
+            for (int ch = 0; ch < 8; ++ch) {
+                float av[2][8];
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb) {
+                    const float* x = xs + (4 * ch + jb) * 16;
+                    float xv[3][2];
+#pragma unroll
+                    for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                        for (int cc = 0; cc < 2; ++cc) xv[rr][cc] = x[(kdh + rr) * 4 + half + kdw + cc];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e)
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) {
+                            float pre = bc[u];
+                            pre = fmaf(wc[u].x, xv[e][0], pre);
+                            pre = fmaf(wc[u].y, xv[e][1], pre);
+                            pre = fmaf(wc[u].z, xv[e + 1][0], pre);
+                            pre = fmaf(wc[u].w, xv[e + 1][1], pre);
+                            av[u][2 * jb + e] = fmaxf(pre, 0.f);
+                        }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int m = 2 * (8 * ch + j) + half, s = m >> 2, q = m & 3;
+                    const float g0 = h2[s * H2_STRIDE + q * 64 + l32];
+                    const float g1 = h2[s * H2_STRIDE + q * 64 + 32 + l32];
+                    accW2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][j], g0, accW2[0], 0, 0, 0);
+                    accW2[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[0][j], g1, accW2[1], 0, 0, 0);
+                    accW2[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][j], g0, accW2[2], 0, 0, 0);
+                    accW2[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[1][j], g1, accW2[3], 0, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         TPHASE(10);
         // ---- K: dP = dh2 @ W2 per (m-tile, k-tile); epilogue folds col2im + relu'(h1) into
-        //         per-lane dW1 / db1 sums.  Lane col k = kt*32 + l32 (kt = 2*wave + u).
+        //         per-lane dW1 / db1 sums.  Lane col k_u = (2*wave + u)*32 + l32: kh, kw are
+        //         the same for both u (k & 3 = l32 & 3), so per m-tile one MFMA loop makes both
+        //         k-tiles (shared A operand), and the lane's 3x3 input window of each of its 4
+        //         boards is read once into registers for both epilogues.
+        {
+            const int kh = (l32 >> 1) & 1, kw = l32 & 1;
+            float4 wc[2];
+            float bc[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int kt = 2 * wave + u, k = kt * 32 + l32;
-            const int c = k >> 2, kh = (k >> 1) & 1, kw = k & 1;
-            const float4 wc = *reinterpret_cast<const float4*>(sw1 + c * 4);
-            const float bc = sb1[c];
+            for (int u = 0; u < 2; ++u) {
+                const int c = ((2 * wave + u) * 32 + l32) >> 2;
+                wc[u] = *reinterpret_cast<const float4*>(sw1 + c * 4);
+                bc[u] = sb1[c];
+            }
 #pragma unroll 1
             for (int mt = 0; mt < 4; ++mt) {
-                f32x16 dp = f32x16{0};
+                f32x16 dp0 = f32x16{0}, dp1 = f32x16{0};
                 const int m = mt * 32 + l32, s = m >> 2, q = m & 3;
 #pragma unroll 8
                 for (int kk = 0; kk < 32; ++kk) {
                     const int cp = 2 * kk + half;
-                    dp = __builtin_amdgcn_mfma_f32_32x32x2f32(h2[s * H2_STRIDE + q * 64 + cp],
-                                                              w[cp * WR_STRIDE + k], dp, 0, 0, 0);
+                    const float av = h2[s * H2_STRIDE + q * 64 + cp];
+                    dp0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w[cp * WR_STRIDE + (2 * wave) * 32 + l32], dp0, 0, 0, 0);
+                    dp1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, w[cp * WR_STRIDE + (2 * wave + 1) * 32 + l32], dp1, 0, 0, 0);
                 }
+                // rows of register i: board sr = mt*8 + 2*(i>>2) + half, position qr = i & 3
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int mr = mt * 32 + acc_row32(i, lane), sr = mr >> 2, qr = mr & 3;
-                    const int ph = (qr >> 1) + kh, pw = (qr & 1) + kw;
-                    const float* x = xs + sr * 16;
-                    const float pre = conv1_pre(x, ph, pw, wc, bc);
-                    const float v = pre > 0.f ? dp[i] : 0.f;
-                    accb1[u] += v;
-                    accw1[u][0] = fmaf(v, x[ph * 4 + pw], accw1[u][0]);
-                    accw1[u][1] = fmaf(v, x[ph * 4 + pw + 1], accw1[u][1]);
-                    accw1[u][2] = fmaf(v, x[(ph + 1) * 4 + pw], accw1[u][2]);
-                    accw1[u][3] = fmaf(v, x[(ph + 1) * 4 + pw + 1], accw1[u][3]);
+                for (int j = 0; j < 4; ++j) {
+                    const float* x = xs + (mt * 8 + 2 * j + half) * 16;
+                    float xw[3][3];
+#pragma unroll
+                    for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+                        for (int cc = 0; cc < 3; ++cc) xw[rr][cc] = x[(kh + rr) * 4 + kw + cc];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+                        for (int qr = 0; qr < 4; ++qr) {
+                            const int qh = qr >> 1, qw = qr & 1, i = 4 * j + qr;
+                            const float x00 = xw[qh][qw], x01 = xw[qh][qw + 1];
+                            const float x10 = xw[qh + 1][qw], x11 = xw[qh + 1][qw + 1];
+                            float pre = bc[u];  // conv1_pre's products, in its order
+                            pre = fmaf(wc[u].x, x00, pre);
+                            pre = fmaf(wc[u].y, x01, pre);
+                            pre = fmaf(wc[u].z, x10, pre);
+                            pre = fmaf(wc[u].w, x11, pre);
+                            const float v = pre > 0.f ? (u ? dp1[i] : dp0[i]) : 0.f;
+                            accb1[u] += v;
+                            accw1[u][0] = fmaf(v, x00, accw1[u][0]);
+                            accw1[u][1] = fmaf(v, x01, accw1[u][1]);
+                            accw1[u][2] = fmaf(v, x10, accw1[u][2]);
+                            accw1[u][3] = fmaf(v, x11, accw1[u][3]);
+                        }
+                    }
                 }
             }
         }
