@@ -215,6 +215,22 @@ G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* params,
                                        float* workspace_dev, float* grad_out_dev,
                                        float* loss_out_dev, uint64_t* step_dev, void* stream);
 
+/* g2048_convnet_train_grad with optimizer.step() folded into the gradient reduction (single
+ * process; src/dqn_lib.py:146-163 in the intended zero_grad -> backward -> step order): the
+ * same sums as train_grad, then Adam exactly as g2048_adam_step_sync (t = *step_dev after the
+ * train launch's increment), applied in place to `params`; when sync_every > 0 and t is a
+ * multiple of it, the updated parameters are also written to `target` (src/dqn_lib.py:227-228).
+ * grad_out may be NULL (then only the parameters change).  2 launches per update. */
+G2048_API int g2048_convnet_train_adam(const g2048_convnet_params* params,
+                                       const uint8_t* rows_dev, const uint8_t* actions_dev,
+                                       const int64_t* idx_dev, const float* y_dev, int64_t batch,
+                                       float* workspace_dev, float* grad_out_dev,
+                                       float* loss_out_dev, uint64_t* step_dev,
+                                       float* exp_avg_dev, float* exp_avg_sq_dev, double lr,
+                                       double beta1, double beta2, double eps,
+                                       const g2048_convnet_params* target, uint64_t sync_every,
+                                       void* stream);
+
 /* Double-DQN targets for a minibatch in one launch (src/dqn_lib.py:67-68,125-132): indices
  * idx_out[b] = idx_in[b], or uniform over the ring's filled rows from Philox (seed, *epoch_dev)
  * -- the same draw as g2048_replay_sample_encode's; then y[b] = r + ((1 - d) * float32(gamma)) *

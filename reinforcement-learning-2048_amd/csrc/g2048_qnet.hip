@@ -5,17 +5,11 @@
 // src/board.py:224-231) read straight from u8 rows -- optionally gathered through replay
 // indices, so sample_experiences + extract_samples_conv + forward are one launch.
 //
-// One workgroup (256 threads, 4 waves) = a tile of S = 32 boards; everything stays in LDS:
-//   conv1  VALU: 32 x 9 positions x 64 channels, 4 MACs each               -> h1  (LDS)
-//   conv2  MFMA v_mfma_f32_32x32x2_f32: [128 = 32 boards x 4 positions] x [256 = c,kh,kw]
-//          @ [256 x 64]; wave w owns rows 32w..32w+31 and both 32-col tiles  -> h2  (LDS)
-//   fc1    MFMA v_mfma_f32_16x16x4_f32: [32 x 256] @ [256 x 64], 2 tiles per wave -> f (LDS)
-//   fc2    VALU: 32 x 4 dot products of length 64                          -> Q (HBM)
-// Weight matrices are staged transposed ([k][n], row stride 65 floats: conflict-free both for
-// the coalesced staging writes and the MFMA B-operand reads); fc1's weights are prefetched into
-// VGPRs during the conv2 MFMA loop (one wave per SIMD leaves plenty of registers).
-// Numerics: f32 in / f32 accumulate; each MFMA is an exact k-ordered fmaf chain, so results
-// differ from torch's GEMMs only by summation order (tests: rtol 1e-5 vs torch fp32).
+// Every launch is persistent: a workgroup (256 threads, 4 waves, one per CU) stages the net
+// once and loops over 16-board tiles; conv2 runs as nine Winograd-domain GEMMs on
+// v_mfma_f32_16x16x4_f32 (layout and numerics: see the persist namespace below).
+// Numerics: f32 in / f32 accumulate; results differ from torch's fp32 GEMMs by summation order
+// and the Winograd transforms' adds (tests: rtol 2e-5 vs torch fp32 and fp64).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -25,26 +19,8 @@
 
 namespace {
 
-constexpr int S = 32;            // boards per workgroup
-constexpr int NT = 256;          // threads per workgroup
-constexpr int H1_STRIDE = 65;    // floats per (board, position) row of h1
-constexpr int WT_STRIDE = 65;    // floats per k row of a staged transposed weight
-constexpr int H2_STRIDE = 257;   // floats per board row of h2, stored [q][c'] (k' = q*64 + c')
-constexpr int F_STRIDE = 65;
+constexpr int NT = 256;  // threads per workgroup
 
-// LDS carve (floats)
-constexpr int OFF_X = 0;                                  // [S][16]
-constexpr int OFF_SMALL = OFF_X + S * 16;                 // w1 256, b1 64, b2 64, bf1 64, wf2 4x65, bf2 4
-constexpr int SMALL_FLOATS = 256 + 64 + 64 + 64 + 4 * 65 + 4;
-constexpr int OFF_R1 = OFF_SMALL + ((SMALL_FLOATS + 3) & ~3);
-constexpr int R1_FLOATS = S * 9 * H1_STRIDE;              // h1, later h2 + f
-constexpr int OFF_R2 = OFF_R1 + ((R1_FLOATS + 3) & ~3);
-constexpr int R2_FLOATS = 256 * WT_STRIDE;                // W2t, later Wf1t
-constexpr int LDS_FLOATS = OFF_R2 + R2_FLOATS;
-static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
-static_assert(S * H2_STRIDE + S * F_STRIDE <= R1_FLOATS, "h2 + f must fit in the h1 region");
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct ConvNetArgs {
@@ -66,372 +42,254 @@ struct NetW {
     const float *w1, *b1, *w2, *b2, *wf1, *bf1, *wf2, *bf2;
 };
 
-// Q-values of the S boards staged in lds[OFF_X] (exponents as floats) with net weights W;
-// writes qs[s*4 + a] (LDS).  Caller: __syncthreads() before (xs staged) -- this function ends
-// with one after qs is written.
-__device__ __forceinline__ void conv_forward_tile(const NetW& W, float* lds, float* qs) {
-    float* xs = lds + OFF_X;
-    float* sw1 = lds + OFF_SMALL;       // [c][4]
-    float* sb1 = sw1 + 256;
-    float* sb2 = sb1 + 64;
-    float* sbf1 = sb2 + 64;
-    float* swf2 = sbf1 + 64;            // [a][j] stride 65
-    float* sbf2 = swf2 + 4 * 65;
-    float* h1 = lds + OFF_R1;           // [(s*9+p)][c] stride 65
-    float* h2 = lds + OFF_R1;           // [s][q*64+c'] stride 257 (after conv2)
-    float* fa = lds + OFF_R1 + S * H2_STRIDE;  // [s][j] stride 65
-    float* wt = lds + OFF_R2;           // [k][n] stride 65
-
-    const int t = threadIdx.x;
-    const int lane = t & 63;
-    const int wave = t >> 6;
-
-    // ---- stage small weights and W2 transposed: wt[k][n] = w2[n][k], k = c*4 + kh*2 + kw
-    sw1[t] = W.w1[t];
-    if (t < 64) {
-        sb1[t] = W.b1[t];
-        sb2[t] = W.b2[t];
-        sbf1[t] = W.bf1[t];
-    }
-    swf2[(t >> 6) * 65 + (t & 63)] = W.wf2[t];
-    if (t < 4) sbf2[t] = W.bf2[t];
-#pragma unroll 4
-    for (int i = 0; i < 64; ++i) wt[t * WT_STRIDE + i] = W.w2[i * NT + t];
-    __syncthreads();
-
-    // ---- conv1 -> h1 (VALU).  thread: channel c = lane, boards s = wave*8 .. wave*8+7
-    {
-        const int c = lane;
-        const float w00 = sw1[c * 4 + 0], w01 = sw1[c * 4 + 1], w10 = sw1[c * 4 + 2],
-                    w11 = sw1[c * 4 + 3], bb = sb1[c];
-#pragma unroll
-        for (int si = 0; si < 8; ++si) {
-            const int s = wave * 8 + si;
-            const float* x = xs + s * 16;
-#pragma unroll
-            for (int p = 0; p < 9; ++p) {
-                const int ph = p / 3, pw = p % 3;
-                float v = bb;
-                v = fmaf(w00, x[ph * 4 + pw], v);
-                v = fmaf(w01, x[ph * 4 + pw + 1], v);
-                v = fmaf(w10, x[(ph + 1) * 4 + pw], v);
-                v = fmaf(w11, x[(ph + 1) * 4 + pw + 1], v);
-                h1[(s * 9 + p) * H1_STRIDE + c] = fmaxf(v, 0.0f);
-            }
-        }
-    }
-    // prefetch fc1 weights into registers (consumed after conv2): 64 per thread
-    float pf[64];
-#pragma unroll
-    for (int i = 0; i < 64; ++i) pf[i] = W.wf1[i * NT + t];
-    __syncthreads();
-
-    // ---- conv2 (MFMA 32x32x2): rows r = 32*wave + (lane&31): board s = r>>2, position q = r&3
-    f32x16 acc0 = {0}, acc1 = {0};
-    {
-        const int r = wave * 32 + (lane & 31);
-        const int s = r >> 2, q = r & 3;
-        const int qh = q >> 1, qw = q & 1;
-        const float* h1s = h1 + s * 9 * H1_STRIDE;
-        const int khalf = lane >> 5;
-        const int ncol = lane & 31;
-#pragma unroll 8
-        for (int kk = 0; kk < 128; ++kk) {
-            const int k = 2 * kk + khalf;
-            const int c = k >> 2, kh = (k >> 1) & 1, kw = k & 1;
-            const float a = h1s[((qh + kh) * 3 + (qw + kw)) * H1_STRIDE + c];
-            const float bA = wt[k * WT_STRIDE + ncol];
-            const float bB = wt[k * WT_STRIDE + 32 + ncol];
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bA, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bB, acc1, 0, 0, 0);
-        }
-    }
-    __syncthreads();  // h1 and W2t are dead from here
-
-    // ---- conv2 epilogue: bias + ReLU -> h2[s][q*64 + c']; stage fc1 weights transposed
-    {
-        const int col = lane & 31;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-            const int r = wave * 32 + row;
-            const int s = r >> 2, q = r & 3;
-            h2[s * H2_STRIDE + q * 64 + col] = fmaxf(acc0[i] + sb2[col], 0.0f);
-            h2[s * H2_STRIDE + q * 64 + col + 32] = fmaxf(acc1[i] + sb2[col + 32], 0.0f);
-        }
-#pragma unroll
-        for (int i = 0; i < 64; ++i) {
-            // wf1[j][m], j = i, m = t (flatten index c'*4 + q) -> row k' = q*64 + c'
-            wt[((t & 3) * 64 + (t >> 2)) * WT_STRIDE + i] = pf[i];
-        }
-    }
-    __syncthreads();
-
-    // ---- fc1 (MFMA 16x16x4): [32 boards x 256] @ [256 x 64]; wave w: m-tile w&1, n-tiles (w>>1)*2 + {0,1}
-    {
-        const int mt = wave & 1;
-        const int nt0 = (wave >> 1) * 2;
-        f32x4 c0 = {0}, c1 = {0};
-        const int arow = mt * 16 + (lane & 15);
-        const int kq = lane >> 4;
-        const int ncol = lane & 15;
-#pragma unroll 8
-        for (int kk = 0; kk < 64; ++kk) {
-            const int k = 4 * kk + kq;
-            const float a = h2[arow * H2_STRIDE + k];
-            const float bA = wt[k * WT_STRIDE + nt0 * 16 + ncol];
-            const float bB = wt[k * WT_STRIDE + (nt0 + 1) * 16 + ncol];
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bA, c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bB, c1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = mt * 16 + (lane >> 4) * 4 + i;
-            const int ja = nt0 * 16 + ncol, jb = (nt0 + 1) * 16 + ncol;
-            fa[row * F_STRIDE + ja] = fmaxf(c0[i] + sbf1[ja], 0.0f);
-            fa[row * F_STRIDE + jb] = fmaxf(c1[i] + sbf1[jb], 0.0f);
-        }
-    }
-    __syncthreads();
-
-    // ---- fc2 (VALU): thread t < 128 -> board s = t>>2, action a = t&3
-    if (t < S * 4) {
-        const int s = t >> 2, a = t & 3;
-        float v = sbf2[a];
-#pragma unroll 16
-        for (int j = 0; j < 64; ++j) v = fmaf(swf2[a * 65 + j], fa[s * F_STRIDE + j], v);
-        qs[t] = v;
-    }
-    __syncthreads();
-}
-
-// stage 32 boards (rows[idx[b]] or rows[b]) as float exponents into xs
-__device__ __forceinline__ void stage_boards(float* xs, const uint8_t* rows, const int64_t* idx,
-                                             int64_t b0, int64_t n) {
-    const int t = threadIdx.x;
-    if (t < S * 4) {
-        const int s = t >> 2, w = t & 3;
-        const int64_t b = b0 + s;
-        uint32_t v = 0;
-        if (b < n) {
-            const int64_t row = idx ? idx[b] : b;
-            v = reinterpret_cast<const uint32_t*>(rows)[row * 4 + w];
-        }
-        float* dst = xs + s * 16 + w * 4;
-        dst[0] = (float)(v & 0xFFu);
-        dst[1] = (float)((v >> 8) & 0xFFu);
-        dst[2] = (float)((v >> 16) & 0xFFu);
-        dst[3] = (float)(v >> 24);
-    }
-}
-
-__global__ __launch_bounds__(NT) void k_conv_forward(ConvNetArgs A) {
-    __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
-    __shared__ float qs[S * 4];
-    const int64_t b0 = (int64_t)blockIdx.x * S;
-    stage_boards(lds + OFF_X, A.rows, A.idx, b0, A.n);
-    __syncthreads();
-    conv_forward_tile(NetW{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2}, lds, qs);
-    const int t = threadIdx.x;
-    if (t < S * 4 && b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = qs[t];
-}
+// Phase profiler (tools/prof_forward.hip builds with G2048_PHASE_PROF): thread 0 of workgroup 0
+// accumulates s_memtime deltas between the tile's barriers.
+#ifdef G2048_PHASE_PROF
+__device__ unsigned long long g2048_phase_ticks[8];
+#define PHASE_BEGIN() unsigned long long phase_t0_ = __builtin_amdgcn_s_memtime()
+#define PHASE(k)                                                          \
+    do {                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                        \
+            const unsigned long long n_ = __builtin_amdgcn_s_memtime();   \
+            g2048_phase_ticks[k] += n_ - phase_t0_;                       \
+            phase_t0_ = n_;                                               \
+        }                                                                 \
+    } while (0)
+#else
+#define PHASE_BEGIN()
+#define PHASE(k)
+#endif
 
 // ---------------------------------------------------------------------------------------------
-// ---------------------------------------------------------------------------------------------
-// Persistent kernels (rollout forward for large n, Double-DQN targets): a workgroup stages a
-// net's W2 once (LDS) and its fc1_w once (registers: each wave keeps its 16-unit slice in 64
-// VGPRs, fc1's B operand), then runs 16-board tiles.
+// Persistent kernels (every conv forward, Double-DQN targets): a workgroup stages a net once
+// and then runs 16-board tiles.  conv2 runs in the Winograd domain F(2x2, 2x2):
+//
+//   Y = A^T [ sum_c (G g_oc G^T) .* (B^T d_c B) ] A,
+//   B^T = [[1,-1,0],[0,1,0],[0,-1,1]]   G = [[1,0],[1,1],[0,1]]   A^T = [[1,1,0],[0,1,1]]
+//
+// with d_c the 3x3 relu(conv1) map of input channel c and g_oc the 2x2 kernel.  The 2x2 output
+// of a 3x3 input then costs 9 products per (c, o) instead of 16: conv2 becomes nine
+// [16 boards x 64 c] @ [64 c x 64 o] GEMMs per tile (36 864 MAC per board instead of 65 536).
+// All coefficients are 0 / +-1, so the only extra rounding is a handful of adds per value
+// (measured: fp32 error 1.4x that of the direct sum, both ~1e-7 relative).
 //
 // On gfx950 a VALU op between f32 MFMAs is not hidden (tools/prof_forward.hip: +4 cycles per op,
 // ~12 when the ops form dependent chains), so the MFMA loops carry no VALU at all:
-//  * conv1 runs as its own phase: thread (channel c = t&63, board group t>>6) reads its 4
-//    boards' 64 cells at once and runs 36 independent fma chains into h1[c][board*9 + pos]
-//    (channel stride 145 = 17 mod 64: conflict-free writes and reads);
-//  * conv2 is split by ROWS: wave w owns boards 4w..4w+3 (16 rows (s, q)) x all 64 channels as
-//    four 16x16x4 tiles.  Lane group g = lane>>4 is the tap (kh, kw) = (g>>1, g&1) and step c is
-//    the input channel, so k = 4c + g is conv2's flat weight index.  Per step: one ds_read_b32
-//    of h1 (A, shared by the four tiles) + one ds_read_b128 of W2 (B) -> 4 MFMAs;
-//  * fc1: A = h2 read along k as ds_read_b128, B = the wave's fc1_w slice in registers;
+//  * conv1 + the input transform run as their own phase: thread (channel c = t&63, board
+//    group t>>6) computes relu(conv1) at the 9 positions of its boards (independent fma
+//    chains) and writes V_xi = (B^T d B)_xi to V[xi][board][c] (row stride 68 floats);
+//  * conv2: wave w owns output channels 16w..16w+15.  Its B operands U_xi[c][o] (9 x 64 x 16
+//    values, 144 per lane) are computed from W2 when the net is staged and stay in VGPRs.
+//    Lane group g covers input channels 16g..16g+15, so a lane's A operands for one point xi
+//    are 4 ds_read_b128 of V; per point 16 MFMAs 16x16x4, three point-chains interleaved;
+//  * the output transform (lane-local: a lane holds all 9 points of its 4 boards x 1 channel)
+//    + bias + ReLU writes h2[s][q*64 + o];
+//  * fc1: A = h2 and B = fc1_w[j][k'] (LDS, k' = q*64 + c' = torch's flat index permuted),
+//    both read along k as ds_read_b128;
 //  * fc2 uses all 256 threads and leaves Q[16][4] in LDS.
 namespace persist {
 constexpr int S = 16;
-constexpr int TMAX = 8;   // tiles per workgroup in the targets kernel
-constexpr int H1S = 145;  // floats per channel of h1: [c][board*9 + pos], 16*9 = 144 used
-constexpr int H2S = 260;  // h2[s][k'], k' = q*64 + n (fc1's input index permuted)
-constexpr int FS = 68;    // fa[s][j] (16-byte aligned rows for fc2's b128 reads)
-constexpr int WF2S = 68;  // swf2[a][j]
+constexpr int TMAX = 8;    // tiles per workgroup in the targets kernel
+constexpr int VS = 68;     // floats per board row of V[xi][board][c] (64 used)
+constexpr int VXI = S * VS;  // floats per Winograd point
+constexpr int H2S = 260;   // h2[s][k'], k' = q*64 + n (fc1's input index permuted)
+constexpr int WF1S = 260;  // fc1_w[j][k']
+constexpr int FS = 68;     // fa[s][j] (16-byte aligned rows for fc2's b128 reads)
+constexpr int WF2S = 68;   // swf2[a][j]
 constexpr int OFF_X = 0;                          // [TMAX][S][16] boards (exponents as floats)
 constexpr int OFF_B2 = OFF_X + TMAX * S * 16;     // 64
 constexpr int OFF_BF1 = OFF_B2 + 64;              // 64
 constexpr int OFF_WF2 = OFF_BF1 + 64;             // [4][WF2S]
 constexpr int OFF_BF2 = OFF_WF2 + 4 * WF2S;       // 4
-constexpr int OFF_W2 = OFF_BF2 + 4;               // W2s[k][16 x 4] swizzled, see w2s_index
-constexpr int OFF_H1 = OFF_W2 + 256 * 64;         // also the fc1_w staging area (32 x 260)
-constexpr int OFF_H2 = (OFF_H1 + 64 * H1S + 3) & ~3;
+constexpr int OFF_WF1 = OFF_BF2 + 4;              // [64][WF1S]
+constexpr int OFF_V = OFF_WF1 + 64 * WF1S;        // [9][S][VS]
+constexpr int OFF_H2 = OFF_V + 9 * VXI;
 constexpr int OFF_F = OFF_H2 + S * H2S;
 constexpr int OFF_Q = OFF_F + S * FS;             // [TMAX + 1][S][4] Q of a tile
 constexpr int FLOATS = OFF_Q + (TMAX + 1) * S * 4;
-static_assert(OFF_W2 % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 && OFF_WF2 % 4 == 0 &&
-                  OFF_Q % 4 == 0,
+static_assert(OFF_WF1 % 4 == 0 && OFF_V % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 &&
+                  OFF_WF2 % 4 == 0 && OFF_Q % 4 == 0,
               "b128 alignment");
-static_assert(64 * H1S >= 32 * 260, "fc1_w staging must fit in the h1 area");
-static_assert(FLOATS * 4 <= 160 * 1024, "LDS budget (persistent kernels)");
-// W2s row k holds w2[16nt + j][k] at 4*(j ^ (k & 15)) + nt: a lane group reads 16 distinct
-// 16-byte slots of one row (conflict-free b128) and the staging writes spread over 16 banks.
-__device__ __forceinline__ int w2s_index(int k, int j, int nt) {
-    return k * 64 + 4 * (j ^ (k & 15)) + nt;
-}
+static_assert(FLOATS * 4 <= 156 * 1024, "LDS budget (persistent kernels, + the sample index)");
 
 struct Regs {  // per-thread weights held in registers
-    float4 w1c;    // conv1 weights of channel t & 63
+    float4 w1c;     // conv1 weights of channel t & 63
     float b1c;
-    float wf[64];  // fc1_w[16*wave + l16][kk*4 + g]  (k' = 64g + kk <-> orig kk*4 + g)
+    float u[9][16];  // U_xi[c = 16g + kk][o = 16*wave + l16] = (G g_oc G^T)_xi
 };
 
-// Stage net W: W2 + small tensors into LDS, conv1 channel + fc1_w slice into registers.  All
-// global loads (W2 and both fc1_w halves) are issued before the first LDS store: one memory
-// round trip.  Starts and ends with __syncthreads().
+// Stage net W: U into registers, fc1_w + small tensors into LDS.  All global loads are issued
+// before the first LDS store (one memory round trip).  Starts and ends with __syncthreads().
 __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
-    float v2[64], f[2][32];
+    const int o = 16 * wave + l16;
+    // w2[o][c][kh][kw] for c = 16g .. 16g+15: 64 contiguous floats
+    float4 wv[16];
+    const float4* src = reinterpret_cast<const float4*>(W.w2 + o * 256 + 64 * g);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) v2[i] = W.w2[i * NT + t];  // w2[n = i][k = t]
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 32; ++i) f[h][i] = W.wf1[(32 * h + i) * NT + t];
+    for (int kk = 0; kk < 16; ++kk) wv[kk] = src[kk];
     const int cc = t & 63;
     R.w1c = make_float4(W.w1[4 * cc], W.w1[4 * cc + 1], W.w1[4 * cc + 2], W.w1[4 * cc + 3]);
     R.b1c = W.b1[cc];
     const float b2 = t < 64 ? W.b2[t] : 0.f, bf1 = t < 64 ? W.bf1[t] : 0.f;
     const float wf2 = W.wf2[t], bf2 = t < 4 ? W.bf2[t] : 0.f;
-    __syncthreads();  // previous users of W2s / the h1 area are done
-    float* w2s = lds + OFF_W2;
+    float f[64];  // fc1_w[i][t], i = 0..63
 #pragma unroll
-    for (int i = 0; i < 64; ++i) w2s[w2s_index(t, i & 15, i >> 4)] = v2[i];
+    for (int i = 0; i < 64; ++i) f[i] = W.wf1[i * NT + t];
+    __syncthreads();  // previous users of the LDS weight areas are done
     if (t < 64) {
         lds[OFF_B2 + t] = b2;
         lds[OFF_BF1 + t] = bf1;
     }
     lds[OFF_WF2 + (t >> 6) * WF2S + (t & 63)] = wf2;
     if (t < 4) lds[OFF_BF2 + t] = bf2;
-    // fc1_w through the h1 area in two halves of 32 rows (row stride 260 = 4 mod 64, so the
-    // stride-4 register gather is conflict-free)
-    float* st = lds + OFF_H1;
+    // fc1_w[j][k], k = c'*4 + q (torch Flatten order) -> fc1_w[j][k' = q*64 + c']
+    float* wf1s = lds + OFF_WF1 + (t & 3) * 64 + (t >> 2);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int i = 0; i < 64; ++i) wf1s[i * WF1S] = f[i];
+    // G g G^T with g = [[a, b], [c, d]] (rows kh, columns kw):
+    //   [[a, a+b, b], [a+c, (a+c)+(b+d), b+d], [c, c+d, d]]
 #pragma unroll
-        for (int i = 0; i < 32; ++i) st[i * 260 + t] = f[h][i];
-        __syncthreads();
-        if ((wave >> 1) == h) {
-            const float* src = st + (16 * (wave & 1) + l16) * 260 + g;
-#pragma unroll
-            for (int kk = 0; kk < 64; ++kk) R.wf[kk] = src[4 * kk];
-        }
-        __syncthreads();
+    for (int kk = 0; kk < 16; ++kk) {
+        const float a = wv[kk].x, b = wv[kk].y, c = wv[kk].z, d = wv[kk].w;
+        const float ac = a + c, bd = b + d;
+        R.u[0][kk] = a;
+        R.u[1][kk] = a + b;
+        R.u[2][kk] = b;
+        R.u[3][kk] = ac;
+        R.u[4][kk] = ac + bd;
+        R.u[5][kk] = bd;
+        R.u[6][kk] = c;
+        R.u[7][kk] = c + d;
+        R.u[8][kk] = d;
     }
+    __syncthreads();
 }
 
 // Q[16][4] of the 16 boards in xs (exponents as floats, visible to all threads) -> qs (LDS).
-// Ends with __syncthreads() (qs visible; h1 / h2 / fa free for the next tile).
+// Ends with __syncthreads() (qs visible; V / h2 / fa free for the next tile).
 __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R, float* qs) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
-    const float* w2s = lds + OFF_W2;
-    float* h1 = lds + OFF_H1;
     float* h2 = lds + OFF_H2;
     float* fa = lds + OFF_F;
-    // ---- conv1 -> h1: channel cc at the 9 positions of boards 4*wave .. 4*wave+3: the 64
-    //      input cells are read at once (one LDS round trip), then 36 independent fma chains
+    PHASE_BEGIN();
+    // ---- conv1 + ReLU + input transform -> V: channel cc of boards 4*wave .. 4*wave+3, two
+    //      boards (32 cells, 18 independent fma chains) at a time
     {
         const int cc = t & 63;
-        float x[4][16];
-#pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float4 v = *reinterpret_cast<const float4*>(xs + (4 * wave + bb) * 16 + 4 * r);
-                x[bb][4 * r] = v.x;
-                x[bb][4 * r + 1] = v.y;
-                x[bb][4 * r + 2] = v.z;
-                x[bb][4 * r + 3] = v.w;
-            }
         const float wt[4] = {R.w1c.x, R.w1c.y, R.w1c.z, R.w1c.w};
-        float v[4][9];
+        float* vdst = lds + OFF_V + cc;
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
+        for (int bp = 0; bp < 2; ++bp) {
+            float x[2][16];
 #pragma unroll
-            for (int p = 0; p < 9; ++p) v[bb][p] = R.b1c;
+            for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-        for (int tap = 0; tap < 4; ++tap)
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb)
-#pragma unroll
-                for (int p = 0; p < 9; ++p) {
-                    const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
-                    v[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], v[bb][p]);
+                for (int r = 0; r < 4; ++r) {
+                    const float4 v =
+                        *reinterpret_cast<const float4*>(xs + (4 * wave + 2 * bp + bb) * 16 + 4 * r);
+                    x[bb][4 * r] = v.x;
+                    x[bb][4 * r + 1] = v.y;
+                    x[bb][4 * r + 2] = v.z;
+                    x[bb][4 * r + 3] = v.w;
                 }
-        float* dst = h1 + cc * H1S + 4 * wave * 9;
+            float h[2][9];
 #pragma unroll
-        for (int bb = 0; bb < 4; ++bb)
+            for (int bb = 0; bb < 2; ++bb)
 #pragma unroll
-            for (int p = 0; p < 9; ++p) dst[bb * 9 + p] = fmaxf(v[bb][p], 0.f);
-    }
-    __syncthreads();
-    // ---- conv2: 64 steps x (A from h1, B from W2s) -> 4 MFMAs, chunks of 8 steps with the next
-    //      chunk's LDS reads in flight
-    {
-        const int s_r = 4 * wave + (l16 >> 2), q_r = l16 & 3;
-        const int pos_r = ((q_r >> 1) + (g >> 1)) * 3 + (q_r & 1) + (g & 1);
-        const float* abase = h1 + s_r * 9 + pos_r;
-        f32x4 acc[4] = {f32x4{0}, f32x4{0}, f32x4{0}, f32x4{0}};
-        float av[2][8];
-        f32x4 bv[2][8];
-        auto load = [&](int chunk, int buf) {
+                for (int p = 0; p < 9; ++p) h[bb][p] = R.b1c;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int c = chunk * 8 + j;
-                av[buf][j] = abase[c * H1S];
-                bv[buf][j] = *reinterpret_cast<const f32x4*>(w2s + w2s_index(4 * c + g, l16, 0));
+            for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+                for (int bb = 0; bb < 2; ++bb)
+#pragma unroll
+                    for (int p = 0; p < 9; ++p) {
+                        const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
+                        h[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], h[bb][p]);
+                    }
+#pragma unroll
+            for (int bb = 0; bb < 2; ++bb) {
+                float d[9];
+#pragma unroll
+                for (int p = 0; p < 9; ++p) d[p] = fmaxf(h[bb][p], 0.f);
+                float r[3][3];  // B^T d: rows (d0 - d1, d1, d2 - d1)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    r[0][j] = d[j] - d[3 + j];
+                    r[1][j] = d[3 + j];
+                    r[2][j] = d[6 + j] - d[3 + j];
+                }
+                float* vb = vdst + (4 * wave + 2 * bp + bb) * VS;
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {  // (B^T d) B: the same on columns
+                    vb[(3 * i + 0) * VXI] = r[i][0] - r[i][1];
+                    vb[(3 * i + 1) * VXI] = r[i][1];
+                    vb[(3 * i + 2) * VXI] = r[i][2] - r[i][1];
+                }
             }
-        };
-        load(0, 0);
-#pragma unroll
-        for (int ch = 0; ch < 8; ++ch) {
-            const int cur = ch & 1;
-            if (ch < 7) load(ch + 1, cur ^ 1);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-#pragma unroll
-                for (int nt = 0; nt < 4; ++nt)
-                    acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[cur][j], bv[cur][j][nt],
-                                                                   acc[nt], 0, 0, 0);
-        }
-        // C: row 4g + i of the wave's 16 -> board 4*wave + g, q = i; col n = 16nt + l16
-        const float* sb2 = lds + OFF_B2;
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) {
-            const int n = 16 * nt + l16;
-            const float bn = sb2[n];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                h2[(4 * wave + g) * H2S + i * 64 + n] = fmaxf(acc[nt][i] + bn, 0.f);
         }
     }
     __syncthreads();
+    PHASE(0);
+    // ---- conv2 in the Winograd domain: M_xi[s][o] = sum_c V_xi[s][c] U_xi[c][o], 9 x 16 MFMAs
+    //      per wave, then Y = A^T M A + bias, ReLU -> h2
+    {
+        f32x4 acc[9];
+#pragma unroll
+        for (int xi = 0; xi < 9; ++xi) acc[xi] = f32x4{0, 0, 0, 0};
+        const float* vsrc = lds + OFF_V + l16 * VS + 16 * g;
+#pragma unroll
+        for (int grp = 0; grp < 3; ++grp) {
+            f32x4 av[3][4];
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+#pragma unroll
+                for (int q4 = 0; q4 < 4; ++q4)
+                    av[e][q4] = *reinterpret_cast<const f32x4*>(vsrc + (3 * grp + e) * VXI + 4 * q4);
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                    acc[3 * grp + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                        av[e][kk >> 2][kk & 3], R.u[3 * grp + e][kk], acc[3 * grp + e], 0, 0, 0);
+        }
+        // C: row 4g + i -> board 4g + i; col -> o = 16*wave + l16
+        const int o = 16 * wave + l16;
+        const float bo = lds[OFF_B2 + o];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            float m[9];
+#pragma unroll
+            for (int xi = 0; xi < 9; ++xi) m[xi] = acc[xi][i];
+            const float r0a = m[0] + m[1], r0b = m[1] + m[2];
+            const float r1a = m[3] + m[4], r1b = m[4] + m[5];
+            const float r2a = m[6] + m[7], r2b = m[7] + m[8];
+            float* hrow = h2 + (4 * g + i) * H2S + o;
+            hrow[0] = fmaxf((r0a + r1a) + bo, 0.f);    // (qh, qw) = (0, 0)
+            hrow[64] = fmaxf((r0b + r1b) + bo, 0.f);   // (0, 1)
+            hrow[128] = fmaxf((r1a + r2a) + bo, 0.f);  // (1, 0)
+            hrow[192] = fmaxf((r1b + r2b) + bo, 0.f);  // (1, 1)
+        }
+    }
+    __syncthreads();
+    PHASE(1);
     // ---- fc1 (16x16x4): [16 boards x 256] @ [256 x 64]; wave w: units 16w .. 16w+15.
-    //      Lane group g covers k' in [64g, 64g+64): A read 4 steps at a time, B in registers.
+    //      Lane group g covers k' in [64g, 64g+64): A and B read 4 steps at a time.
     {
         f32x4 c0 = f32x4{0}, c1 = f32x4{0};
         const int jc = wave * 16 + l16;
         const float* ap = h2 + l16 * H2S + 64 * g;
+        const float* bp = lds + OFF_WF1 + jc * WF1S + 64 * g;
 #pragma unroll
         for (int kk = 0; kk < 64; kk += 8) {
             const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
             const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
+            const f32x4 bv0 = *reinterpret_cast<const f32x4*>(bp + kk);
+            const f32x4 bv1 = *reinterpret_cast<const f32x4*>(bp + kk + 4);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], R.wf[kk + e], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], R.wf[kk + 4 + e], c1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv0[e], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv1[e], c1, 0, 0, 0);
             }
         }
         const float* sbf1 = lds + OFF_BF1;
@@ -440,6 +298,7 @@ __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R,
             fa[(4 * g + i) * FS + jc] = fmaxf((c0[i] + c1[i]) + sbf1[jc], 0.f);
     }
     __syncthreads();
+    PHASE(2);
     // ---- fc2: output o = t >> 2 (board o >> 2, action o & 3), part p = t & 3 sums 16 units
     {
         const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
@@ -458,6 +317,7 @@ __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R,
         if (p == 0) qs[o] = v + lds[OFF_BF2 + a];
     }
     __syncthreads();
+    PHASE(3);
 }
 
 // One board word (t < 64: word t&3 of board t>>2) -> 4 exponent floats in xs.
@@ -631,12 +491,8 @@ extern "C" G2048_API int g2048_convnet_forward(const g2048_convnet_params* p, co
     A.q = q_out;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t tiles16 = (n + persist::S - 1) / persist::S;
-    if (tiles16 >= 4 * 256) {  // >= 4 tiles per CU: stage weights once per workgroup
-        hipLaunchKernelGGL(k_conv_forward_persist, dim3(256), dim3(NT), 0, st, A);
-    } else {
-        const unsigned grid = (unsigned)((n + S - 1) / S);
-        hipLaunchKernelGGL(k_conv_forward, dim3(grid), dim3(NT), 0, st, A);
-    }
+    const unsigned grid = (unsigned)(tiles16 < 256 ? tiles16 : 256);  // one workgroup per CU
+    hipLaunchKernelGGL(k_conv_forward_persist, dim3(grid), dim3(NT), 0, st, A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_forward: %s", hipGetErrorString(e));

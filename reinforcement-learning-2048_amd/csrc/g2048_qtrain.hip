@@ -21,6 +21,7 @@
 // The weight matrix needed by each phase is staged into one 65 KB LDS region (padded strides).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "../../include/g2048.h"
 #include "g2048_common.hpp"
@@ -78,7 +79,7 @@ struct TrainArgs {
 };
 
 // conv1 pre-activation of board s (x in LDS) at output position (ph, pw), channel weights w/b
-__device__ __forceinline__ float conv1_pre(const float* x, int ph, int pw, float4 w, float b) {
+[[maybe_unused]] __device__ __forceinline__ float conv1_pre(const float* x, int ph, int pw, float4 w, float b) {
     float v = b;
     v = fmaf(w.x, x[ph * 4 + pw], v);
     v = fmaf(w.y, x[ph * 4 + pw + 1], v);
@@ -563,13 +564,27 @@ __device__ __forceinline__ int slab_to_param(int pos) {
     return P_BF2 + p3 - 704;
 }
 
+// Optional Adam folded into the reduction (single process): each final gradient element is
+// applied by its own thread with the shared adam_apply (bitwise k_adam on the same sums), and
+// the target net is synced on the device counter like g2048_adam_step_sync.
+struct ReduceAdam {
+    float* p[8];   // parameters in torch order (w1, b1, w2, b2, fc1_w, fc1_b, fc2_w, fc2_b)
+    float* tp[8];  // target-net parameters (nullable unless sync_every)
+    float* m;
+    float* v;
+    const unsigned long long* step;  // t (already bumped by k_conv_train)
+    double lr, b1, b2, eps;
+    unsigned long long sync_every;
+    int on;
+};
+
 // Deterministic slab reduction: a block owns 64 slab positions; its 16 waves sum the slabs
 // g = wave, wave + 16, ... (<= 16 independent loads per lane, all issued at once: one memory
 // round trip for the ~34 MB instead of 8), then the 16 partials are added in a fixed order.
 constexpr int RW = 16;  // waves per reduction block
 
 __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int nslab,
-                                                          float* grad, float* loss) {
+                                                          float* grad, float* loss, ReduceAdam R) {
     __shared__ float part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
@@ -591,7 +606,21 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         if (pos == SL_LOSS) {
             if (loss) *loss = s;
         } else {
-            grad[slab_to_param(pos)] = s;
+            const int pi = slab_to_param(pos);
+            if (grad) grad[pi] = s;
+            if (R.on) {
+                constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
+                int k = 0;
+#pragma unroll
+                for (int j = 1; j < 8; ++j) k += pi >= off[j] ? 1 : 0;
+                const int e = pi - off[k];
+                const unsigned long long t = *R.step;
+                const g2048::AdamCoef c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
+                float* pp = R.p[k] + e;
+                const float np = g2048::adam_apply(c, s, R.m + pi, R.v + pi, *pp);
+                *pp = np;
+                if (R.sync_every && t % R.sync_every == 0ull) R.tp[k][e] = np;
+            }
         }
     }
 }
@@ -604,14 +633,10 @@ extern "C" G2048_API int64_t g2048_convnet_train_workspace(int64_t batch) {
     return g * SLAB;
 }
 
-extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
-                                                  const uint8_t* rows, const uint8_t* actions,
-                                                  const int64_t* idx, const float* y, int64_t batch,
-                                                  float* workspace, float* grad_out,
-                                                  float* loss_out, uint64_t* step_dev,
-                                                  void* stream) {
-    if (!p || !rows || !actions || !idx || !y || !workspace || !grad_out || batch <= 0)
-        return g2048_fail(G2048_EINVAL, "convnet_train_grad: NULL argument or batch <= 0");
+static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
+                        const uint8_t* actions, const int64_t* idx, const float* y, int64_t batch,
+                        float* workspace, float* grad_out, float* loss_out, uint64_t* step_dev,
+                        const ReduceAdam& R, void* stream) {
     TrainArgs A;
     A.w1 = p->w1;
     A.b1 = p->b1;
@@ -635,8 +660,59 @@ extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train: %s", hipGetErrorString(e));
     hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, st,
-                       workspace, grid, grad_out, loss_out);
+                       workspace, grid, grad_out, loss_out, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "k_reduce_slabs: %s", hipGetErrorString(e));
+}
+
+static bool ok_params(const g2048_convnet_params* p) {
+    return p && p->w1 && p->b1 && p->w2 && p->b2 && p->fc1_w && p->fc1_b && p->fc2_w && p->fc2_b;
+}
+
+extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
+                                                  const uint8_t* rows, const uint8_t* actions,
+                                                  const int64_t* idx, const float* y, int64_t batch,
+                                                  float* workspace, float* grad_out,
+                                                  float* loss_out, uint64_t* step_dev,
+                                                  void* stream) {
+    if (!ok_params(p) || !rows || !actions || !idx || !y || !workspace || !grad_out || batch <= 0)
+        return g2048_fail(G2048_EINVAL, "convnet_train_grad: NULL argument or batch <= 0");
+    ReduceAdam R;
+    memset(&R, 0, sizeof(R));
+    return train_launch(p, rows, actions, idx, y, batch, workspace, grad_out, loss_out, step_dev,
+                        R, stream);
+}
+
+extern "C" G2048_API int g2048_convnet_train_adam(
+    const g2048_convnet_params* p, const uint8_t* rows, const uint8_t* actions,
+    const int64_t* idx, const float* y, int64_t batch, float* workspace, float* grad_out,
+    float* loss_out, uint64_t* step_dev, float* exp_avg, float* exp_avg_sq, double lr,
+    double beta1, double beta2, double eps, const g2048_convnet_params* target,
+    uint64_t sync_every, void* stream) {
+    if (!ok_params(p) || !rows || !actions || !idx || !y || !workspace || !step_dev || !exp_avg ||
+        !exp_avg_sq || batch <= 0)
+        return g2048_fail(G2048_EINVAL, "convnet_train_adam: NULL argument or batch <= 0");
+    if (sync_every && !ok_params(target))
+        return g2048_fail(G2048_EINVAL, "convnet_train_adam: sync_every > 0 needs the target net");
+    ReduceAdam R;
+    memset(&R, 0, sizeof(R));
+    const g2048_convnet_params* nets[2] = {p, sync_every ? target : nullptr};
+    for (int h = 0; h < 2; ++h) {
+        if (!nets[h]) continue;
+        const float* ps[8] = {nets[h]->w1, nets[h]->b1, nets[h]->w2, nets[h]->b2,
+                              nets[h]->fc1_w, nets[h]->fc1_b, nets[h]->fc2_w, nets[h]->fc2_b};
+        for (int k = 0; k < 8; ++k) (h ? R.tp : R.p)[k] = const_cast<float*>(ps[k]);
+    }
+    R.m = exp_avg;
+    R.v = exp_avg_sq;
+    R.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    R.lr = lr;
+    R.b1 = beta1;
+    R.b2 = beta2;
+    R.eps = eps;
+    R.sync_every = sync_every;
+    R.on = 1;
+    return train_launch(p, rows, actions, idx, y, batch, workspace, grad_out, loss_out, step_dev,
+                        R, stream);
 }

@@ -51,6 +51,8 @@ SIGNATURES = {
     "g2048_convnet_forward": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "g2048_convnet_train_workspace": (_i64, [_i64]),
     "g2048_convnet_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "g2048_convnet_train_adam": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _dbl, _dbl, _dbl, _dbl, _vp, _u64, _vp]),
     "g2048_convnet_targets": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
                                      _vp, _vp]),
     "g2048_adam_step": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _vp]),

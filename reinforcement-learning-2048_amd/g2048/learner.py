@@ -72,7 +72,6 @@ class DQNLearner:
             # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip); targets (sampler,
             # both target-side forwards, Bellman) as one launch; Adam as one launch.  The device
             # update counter is the sampler epoch and Adam's t (bumped by the train launch).
-            self._train_grad = qnet.TrainGrad(self.model, self.B)
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
@@ -81,6 +80,11 @@ class DQNLearner:
             # the device update counter: no host decision between graph replays
             if self.target_sync_every:
                 self._adam.attach_target(list(self.target.parameters()), self.target_sync_every)
+            # conv, single process: Adam (+ target sync) folded into the gradient reduction --
+            # targets, train, reduce+Adam = 3 launches per update
+            self._fold_adam = self.kind == "conv" and self.world == 1
+            self._train_grad = qnet.TrainGrad(self.model, self.B,
+                                              adam=self._adam if self._fold_adam else None)
             # dense64: sampler + targets + gradient in ONE launch, and (single process) Adam
             # folded into the gradient reduction -- 2 launches per update
             self._upd = (qnet.Dense64Update(self.model, self.target, self.B,
@@ -130,6 +134,8 @@ class DQNLearner:
     def _apply(self):
         if self._upd is not None and self._upd.adam is not None:
             return  # applied inside the dense64 update's reduction
+        if self.fused and self._fold_adam:
+            return  # applied inside the conv gradient reduction
         if self.fused:
             self._adam.step(self.grad_flat, self.step_dev)
         else:

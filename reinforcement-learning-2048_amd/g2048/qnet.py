@@ -95,29 +95,55 @@ conv_forward = forward
 class TrainGrad:
     """Graded half of train_step for a fused net: writes the loss and the gradient of
     sum_b (Q(s_b)[a_b] - y_b)^2 into a flat fp32 buffer laid out like
-    torch.cat([p.reshape(-1) for p in model.parameters()])."""
+    torch.cat([p.reshape(-1) for p in model.parameters()]).  For the conv net an `adam`
+    (FusedAdam over model.parameters()) folds optimizer.step() -- and its attached target sync --
+    into the gradient reduction (g2048_convnet_train_adam; single process only: the gradient is
+    final there, with no all-reduce in between)."""
 
-    def __init__(self, model, batch: int):
+    def __init__(self, model, batch: int, adam=None):
         self.kind = kind_of(model)
         self.params = net_params(model)
         self.batch = int(batch)
         self.n_params = sum(p.numel() for p in model.parameters())
+        if adam is not None and self.kind != "conv":
+            raise TypeError("the Adam-folded reduction exists for the conv net only")
+        self.adam = adam
+        self._tparams = None
+        if adam is not None and adam.sync_every:
+            tps = list(adam._target)  # model.parameters() order == the struct's field order
+            if len(tps) != 8:
+                raise ValueError("the attached target must be the conv net's 8 tensors")
+            self._tparams = N.ConvNetParams(*[t.data_ptr() for t in tps])
         dev = next(model.parameters()).device
         n = _sym(self.kind, "train_workspace")(self.batch)
         self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
 
     def __call__(self, rows: torch.Tensor, actions: torch.Tensor, idx: torch.Tensor,
-                 y: torch.Tensor, grad_out: torch.Tensor, loss_out: torch.Tensor | None = None,
+                 y: torch.Tensor, grad_out: torch.Tensor | None, loss_out: torch.Tensor | None = None,
                  step: torch.Tensor | None = None):
         if idx.numel() != self.batch or y.numel() != self.batch:
             raise ValueError("idx / y must have `batch` elements")
-        if (y.dtype != torch.float32 or grad_out.dtype != torch.float32
-                or grad_out.numel() != self.n_params):
+        if y.dtype != torch.float32 or (grad_out is not None and (
+                grad_out.dtype != torch.float32 or grad_out.numel() != self.n_params)):
             raise ValueError(f"y and grad_out must be float32; grad_out has {self.n_params} elements")
-        N.check(_sym(self.kind, "train_grad")(
+        a = self.adam
+        if a is None:
+            if grad_out is None:
+                raise ValueError("without Adam state the gradient needs a grad_out buffer")
+            N.check(_sym(self.kind, "train_grad")(
+                C.byref(self.params), N.ptr(rows), N.ptr(actions), N.ptr(idx), N.ptr(y), self.batch,
+                N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(step),
+                N.stream_of(rows.device)), "fused train_grad")
+            return
+        if step is None:
+            raise ValueError("the Adam-folded update needs the device step counter")
+        tp = C.byref(self._tparams) if self._tparams is not None else None
+        N.check(N.load().g2048_convnet_train_adam(
             C.byref(self.params), N.ptr(rows), N.ptr(actions), N.ptr(idx), N.ptr(y), self.batch,
             N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(step),
-            N.stream_of(rows.device)), "fused train_grad")
+            N.ptr(a.exp_avg), N.ptr(a.exp_avg_sq), a.lr, a.betas[0], a.betas[1], a.eps, tp,
+            int(a.sync_every) if self._tparams is not None else 0, N.stream_of(rows.device)),
+            "g2048_convnet_train_adam")
 
 
 ConvTrainGrad = TrainGrad

@@ -177,6 +177,50 @@ def test_fused_adam_matches_torch_adam(G):
         torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("sync_every", [0, 2])
+def test_conv_train_adam_equals_grad_then_adam(G, sync_every):
+    """g2048_convnet_train_adam (Adam + target sync folded into the gradient reduction) is
+    bitwise train_grad followed by g2048_adam_step_sync, over 3 updates."""
+    from g2048.nets import make_net
+    from g2048.optim import FusedAdam
+    from g2048.qnet import ConvTrainGrad
+
+    C, B = 16384, 2048
+    env = G.VecEnv2048(4096, device=DEV, seed=5)
+    rb = G.ReplayBuffer(C, device=DEV)
+    env.rollout(C // 4096, replay=rb)
+    torch.manual_seed(5)
+    nets = [make_net("conv", torch.float32, DEV) for _ in range(4)]
+    for m in nets[1:]:
+        m.load_state_dict(nets[0].state_dict())
+    (m1, t1), (m2, t2) = (nets[0], nets[1]), (nets[2], nets[3])
+    a1, a2 = FusedAdam(list(m1.parameters()), lr=1e-2), FusedAdam(list(m2.parameters()), lr=1e-2)
+    if sync_every:
+        a1.attach_target(list(t1.parameters()), sync_every)
+        a2.attach_target(list(t2.parameters()), sync_every)
+    tg1, tg2 = ConvTrainGrad(m1, B), ConvTrainGrad(m2, B, adam=a2)
+    s1 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    s2 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    g1 = torch.zeros(33476, device=DEV)
+    g2 = torch.zeros(33476, device=DEV)
+    l1, l2 = torch.zeros((), device=DEV), torch.zeros((), device=DEV)
+    for it in range(3):
+        idx = torch.randint(0, C, (B,), device=DEV)
+        y = (torch.randn(B, device=DEV) * 20 + 30).float()
+        tg1(rb.s, rb.a, idx, y, g1, l1, s1)
+        a1.step(g1, s1)
+        tg2(rb.s, rb.a, idx, y, g2, l2, s2)
+        assert torch.equal(g1, g2) and torch.equal(l1, l2)
+    assert int(s1) == int(s2) == 3
+    for p1, p2 in zip(list(m1.parameters()) + list(t1.parameters()),
+                      list(m2.parameters()) + list(t2.parameters())):
+        assert torch.equal(p1, p2)
+    assert torch.equal(a1.exp_avg, a2.exp_avg) and torch.equal(a1.exp_avg_sq, a2.exp_avg_sq)
+    if sync_every:  # synced at t = 2, then the online net moved on at t = 3
+        assert not all(torch.equal(p, q) for p, q in zip(m2.parameters(), t2.parameters()))
+        assert not all(torch.equal(p, q) for p, q in zip(t2.parameters(), nets[0].parameters()))
+
+
 # ------------------------------------------------------------------ dense 16-64-4 (configs[2])
 def test_dense64_forward_and_targets(G):
     from g2048 import dqn_lib

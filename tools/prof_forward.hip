@@ -1,4 +1,5 @@
-// f32 MFMA / VALU calibration and k_conv_forward_persist timing, built only for kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip
+// f32 MFMA / VALU calibration and k_conv_forward_persist timing + per-phase ticks, built only for
+// kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip -o tools/prof_forward
 #define G2048_PHASE_PROF 1
 #include <cstdarg>
 #include <cstdio>
@@ -11,6 +12,7 @@ int g2048_fail(int code, const char* fmt, ...) {
     return code;
 }
 #include "../reinforcement-learning-2048_amd/csrc/g2048_qnet.hip"
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 extern "C" int g2048_replay_views(g2048_replay*, uint8_t**, uint8_t**, uint8_t**, int32_t**, uint8_t**,
                                   uint64_t**) {
@@ -138,5 +140,10 @@ int main(int argc, char** argv) {
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
     printf("n=%ld  %.2f us/launch\n", n, ms * 1e3 / 20);
+    unsigned long long ph[8];
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g2048_phase_ticks), sizeof(ph));
+    const double tiles = 25.0 * (double)((n + 15) / 16 + 255) / 256;  // per workgroup, 25 launches
+    const char* names[4] = {"conv1+V", "conv2+out", "fc1", "fc2"};
+    for (int k = 0; k < 4; ++k) printf("phase %-10s %8.0f ticks/tile\n", names[k], ph[k] / tiles);
     return 0;
 }
