@@ -16,12 +16,12 @@
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
 #include "g2048_common.hpp"
+#include "g2048_convnet.hpp"
 
 namespace {
 
-constexpr int NT = 256;  // threads per workgroup
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
+using g2048::cnet::NetW;
+using g2048::cnet::NT;
 
 struct ConvNetArgs {
     const float* w1;   // [64][1][2][2]
@@ -36,10 +36,6 @@ struct ConvNetArgs {
     const int64_t* idx;    // row of board b (nullptr: b)
     int64_t n;
     float* q;              // [n][4]
-};
-
-struct NetW {
-    const float *w1, *b1, *w2, *b2, *wf1, *bf1, *wf2, *bf2;
 };
 
 // Phase profiler (tools/prof_forward.hip builds with G2048_PHASE_PROF): thread 0 of workgroup 0
@@ -62,40 +58,14 @@ __device__ unsigned long long g2048_phase_ticks[8];
 
 // ---------------------------------------------------------------------------------------------
 // Persistent kernels (every conv forward, Double-DQN targets): a workgroup stages a net once
-// and then runs 16-board tiles.  conv2 runs in the Winograd domain F(2x2, 2x2):
-//
-//   Y = A^T [ sum_c (G g_oc G^T) .* (B^T d_c B) ] A,
-//   B^T = [[1,-1,0],[0,1,0],[0,-1,1]]   G = [[1,0],[1,1],[0,1]]   A^T = [[1,1,0],[0,1,1]]
-//
-// with d_c the 3x3 relu(conv1) map of input channel c and g_oc the 2x2 kernel.  The 2x2 output
-// of a 3x3 input then costs 9 products per (c, o) instead of 16: conv2 becomes nine
-// [16 boards x 64 c] @ [64 c x 64 o] GEMMs per tile (36 864 MAC per board instead of 65 536).
-// All coefficients are 0 / +-1, so the only extra rounding is a handful of adds per value
-// (measured: fp32 error 1.4x that of the direct sum, both ~1e-7 relative).
-//
-// On gfx950 a VALU op between f32 MFMAs is not hidden (tools/prof_forward.hip: +4 cycles per op,
-// ~12 when the ops form dependent chains), so the MFMA loops carry no VALU at all:
-//  * conv1 + the input transform run as their own phase: thread (channel c = t&63, board
-//    group t>>6) computes relu(conv1) at the 9 positions of its boards (independent fma
-//    chains) and writes V_xi = (B^T d B)_xi to V[xi][board][c] (row stride 68 floats);
-//  * conv2: wave w owns output channels 16w..16w+15.  Its B operands U_xi[c][o] (9 x 64 x 16
-//    values, 144 per lane) are computed from W2 when the net is staged and stay in VGPRs.
-//    Lane group g covers input channels 16g..16g+15, so a lane's A operands for one point xi
-//    are 4 ds_read_b128 of V; per point 16 MFMAs 16x16x4, three point-chains interleaved;
-//  * the output transform (lane-local: a lane holds all 9 points of its 4 boards x 1 channel)
-//    + bias + ReLU writes h2[s][q*64 + o];
-//  * fc1: A = h2 and B = fc1_w[j][k'] (LDS, k' = q*64 + c' = torch's flat index permuted),
-//    both read along k as ds_read_b128;
-//  * fc2 uses all 256 threads and leaves Q[16][4] in LDS.
+// and then runs 16-board tiles through the blocks of g2048_convnet.hpp (conv1 + Winograd input
+// transform, conv2 as nine Winograd-domain GEMMs with U in VGPRs, fc1 with fc1_w in LDS), then
+// fc2 over all 256 threads.  On gfx950 a VALU op between f32 MFMAs is not hidden
+// (tools/prof_forward.hip: +4 cycles per op, ~12 when the ops form dependent chains), so the
+// MFMA loops carry no VALU at all.
 namespace persist {
-constexpr int S = 16;
+using namespace g2048::cnet;
 constexpr int TMAX = 8;    // tiles per workgroup in the targets kernel
-constexpr int VS = 68;     // floats per board row of V[xi][board][c] (64 used)
-constexpr int VXI = S * VS;  // floats per Winograd point
-constexpr int H2S = 260;   // h2[s][k'], k' = q*64 + n (fc1's input index permuted)
-constexpr int WF1S = 260;  // fc1_w[j][k']
-constexpr int FS = 68;     // fa[s][j] (16-byte aligned rows for fc2's b128 reads)
-constexpr int WF2S = 68;   // swf2[a][j]
 constexpr int OFF_X = 0;                          // [TMAX][S][16] boards (exponents as floats)
 constexpr int OFF_B2 = OFF_X + TMAX * S * 16;     // 64
 constexpr int OFF_BF1 = OFF_B2 + 64;              // 64
@@ -112,25 +82,13 @@ static_assert(OFF_WF1 % 4 == 0 && OFF_V % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4
               "b128 alignment");
 static_assert(FLOATS * 4 <= 156 * 1024, "LDS budget (persistent kernels, + the sample index)");
 
-struct Regs {  // per-thread weights held in registers
-    float4 w1c;     // conv1 weights of channel t & 63
-    float b1c;
-    float u[9][16];  // U_xi[c = 16g + kk][o = 16*wave + l16] = (G g_oc G^T)_xi
-};
-
-// Stage net W: U into registers, fc1_w + small tensors into LDS.  All global loads are issued
-// before the first LDS store (one memory round trip).  Starts and ends with __syncthreads().
+// Stage net W: U (forward layout) + conv1 into registers, fc1_w + small tensors into LDS.  All
+// global loads are issued before the first LDS store (one memory round trip).  Starts and ends
+// with __syncthreads().
 __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
-    const int o = 16 * wave + l16;
-    // w2[o][c][kh][kw] for c = 16g .. 16g+15: 64 contiguous floats
-    float4 wv[16];
-    const float4* src = reinterpret_cast<const float4*>(W.w2 + o * 256 + 64 * g);
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) wv[kk] = src[kk];
-    const int cc = t & 63;
-    R.w1c = make_float4(W.w1[4 * cc], W.w1[4 * cc + 1], W.w1[4 * cc + 2], W.w1[4 * cc + 3]);
-    R.b1c = W.b1[cc];
+    const int t = threadIdx.x;
+    load_u_fwd(W.w2, R);
+    load_conv1(W, R);
     const float b2 = t < 64 ? W.b2[t] : 0.f, bf1 = t < 64 ? W.bf1[t] : 0.f;
     const float wf2 = W.wf2[t], bf2 = t < 4 ? W.bf2[t] : 0.f;
     float f[64];  // fc1_w[i][t], i = 0..63
@@ -143,160 +101,23 @@ __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     }
     lds[OFF_WF2 + (t >> 6) * WF2S + (t & 63)] = wf2;
     if (t < 4) lds[OFF_BF2 + t] = bf2;
-    // fc1_w[j][k], k = c'*4 + q (torch Flatten order) -> fc1_w[j][k' = q*64 + c']
-    float* wf1s = lds + OFF_WF1 + (t & 3) * 64 + (t >> 2);
-#pragma unroll
-    for (int i = 0; i < 64; ++i) wf1s[i * WF1S] = f[i];
-    // G g G^T with g = [[a, b], [c, d]] (rows kh, columns kw):
-    //   [[a, a+b, b], [a+c, (a+c)+(b+d), b+d], [c, c+d, d]]
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-        const float a = wv[kk].x, b = wv[kk].y, c = wv[kk].z, d = wv[kk].w;
-        const float ac = a + c, bd = b + d;
-        R.u[0][kk] = a;
-        R.u[1][kk] = a + b;
-        R.u[2][kk] = b;
-        R.u[3][kk] = ac;
-        R.u[4][kk] = ac + bd;
-        R.u[5][kk] = bd;
-        R.u[6][kk] = c;
-        R.u[7][kk] = c + d;
-        R.u[8][kk] = d;
-    }
+    store_fc1(f, lds + OFF_WF1);
     __syncthreads();
 }
 
 // Q[16][4] of the 16 boards in xs (exponents as floats, visible to all threads) -> qs (LDS).
 // Ends with __syncthreads() (qs visible; V / h2 / fa free for the next tile).
 __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R, float* qs) {
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
-    float* h2 = lds + OFF_H2;
+    const int t = threadIdx.x;
     float* fa = lds + OFF_F;
     PHASE_BEGIN();
-    // ---- conv1 + ReLU + input transform -> V: channel cc of boards 4*wave .. 4*wave+3, two
-    //      boards (32 cells, 18 independent fma chains) at a time
-    {
-        const int cc = t & 63;
-        const float wt[4] = {R.w1c.x, R.w1c.y, R.w1c.z, R.w1c.w};
-        float* vdst = lds + OFF_V + cc;
-#pragma unroll
-        for (int bp = 0; bp < 2; ++bp) {
-            float x[2][16];
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float4 v =
-                        *reinterpret_cast<const float4*>(xs + (4 * wave + 2 * bp + bb) * 16 + 4 * r);
-                    x[bb][4 * r] = v.x;
-                    x[bb][4 * r + 1] = v.y;
-                    x[bb][4 * r + 2] = v.z;
-                    x[bb][4 * r + 3] = v.w;
-                }
-            float h[2][9];
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-                for (int p = 0; p < 9; ++p) h[bb][p] = R.b1c;
-#pragma unroll
-            for (int tap = 0; tap < 4; ++tap)
-#pragma unroll
-                for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-                    for (int p = 0; p < 9; ++p) {
-                        const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
-                        h[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], h[bb][p]);
-                    }
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb) {
-                float d[9];
-#pragma unroll
-                for (int p = 0; p < 9; ++p) d[p] = fmaxf(h[bb][p], 0.f);
-                float r[3][3];  // B^T d: rows (d0 - d1, d1, d2 - d1)
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    r[0][j] = d[j] - d[3 + j];
-                    r[1][j] = d[3 + j];
-                    r[2][j] = d[6 + j] - d[3 + j];
-                }
-                float* vb = vdst + (4 * wave + 2 * bp + bb) * VS;
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {  // (B^T d) B: the same on columns
-                    vb[(3 * i + 0) * VXI] = r[i][0] - r[i][1];
-                    vb[(3 * i + 1) * VXI] = r[i][1];
-                    vb[(3 * i + 2) * VXI] = r[i][2] - r[i][1];
-                }
-            }
-        }
-    }
+    conv1_v(xs, lds + OFF_V, R);
     __syncthreads();
     PHASE(0);
-    // ---- conv2 in the Winograd domain: M_xi[s][o] = sum_c V_xi[s][c] U_xi[c][o], 9 x 16 MFMAs
-    //      per wave, then Y = A^T M A + bias, ReLU -> h2
-    {
-        f32x4 acc[9];
-#pragma unroll
-        for (int xi = 0; xi < 9; ++xi) acc[xi] = f32x4{0, 0, 0, 0};
-        const float* vsrc = lds + OFF_V + l16 * VS + 16 * g;
-#pragma unroll
-        for (int grp = 0; grp < 3; ++grp) {
-            f32x4 av[3][4];
-#pragma unroll
-            for (int e = 0; e < 3; ++e)
-#pragma unroll
-                for (int q4 = 0; q4 < 4; ++q4)
-                    av[e][q4] = *reinterpret_cast<const f32x4*>(vsrc + (3 * grp + e) * VXI + 4 * q4);
-#pragma unroll
-            for (int kk = 0; kk < 16; ++kk)
-#pragma unroll
-                for (int e = 0; e < 3; ++e)
-                    acc[3 * grp + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                        av[e][kk >> 2][kk & 3], R.u[3 * grp + e][kk], acc[3 * grp + e], 0, 0, 0);
-        }
-        // C: row 4g + i -> board 4g + i; col -> o = 16*wave + l16
-        const int o = 16 * wave + l16;
-        const float bo = lds[OFF_B2 + o];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            float m[9];
-#pragma unroll
-            for (int xi = 0; xi < 9; ++xi) m[xi] = acc[xi][i];
-            const float r0a = m[0] + m[1], r0b = m[1] + m[2];
-            const float r1a = m[3] + m[4], r1b = m[4] + m[5];
-            const float r2a = m[6] + m[7], r2b = m[7] + m[8];
-            float* hrow = h2 + (4 * g + i) * H2S + o;
-            hrow[0] = fmaxf((r0a + r1a) + bo, 0.f);    // (qh, qw) = (0, 0)
-            hrow[64] = fmaxf((r0b + r1b) + bo, 0.f);   // (0, 1)
-            hrow[128] = fmaxf((r1a + r2a) + bo, 0.f);  // (1, 0)
-            hrow[192] = fmaxf((r1b + r2b) + bo, 0.f);  // (1, 1)
-        }
-    }
+    conv2_h2(lds + OFF_V, lds + OFF_H2, lds + OFF_B2, R);
     __syncthreads();
     PHASE(1);
-    // ---- fc1 (16x16x4): [16 boards x 256] @ [256 x 64]; wave w: units 16w .. 16w+15.
-    //      Lane group g covers k' in [64g, 64g+64): A and B read 4 steps at a time.
-    {
-        f32x4 c0 = f32x4{0}, c1 = f32x4{0};
-        const int jc = wave * 16 + l16;
-        const float* ap = h2 + l16 * H2S + 64 * g;
-        const float* bp = lds + OFF_WF1 + jc * WF1S + 64 * g;
-#pragma unroll
-        for (int kk = 0; kk < 64; kk += 8) {
-            const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
-            const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
-            const f32x4 bv0 = *reinterpret_cast<const f32x4*>(bp + kk);
-            const f32x4 bv1 = *reinterpret_cast<const f32x4*>(bp + kk + 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv0[e], c0, 0, 0, 0);
-                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[e], bv1[e], c1, 0, 0, 0);
-            }
-        }
-        const float* sbf1 = lds + OFF_BF1;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            fa[(4 * g + i) * FS + jc] = fmaxf((c0[i] + c1[i]) + sbf1[jc], 0.f);
-    }
+    fc1_f(lds + OFF_H2, lds + OFF_WF1, lds + OFF_BF1, fa);
     __syncthreads();
     PHASE(2);
     // ---- fc2: output o = t >> 2 (board o >> 2, action o & 3), part p = t & 3 sums 16 units
@@ -318,15 +139,6 @@ __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R,
     }
     __syncthreads();
     PHASE(3);
-}
-
-// One board word (t < 64: word t&3 of board t>>2) -> 4 exponent floats in xs.
-__device__ __forceinline__ void put_word(float* xs, int t, uint32_t v) {
-    float* dst = xs + (t >> 2) * 16 + (t & 3) * 4;
-    dst[0] = (float)(v & 0xFFu);
-    dst[1] = (float)((v >> 8) & 0xFFu);
-    dst[2] = (float)((v >> 16) & 0xFFu);
-    dst[3] = (float)(v >> 24);
 }
 }  // namespace persist
 

@@ -1,5 +1,6 @@
-// Phase timing of k_conv_train (s_memtime deltas of block 0 per wave; each delta is charged to
-// the phase that ENDS at the marker), built only for kernel tuning:
+// Per-kernel event timing of the conv train launches and phase ticks of k_conv_train_fwd
+// (s_memtime deltas of thread 0 of block 0, charged to the phase that ENDS at the marker),
+// built only for kernel tuning:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_train.hip -o tools/prof_train
 #define G2048_PHASE_PROF 1
 #include <cstdarg>
@@ -44,28 +45,54 @@ int main() {
     const int64_t nws = g2048_convnet_train_workspace(B);
     (void)hipMalloc(&ws, nws * 4);
     g2048_convnet_params p{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
-    hipEvent_t a, b;
-    (void)hipEventCreate(&a);
-    (void)hipEventCreate(&b);
     for (int it = 0; it < 3; ++it)
         g2048_convnet_train_grad(&p, rows, acts, idx, y, B, ws, grad, loss, nullptr, nullptr);
-    (void)hipEventRecord(a, nullptr);
-    for (int it = 0; it < 20; ++it)
-        g2048_convnet_train_grad(&p, rows, acts, idx, y, B, ws, grad, loss, nullptr, nullptr);
-    (void)hipEventRecord(b, nullptr);
-    (void)hipEventSynchronize(b);
-    float ms;
-    (void)hipEventElapsedTime(&ms, a, b);
-    unsigned long long ph[4][16];
-    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_tphase), sizeof(ph));
-    printf("B=%d  train+reduce %.2f us/launch\n", B, ms * 1e3 / 20);
-    const char* names[13] = {"start", "A stage", "B conv2 fwd", "C Wf1t", "D fc1 fwd", "E loss",
-                             "F dWf2+Wf1r", "G df", "H dWf1+dh2", "I dh2+W2r", "J dW2",
-                             "K dP+dW1", "slab"};
-    for (int k = 0; k < 13; ++k) {
-        printf("%-12s", names[k]);
-        for (int wv = 0; wv < 4; ++wv) printf(" %8llu", ph[wv][k]);
-        printf("\n");
+    (void)hipDeviceSynchronize();
+    unsigned long long zero[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tphase), zero, sizeof(zero));
+    TrainArgs A;
+    A.W = NetW{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
+    A.rows = rows;
+    A.actions = acts;
+    A.idx = idx;
+    A.y = y;
+    A.batch = B;
+    A.slab = ws;
+    const int grid = (int)train_grid(B);
+    A.dm = ws + (int64_t)grid * SLAB;
+    A.step = nullptr;
+    ReduceAdam R;
+    memset(&R, 0, sizeof(R));
+    hipEvent_t ev[4];
+    for (int i = 0; i < 4; ++i) (void)hipEventCreate(&ev[i]);
+    float tk[3] = {0, 0, 0};
+    const int N = 20;
+    for (int it = 0; it < N; ++it) {
+        (void)hipEventRecord(ev[0], nullptr);
+        hipLaunchKernelGGL(k_conv_train_fwd, dim3(grid), dim3(NT), 0, nullptr, A);
+        (void)hipEventRecord(ev[1], nullptr);
+        hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, nullptr, A);
+        (void)hipEventRecord(ev[2], nullptr);
+        hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, nullptr,
+                           ws, grid, grad, loss, R);
+        (void)hipEventRecord(ev[3], nullptr);
+        (void)hipEventSynchronize(ev[3]);
+        for (int k = 0; k < 3; ++k) {
+            float ms;
+            (void)hipEventElapsedTime(&ms, ev[k], ev[k + 1]);
+            tk[k] += ms * 1e3f / N;
+        }
     }
+    printf("B=%d grid=%d  fwd %.2f us  bwd %.2f us  reduce %.2f us\n", B, grid, tk[0], tk[1], tk[2]);
+    unsigned long long ph[16];
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_tphase), sizeof(ph));
+    const char* names[8] = {"stage", "conv1+V", "conv2", "fc1", "loss+df", "dWf1+dY", "dM+dU+st", "slab"};
+    const double tiles = (double)N * ((B / 16 + grid - 1) / grid);
+    for (int k = 0; k < 8; ++k)
+        printf("%-10s %9.0f ticks/%s\n", names[k], ph[k] / (k == 0 || k == 7 ? N : tiles),
+               k == 0 || k == 7 ? "launch" : "tile");
+    const char* n2[4] = {"bwd stage", "bwd dM ld", "bwd dV", "bwd epi"};
+    for (int k = 8; k < 12; ++k)
+        printf("%-10s %9.0f ticks/%s\n", n2[k - 8], ph[k] / (k == 8 ? N : tiles), k == 8 ? "launch" : "tile");
     return 0;
 }
