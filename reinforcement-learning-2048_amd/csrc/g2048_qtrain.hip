@@ -415,6 +415,24 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
     const int64_t ntiles = (A.batch + S - 1) / S;
     const int T = tiles_here(ntiles);
+    // dM of tiles k and k + 1 -> the two LDS buffers [xi][b][VS] in one memory round trip
+    // (coalesced float4: 9 per thread per tile)
+    auto copy_pair = [&](int k) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (k + h >= T) break;
+            const float4* src = reinterpret_cast<const float4*>(
+                A.dm + (blockIdx.x + (int64_t)(k + h) * gridDim.x) * DM_TILE);
+            float* dst = lds + K2_DM + h * 9 * VXI;
+#pragma unroll
+            for (int r = 0; r < 9; ++r) {
+                const int f4 = r * NT + t;
+                *reinterpret_cast<float4*>(dst + (f4 >> 4) * VS + (f4 & 15) * 4) = src[f4];
+            }
+        }
+    };
+    // the first pair, the boards and the weights share one memory round trip
+    copy_pair(0);
     uint32_t bw[TMAXT];
 #pragma unroll
     for (int k = 0; k < TMAXT; ++k)
@@ -429,27 +447,15 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     for (int k = 0; k < TMAXT; ++k)
         if (k < T && t < S * 4) put_word(lds + K2_X + k * S * 16, t, bw[k]);
     float gw[4] = {0.f, 0.f, 0.f, 0.f}, gb = 0.f;
+    lds_barrier();
     TPHASE_BEGIN();
     TPHASE(8);
     for (int k = 0; k < T; ++k) {
         float* dms = lds + K2_DM + (k & 1) * 9 * VXI;
-        if ((k & 1) == 0) {
-            // ---- dM of tiles k and k + 1 -> the two LDS buffers [xi][b][VS] in one memory
-            //      round trip (coalesced float4: 9 per thread per tile)
-            if (k > 0) lds_barrier();  // the previous pair's reads are done
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (k + h >= T) break;
-                const float4* src = reinterpret_cast<const float4*>(
-                    A.dm + (blockIdx.x + (int64_t)(k + h) * gridDim.x) * DM_TILE);
-                float* dst = lds + K2_DM + h * 9 * VXI;
-#pragma unroll
-                for (int r = 0; r < 9; ++r) {
-                    const int f4 = r * NT + t;
-                    *reinterpret_cast<float4*>(dst + (f4 >> 4) * VS + (f4 & 15) * 4) = src[f4];
-                }
-            }
-            lds_barrier();  // (k = 0: the boards too)
+        if ((k & 1) == 0 && k > 0) {
+            lds_barrier();  // the previous pair's reads are done
+            copy_pair(k);
+            lds_barrier();
         }
         TPHASE(9);
         // ---- dV_xi = dM_xi U_xi^T  (m = board l16, k = o = 16g + kk, n = c): groups of three
