@@ -44,8 +44,8 @@ struct NetW {
 };
 
 struct Regs {       // per-thread weights held in registers
-    float4 w1c;     // conv1 weights of channel t & 63
-    float b1c;
+    float w1t;      // conv1 weight w1[c = 16*wave + l16][tap = g] (conv1's MFMA B operand)
+    float b1o;      // conv1 bias b1[16*wave + l16]
     float u[9][16]; // Winograd-domain conv2 weights, layout chosen by the loader
 };
 
@@ -88,11 +88,12 @@ __device__ __forceinline__ void load_u_bwd(const float* w2, Regs& R) {
     for (int kk = 0; kk < 16; ++kk) winograd_u(wv[kk], R.u, kk);
 }
 
-// conv1 weights of channel t & 63 (the conv1 phase's thread -> channel map).
+// conv1 operands of this lane: channel 16*wave + l16, tap g (w1[c][0][kh][kw], tap = 2kh + kw).
 __device__ __forceinline__ void load_conv1(const NetW& W, Regs& R) {
-    const int cc = threadIdx.x & 63;
-    R.w1c = make_float4(W.w1[4 * cc], W.w1[4 * cc + 1], W.w1[4 * cc + 2], W.w1[4 * cc + 3]);
-    R.b1c = W.b1[cc];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c = 16 * wave + (lane & 15);
+    R.w1t = W.w1[4 * c + (lane >> 4)];
+    R.b1o = W.b1[c];
 }
 
 // fc1_w[j][k], k = c'*4 + q (torch Flatten order) -> wf1s[j][k' = q*64 + c'] (stride WF1S).
@@ -104,73 +105,44 @@ __device__ __forceinline__ void store_fc1(const float (&f)[64], float* wf1s) {
     for (int i = 0; i < 64; ++i) dst[i * WF1S] = f[i];
 }
 
-// conv1 pre-activation at position p (ph = p / 3, pw = p % 3) of a board x[16]: bias first,
-// then the taps in weight order -- the order every kernel here uses, so the forward's h1 and the
-// backward's relu' mask see the same float.
-__device__ __forceinline__ float conv1_pre(const float* x, int p, float4 w, float b) {
-    const int ph = p / 3, pw = p % 3;
-    float v = b;
-    v = fmaf(w.x, x[ph * 4 + pw], v);
-    v = fmaf(w.y, x[ph * 4 + pw + 1], v);
-    v = fmaf(w.z, x[(ph + 1) * 4 + pw], v);
-    v = fmaf(w.w, x[(ph + 1) * 4 + pw + 1], v);
-    return v;
+// ---- conv1 without bias as 9 MFMAs per wave (M = 16 boards, K = 4 taps, N = the wave's 16
+//      channels): pre[p][i] = sum_tap x[b = 4g + i][cell(p, tap)] * w1[16*wave + l16][tap].
+//      The forward (relu(pre + b1)) and the backward's relu' mask (pre + b1 > 0) both use this,
+//      so they see the same float.  xs: the tile's boards as floats [S][16].
+__device__ __forceinline__ void conv1_pre_mfma(const float* xs, float w1t, f32x4 (&pre)[9]) {
+    const int lane = threadIdx.x & 63, g = lane >> 4, l16 = lane & 15;
+    const float* xr = xs + l16 * 16 + (g >> 1) * 4 + (g & 1);  // A: board l16, tap g
+#pragma unroll
+    for (int p = 0; p < 9; ++p)
+        pre[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(xr[(p / 3) * 4 + p % 3], w1t,
+                                                      f32x4{0, 0, 0, 0}, 0, 0, 0);
 }
 
-// ---- conv1 + ReLU + input transform -> V[xi][b][c] (stride VS, point stride VXI): thread =
-//      channel t & 63 for boards 4*wave .. 4*wave+3, two boards (18 independent fma chains) at
-//      a time.  xs: the tile's boards as floats [S][16] (16-byte aligned rows).
+// ---- conv1 + ReLU + input transform -> V[xi][b][c] (stride VS, point stride VXI): lane
+//      (channel 16*wave + l16, boards 4g .. 4g+3) from conv1_pre_mfma's accumulators.
 __device__ __forceinline__ void conv1_v(const float* xs, float* V, const Regs& R) {
-    const int t = threadIdx.x, wave = t >> 6, cc = t & 63;
-    const float wt[4] = {R.w1c.x, R.w1c.y, R.w1c.z, R.w1c.w};
-    float* vdst = V + cc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+    f32x4 pre[9];
+    conv1_pre_mfma(xs, R.w1t, pre);
+    float* vdst = V + 4 * g * VS + 16 * wave + l16;
 #pragma unroll
-    for (int bp = 0; bp < 2; ++bp) {
-        float x[2][16];
+    for (int i = 0; i < 4; ++i) {
+        float d[9];
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
+        for (int p = 0; p < 9; ++p) d[p] = fmaxf(pre[p][i] + R.b1o, 0.f);
+        float r[3][3];  // B^T d: rows (d0 - d1, d1, d2 - d1)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float4 v =
-                    *reinterpret_cast<const float4*>(xs + (4 * wave + 2 * bp + bb) * 16 + 4 * r);
-                x[bb][4 * r] = v.x;
-                x[bb][4 * r + 1] = v.y;
-                x[bb][4 * r + 2] = v.z;
-                x[bb][4 * r + 3] = v.w;
-            }
-        float h[2][9];
+        for (int j = 0; j < 3; ++j) {
+            r[0][j] = d[j] - d[3 + j];
+            r[1][j] = d[3 + j];
+            r[2][j] = d[6 + j] - d[3 + j];
+        }
+        float* vb = vdst + i * VS;
 #pragma unroll
-        for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-            for (int p = 0; p < 9; ++p) h[bb][p] = R.b1c;
-#pragma unroll
-        for (int tap = 0; tap < 4; ++tap)
-#pragma unroll
-            for (int bb = 0; bb < 2; ++bb)
-#pragma unroll
-                for (int p = 0; p < 9; ++p) {
-                    const int pr = p / 3 + (tap >> 1), pc = p % 3 + (tap & 1);
-                    h[bb][p] = fmaf(wt[tap], x[bb][pr * 4 + pc], h[bb][p]);
-                }
-#pragma unroll
-        for (int bb = 0; bb < 2; ++bb) {
-            float d[9];
-#pragma unroll
-            for (int p = 0; p < 9; ++p) d[p] = fmaxf(h[bb][p], 0.f);
-            float r[3][3];  // B^T d: rows (d0 - d1, d1, d2 - d1)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                r[0][j] = d[j] - d[3 + j];
-                r[1][j] = d[3 + j];
-                r[2][j] = d[6 + j] - d[3 + j];
-            }
-            float* vb = vdst + (4 * wave + 2 * bp + bb) * VS;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {  // (B^T d) B: the same on columns
-                vb[(3 * i + 0) * VXI] = r[i][0] - r[i][1];
-                vb[(3 * i + 1) * VXI] = r[i][1];
-                vb[(3 * i + 2) * VXI] = r[i][2] - r[i][1];
-            }
+        for (int k = 0; k < 3; ++k) {  // (B^T d) B: the same on columns
+            vb[(3 * k + 0) * VXI] = r[k][0] - r[k][1];
+            vb[(3 * k + 1) * VXI] = r[k][1];
+            vb[(3 * k + 2) * VXI] = r[k][2] - r[k][1];
         }
     }
 }

@@ -412,7 +412,7 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
 
 __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     __shared__ __attribute__((aligned(16))) float lds[K2_FLOATS];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
+    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, l16 = lane & 15;
     const int64_t ntiles = (A.batch + S - 1) / S;
     const int T = tiles_here(ntiles);
     // dM of tiles k and k + 1 -> the two LDS buffers [xi][b][VS] in one memory round trip
@@ -439,10 +439,7 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
         bw[k] = k < T ? board_word(A, (blockIdx.x + (int64_t)k * gridDim.x) * S, t) : 0u;
     Regs R;
     load_u_bwd(A.W.w2, R);  // u[xi][kk] = U_xi[c = 16*wave + l16][o = 16g + kk]
-    const int c = 16 * wave + l16;
-    const float4 w1c = make_float4(A.W.w1[4 * c], A.W.w1[4 * c + 1], A.W.w1[4 * c + 2],
-                                   A.W.w1[4 * c + 3]);
-    const float b1c = A.W.b1[c];
+    load_conv1(A.W, R);  // channel c = 16*wave + l16: the lane's dV column
 #pragma unroll
     for (int k = 0; k < TMAXT; ++k)
         if (k < T && t < S * 4) put_word(lds + K2_X + k * S * 16, t, bw[k]);
@@ -483,6 +480,8 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
         TPHASE(10);
         // ---- dh1 = B dV B^T, relu'(h1), dW1 / db1 for (board 4g + i, channel c)
         const float* xs = lds + K2_X + k * S * 16;
+        f32x4 pre[9];
+        conv1_pre_mfma(xs, R.w1t, pre);  // the forward's pre-activations, bitwise
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             float x[16];
@@ -506,8 +505,7 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
                 const float dd[3] = {rr[ph][0], (rr[ph][1] - rr[ph][0]) - rr[ph][2], rr[ph][2]};
 #pragma unroll
                 for (int pw = 0; pw < 3; ++pw) {
-                    const float pre = conv1_pre(x, 3 * ph + pw, w1c, b1c);
-                    const float gh = pre > 0.f ? dd[pw] : 0.f;
+                    const float gh = pre[3 * ph + pw][i] + R.b1o > 0.f ? dd[pw] : 0.f;
                     gb += gh;
                     gw[0] = fmaf(gh, x[ph * 4 + pw], gw[0]);
                     gw[1] = fmaf(gh, x[ph * 4 + pw + 1], gw[1]);

@@ -13,6 +13,7 @@ int g2048_fail(int code, const char* fmt, ...) {
 }
 #include "../reinforcement-learning-2048_amd/csrc/g2048_qnet.hip"
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 extern "C" int g2048_replay_views(g2048_replay*, uint8_t**, uint8_t**, uint8_t**, int32_t**, uint8_t**,
                                   uint64_t**) {

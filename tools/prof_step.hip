@@ -7,9 +7,9 @@
 
 using namespace g2048;
 
-template <int STAGE>
-__global__ __launch_bounds__(256) void k_stage(uint4* board, uint4* meta, uint32_t* out) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+template <int STAGE, int BS = 256>
+__global__ __launch_bounds__(BS) void k_stage(uint4* board, uint4* meta, uint32_t* out) {
+    const int i = blockIdx.x * BS + threadIdx.x;
     Board b{board[i].x, board[i].y, board[i].z, board[i].w};
     uint4 m = meta[i];
     const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
@@ -79,5 +79,12 @@ int main() {
            per_launch_us([&] { hipLaunchKernelGGL(k_stage<S>, dim3(n / 256), dim3(256), 0, st, \
                                                   board, meta, out); }, st))
     RUN(0); RUN(1); RUN(2); RUN(3); RUN(4); RUN(5);
+    // the full stage with other workgroup sizes (same 64k lanes)
+    printf("stage 5, 64-thread blocks %.3f us\n",
+           per_launch_us([&] { hipLaunchKernelGGL((k_stage<5, 64>), dim3(n / 64), dim3(64), 0, st,
+                                                  board, meta, out); }, st));
+    printf("stage 5, 128-thread blocks %.3f us\n",
+           per_launch_us([&] { hipLaunchKernelGGL((k_stage<5, 128>), dim3(n / 128), dim3(128), 0, st,
+                                                  board, meta, out); }, st));
     return 0;
 }
