@@ -96,11 +96,16 @@ __device__ __forceinline__ void load_conv1(const NetW& W, Regs& R) {
     R.b1o = W.b1[c];
 }
 
-// fc1_w[j][k], k = c'*4 + q (torch Flatten order) -> wf1s[j][k' = q*64 + c'] (stride WF1S).
+// fc1_w[j][k], k = c'*4 + q (torch Flatten order) -> wf1s[j][wf1_col(k' = q*64 + c')] (row
+// stride WF1S).  The column swizzle (c' ^ 16q) puts the four q of one c' -- written by four
+// adjacent lanes -- in different banks; it keeps every aligned group of 4 columns together, so
+// the b128 reads along k' stay contiguous.
+__device__ __forceinline__ int wf1_col(int kp) { return kp ^ (16 * (kp >> 6)); }
+
 // f[64] = this thread's column t of fc1_w (loaded by the caller with the other staging loads).
 __device__ __forceinline__ void store_fc1(const float (&f)[64], float* wf1s) {
     const int t = threadIdx.x;
-    float* dst = wf1s + (t & 3) * 64 + (t >> 2);
+    float* dst = wf1s + wf1_col((t & 3) * 64 + (t >> 2));
 #pragma unroll
     for (int i = 0; i < 64; ++i) dst[i * WF1S] = f[i];
 }
@@ -200,13 +205,13 @@ __device__ __forceinline__ void fc1_f(const float* h2, const float* wf1s, const 
     f32x4 c0 = f32x4{0}, c1 = f32x4{0};
     const int jc = wave * 16 + l16;
     const float* ap = h2 + l16 * H2S + 64 * g;
-    const float* bp = wf1s + jc * WF1S + 64 * g;
+    const float* bp = wf1s + jc * WF1S;
 #pragma unroll
     for (int kk = 0; kk < 64; kk += 8) {
         const f32x4 av0 = *reinterpret_cast<const f32x4*>(ap + kk);
         const f32x4 av1 = *reinterpret_cast<const f32x4*>(ap + kk + 4);
-        const f32x4 bv0 = *reinterpret_cast<const f32x4*>(bp + kk);
-        const f32x4 bv1 = *reinterpret_cast<const f32x4*>(bp + kk + 4);
+        const f32x4 bv0 = *reinterpret_cast<const f32x4*>(bp + wf1_col(64 * g + kk));
+        const f32x4 bv1 = *reinterpret_cast<const f32x4*>(bp + wf1_col(64 * g + kk + 4));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[e], bv0[e], c0, 0, 0, 0);

@@ -87,6 +87,7 @@ static_assert(FLOATS * 4 <= 156 * 1024, "LDS budget (persistent kernels, + the s
 // with __syncthreads().
 __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     const int t = threadIdx.x;
+    PHASE_BEGIN();
     load_u_fwd(W.w2, R);
     load_conv1(W, R);
     const float b2 = t < 64 ? W.b2[t] : 0.f, bf1 = t < 64 ? W.bf1[t] : 0.f;
@@ -95,6 +96,7 @@ __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
 #pragma unroll
     for (int i = 0; i < 64; ++i) f[i] = W.wf1[i * NT + t];
     __syncthreads();  // previous users of the LDS weight areas are done
+    PHASE(4);
     if (t < 64) {
         lds[OFF_B2 + t] = b2;
         lds[OFF_BF1 + t] = bf1;
@@ -103,6 +105,7 @@ __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     if (t < 4) lds[OFF_BF2 + t] = bf2;
     store_fc1(f, lds + OFF_WF1);
     __syncthreads();
+    PHASE(5);
 }
 
 // Q[16][4] of the 16 boards in xs (exponents as floats, visible to all threads) -> qs (LDS).

@@ -295,9 +295,9 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
                 a4[buf] = *reinterpret_cast<const f32x4*>(df + l16 * FS + 16 * m4 + 4 * g);
 #pragma unroll
                 for (int e4 = 0; e4 < 4; ++e4) {
-                    const float* brow = wf1s + (16 * m4 + 4 * g + e4) * WF1S + o;
+                    const float* brow = wf1s + (16 * m4 + 4 * g + e4) * WF1S;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) bq[buf][e4][q] = brow[64 * q];
+                    for (int q = 0; q < 4; ++q) bq[buf][e4][q] = brow[wf1_col(64 * q + o)];
                 }
             };
             ld(0, 0);

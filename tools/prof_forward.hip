@@ -141,10 +141,59 @@ int main(int argc, char** argv) {
     float ms;
     (void)hipEventElapsedTime(&ms, a, b);
     printf("n=%ld  %.2f us/launch\n", n, ms * 1e3 / 20);
+
     unsigned long long ph[8];
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g2048_phase_ticks), sizeof(ph));
     const double tiles = 25.0 * (double)((n + 15) / 16 + 255) / 256;  // per workgroup, 25 launches
     const char* names[4] = {"conv1+V", "conv2+out", "fc1", "fc2"};
     for (int k = 0; k < 4; ++k) printf("phase %-10s %8.0f ticks/tile\n", names[k], ph[k] / tiles);
+    printf("stage: loads+U %8.0f  LDS %8.0f ticks/launch\n", ph[4] / 25.0, ph[5] / 25.0);
+    {  // targets kernel, B = 8192 over a 1M-row ring
+        const int B = 8192;
+        const long C = 1 << 20;
+        uint8_t *s2, *d;
+        int32_t* r;
+        unsigned long long *cnt, *ep;
+        int64_t* io;
+        float* yv;
+        (void)hipMalloc(&s2, C * 16);
+        (void)hipMalloc(&d, C);
+        (void)hipMalloc(&r, C * 4);
+        (void)hipMalloc(&cnt, 8);
+        (void)hipMalloc(&ep, 8);
+        (void)hipMalloc(&io, B * 8);
+        (void)hipMalloc(&yv, B * 4);
+        (void)hipMemset(d, 0, C);
+        (void)hipMemset(r, 0, C * 4);
+        (void)hipMemset(ep, 0, 8);
+        const unsigned long long hc = C;
+        (void)hipMemcpy(cnt, &hc, 8, hipMemcpyHostToDevice);
+        for (long i = 0; i < 16; ++i) (void)hipMemcpy(s2 + i * n * 16, rows, n * 16 > C * 16 - i * n * 16 ? 0 : n * 16, hipMemcpyDeviceToDevice);
+        TargetArgs T;
+        T.on = NetW{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
+        T.tg = T.on;
+        T.s2 = s2;
+        T.r = r;
+        T.d = d;
+        T.count = cnt;
+        T.epoch = ep;
+        T.idx_in = nullptr;
+        T.batch = B;
+        T.seed_lo = 1;
+        T.seed_hi = 2;
+        T.gamma = 0.8f;
+        T.double_dqn = 1;
+        T.idx_out = io;
+        T.y = yv;
+        for (int rep = 0; rep < 2; ++rep) {  // (the first pass warms up)
+            (void)hipEventRecord(a, nullptr);
+            for (int it = 0; it < 20; ++it)
+                hipLaunchKernelGGL(k_conv_targets_persist, dim3(256), dim3(NT), 0, nullptr, T);
+            (void)hipEventRecord(b, nullptr);
+            (void)hipEventSynchronize(b);
+            (void)hipEventElapsedTime(&ms, a, b);
+        }
+        printf("targets B=%d  %.2f us/launch\n", B, ms * 1e3 / 20);
+    }
     return 0;
 }
