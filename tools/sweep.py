@@ -43,16 +43,22 @@ def timed(fn, reps):
 
 def main():
     out = []
-    for n in [1024, 4096, 16384, 65536, 262144, 1 << 20, 1 << 22, 1 << 24]:
+    for n in [1024, 4096, 16384, 65536, 262144, 1 << 20, 1 << 22, 1 << 24, 1 << 26]:
         env = g2048.VecEnv2048(n, seed=1, device="cuda:0")
         r = torch.empty(n, dtype=torch.int32, device="cuda:0")
         d = torch.empty(n, dtype=torch.uint8, device="cuda:0")
         lg = torch.empty(n, dtype=torch.uint8, device="cuda:0")
-        K = 50
+        K = 50 if n <= (1 << 22) else 10
         g = graph_of(lambda: env.step(None, reward=r, done=d, legal=lg), K)
         t = timed(g.replay, 4) / K
         row = {"boards": n, "step_us": t * 1e6, "steps_per_s": n / t,
                "step_GBs": STEP_BYTES * n / t / 1e9}
+        if n >= (1 << 20):  # a plain device copy of the board + meta bytes (read + write 64 B)
+            src = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+            dst = torch.empty_like(src)
+            tc = timed(lambda: dst.copy_(src), 10)
+            row["copy_GBs"] = 64 * n / tc / 1e9
+            del src, dst
         if n <= (1 << 22):
             kk = 16
             rb = g2048.ReplayBuffer(n * kk, device="cuda:0")
