@@ -94,6 +94,42 @@ def test_row_lut_all_directions(g2048, golden_dir, action):
     assert env.error_count() == 0
 
 
+@pytest.mark.parametrize("action", [0, 1, 2, 3])
+def test_high_exponent_rows_vs_oracle(g2048, action):
+    """Rows over exponents {0, 1, 14, 15, 16, 17} (tiles up to 131072, the largest a 4x4 game
+    reaches; the reference LUT stops at 2^15) through every direction: board, merge score
+    (a 65536 + 65536 merge scores 131072) and legal bit equal the oracle's
+    src/board.py:92-126 restatement.  Parity beyond 2^15 rests on the oracle's value arithmetic."""
+    from oracle import oracle as O
+    exps = [0, 1, 14, 15, 16, 17]
+    rows = np.array(list(itertools.product(exps, repeat=4)), dtype=np.uint8)
+    n = len(rows)
+    boards = np.zeros((n, 4, 4), np.uint8)
+    if action == 2:
+        boards[:, 0, :] = rows
+    elif action == 3:
+        boards[:, 0, :] = rows[:, ::-1]
+    elif action == 0:
+        boards[:, :, 0] = rows
+    else:
+        boards[:, :, 0] = rows[:, ::-1]
+    ref = [O.slide_row(r) for r in rows]
+    ref_rows = np.array([x[0] for x in ref], np.uint8)
+    ref_score = np.array([x[1] for x in ref], np.int64)
+    changed = ~np.all(ref_rows == rows, axis=1)
+    env = _env_with(g2048, boards.reshape(n, 16))
+    r, d, lg = env.step_inject(torch.full((n,), action, dtype=torch.uint8),
+                               torch.full((n,), 15, dtype=torch.int8),
+                               torch.full((n,), 1, dtype=torch.uint8))
+    out = _np(env.board).reshape(n, 4, 4)
+    got = {2: out[:, 0, :], 3: out[:, 0, ::-1], 0: out[:, :, 0], 1: out[:, ::-1, 0]}[action]
+    assert np.array_equal(got, ref_rows)
+    assert np.array_equal(_np(r).astype(np.int64), np.where(changed, ref_score, 0))
+    assert int(ref_score.max()) == 2 * 262144  # [17, 17, 17, 17]: two 2^17 + 2^17 merges
+    assert np.array_equal((_np(lg) >> action) & 1, changed.astype(np.uint8))
+    assert env.error_count() == 0
+
+
 def test_legal_mask_vs_oracle(g2048):
     b = _random_boards(20000, 1)
     env = _env_with(g2048, b)
