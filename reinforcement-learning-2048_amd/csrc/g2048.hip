@@ -244,31 +244,37 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
 }
 
-// The fused rollout step of the dense 16-64-4 net (BASELINE configs[2]): each lane evaluates
-// Q(s) of its own board (h = relu(W1 x + b1), Q = W2 h + b2 in the summation order of
-// k_mlp_forward, so Q and the chosen actions are bitwise those of forward +
-// g2048_env_step_egreedy) and then takes the eps-greedy step.  1 280 FMA per lane as 640
-// v_pk_fma_f32 with SGPR weight operands.  At 64k boards (1 wave per SIMD) the MLP phase is
-// bound by exposed scalar-load latency (~12k cycles, measured with s_memtime; an LDS-staged
-// variant hit the same time, bound by LDS broadcast bandwidth).
-
+// The fused rollout step of the dense 16-64-4 net (BASELINE configs[2]): Q(s) of each board
+// (h = relu(W1 x + b1), Q = W2 h + b2 in the summation order of k_mlp_forward, so Q and the
+// chosen actions are bitwise those of forward + g2048_env_step_egreedy), then the eps-greedy
+// step.  Weights are SGPR operands (uniform loads -> s_load): with one wave doing all 64 units
+// per board at 64k boards (1 wave per SIMD) the MLP phase was bound by exposed scalar-load
+// latency (~12k cycles; an LDS-staged variant hit the same time, bound by LDS broadcast
+// bandwidth).
+// The MLP is split over two waves per 64 boards (workgroup of 128): wave 0 evaluates the even
+// hidden units (the e chains, bias included), wave 1 the odd units (the o chains); wave 1 hands
+// its o over through LDS and wave 0 forms Q = e + o and takes the step.  The two waves per SIMD
+// hide each other's scalar-load latency: 7.4 us per 64k-board step against 8.6 us with one wave
+// doing all 64 units (tools/stepbench.py).
 template <bool kFull>
-__global__ __launch_bounds__(kBlock) void k_step_dense64(StepArgs A, const float* __restrict__ w1,
-                                                         const float* __restrict__ b1,
-                                                         const float* __restrict__ w2,
-                                                         const float* __restrict__ b2,
-                                                         float* q_out) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (!kFull && i >= A.n) return;
-    Board b = load_board(A.board[i]);
-    uint4 m = A.meta[i];
-    uint4 ep = A.ep[i];
-    double eps;
-    if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board
-        const double e = (double)ep.x;
-        eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
-    } else {
-        eps = A.eps_dev ? *A.eps_dev : A.eps;
+__global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const float* __restrict__ w1,
+                                                            const float* __restrict__ b1,
+                                                            const float* __restrict__ w2,
+                                                            const float* __restrict__ b2,
+                                                            float* q_out) {
+    __shared__ float4 so[64];
+    const int lane = threadIdx.x & 63;
+    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+    const bool live = kFull || i < A.n;
+    Board b{0u, 0u, 0u, 0u};
+    uint4 m = make_uint4(0u, 0u, 0u, 0u), ep = make_uint4(0u, 0u, 0u, 0u);
+    if (live) {
+        b = load_board(A.board[i]);
+        if (half == 0) {
+            m = A.meta[i];
+            ep = A.ep[i];
+        }
     }
     float x[16];
     const uint32_t rw[4] = {b.r0, b.r1, b.r2, b.r3};
@@ -276,40 +282,39 @@ __global__ __launch_bounds__(kBlock) void k_step_dense64(StepArgs A, const float
     for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int c = 0; c < 4; ++c) x[4 * r + c] = (float)((rw[r] >> (8 * c)) & 0xFFu);
-    // h_j = (p0 + p1) + (p2 + p3) with p_r the partial sum over k = r (mod 4) (bias in p0) and
-    // Q_a = e + o over even / odd j (bias in e) -- the order of forward_tile in g2048_mlp.hip.
-    // An adjacent pair of the natural [j][k] / [a][j] weights is then the SGPR-pair operand of
-    // one v_pk_fma_f32 (uniform read-only loads -> s_load): 2 packed chains per hidden unit, 4
-    // units per iteration, no LDS.
     typedef float f2 __attribute__((ext_vector_type(2)));
     const f2* w1p = reinterpret_cast<const f2*>(w1);  // [j][k/2]
-    const f2* w2p = reinterpret_cast<const f2*>(w2);  // [a][j/2]
     f2 xp[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) xp[u] = f2{x[2 * u], x[2 * u + 1]};
-    f2 acc2[4];
+    float acc[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) acc2[a] = f2{b2[a], 0.f};
-#pragma unroll 2
+    for (int a = 0; a < 4; ++a) acc[a] = half == 0 ? b2[a] : 0.f;
+#pragma unroll 4
     for (int jj = 0; jj < 32; ++jj) {
-        float hv[2];
+        const int j = 2 * jj + half;
+        f2 pa = f2{b1[j], 0.f}, pb = f2{0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int j = 2 * jj + e;
-            f2 pa = f2{b1[j], 0.f}, pb = f2{0.f, 0.f};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                pa = __builtin_elementwise_fma(w1p[j * 8 + 2 * u], xp[2 * u], pa);
-                pb = __builtin_elementwise_fma(w1p[j * 8 + 2 * u + 1], xp[2 * u + 1], pb);
-            }
-            hv[e] = fmaxf((pa.x + pa.y) + (pb.x + pb.y), 0.f);
+        for (int u = 0; u < 4; ++u) {
+            pa = __builtin_elementwise_fma(w1p[j * 8 + 2 * u], xp[2 * u], pa);
+            pb = __builtin_elementwise_fma(w1p[j * 8 + 2 * u + 1], xp[2 * u + 1], pb);
         }
-        const f2 hp = f2{hv[0], hv[1]};
+        const float h = fmaxf((pa.x + pa.y) + (pb.x + pb.y), 0.f);
 #pragma unroll
-        for (int a = 0; a < 4; ++a) acc2[a] = __builtin_elementwise_fma(w2p[a * 32 + jj], hp, acc2[a]);
+        for (int a = 0; a < 4; ++a) acc[a] = fmaf(w2[a * 64 + j], h, acc[a]);
     }
-    const float4 q = make_float4(acc2[0].x + acc2[0].y, acc2[1].x + acc2[1].y,
-                                 acc2[2].x + acc2[2].y, acc2[3].x + acc2[3].y);
+    if (half == 1) so[lane] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    __syncthreads();
+    if (half == 1 || !live) return;
+    const float4 o = so[lane];
+    const float4 q = make_float4(acc[0] + o.x, acc[1] + o.y, acc[2] + o.z, acc[3] + o.w);
+    double eps;
+    if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board
+        const double e = (double)ep.x;
+        eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
+    } else {
+        eps = A.eps_dev ? *A.eps_dev : A.eps;
+    }
     if (q_out) reinterpret_cast<float4*>(q_out)[i] = q;
     int32_t rew;
     uint32_t done, legal, act;
@@ -805,12 +810,13 @@ int g2048_env_step_egreedy_dense64(g2048_env* e, const g2048_dense64_params* p,
     A.action_out = action_out;
     DeviceGuard g(e->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (e->n % kBlock == 0)
-        hipLaunchKernelGGL((k_step_dense64<true>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A,
-                           p->w1, p->b1, p->w2, p->b2, q_out);
+    const unsigned grid = (unsigned)((e->n + 63) / 64);  // 64 boards per 2-wave workgroup
+    if (e->n % 64 == 0)
+        hipLaunchKernelGGL((k_step_dense64_split<true>), dim3(grid), dim3(128), 0, st, A, p->w1,
+                           p->b1, p->w2, p->b2, q_out);
     else
-        hipLaunchKernelGGL((k_step_dense64<false>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A,
-                           p->w1, p->b1, p->w2, p->b2, q_out);
+        hipLaunchKernelGGL((k_step_dense64_split<false>), dim3(grid), dim3(128), 0, st, A, p->w1,
+                           p->b1, p->w2, p->b2, q_out);
     G_HIP(hipGetLastError());
     return G2048_OK;
 }
