@@ -314,6 +314,23 @@ G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
                                    float* exp_avg_sq_dev, double lr, double beta1, double beta2,
                                    double eps, uint64_t sync_every, void* stream);
 
+/* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
+ * Best-first search from one board (exponents start[16], merge score start_score) until a
+ * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion
+ * order, the reference's closed-list rule and child order (up, down, left, right), one spawn
+ * per child -- Philox4x32-10 keyed (seed, game, expansion counter), or (tests, parity with
+ * reference runs) a 2 in the first empty cell.  Writes the path root .. returned node:
+ * path_boards [len + 1][16], path_moves [len], path_scores [len + 1]; *success = 0 when the
+ * open list empties or max_expansions (> 0) is reached -- the last popped node is returned,
+ * as in the reference.  G2048_EINVAL if the path is longer than max_path.  No GPU needed. */
+#define G2048_ASTAR_SPAWN_PHILOX 0
+#define G2048_ASTAR_SPAWN_FIRST_EMPTY 1
+G2048_API int g2048_astar_search(const uint8_t* start, int64_t start_score, int goal_exp,
+                                 uint64_t seed, uint64_t game, int spawn_mode,
+                                 int64_t max_expansions, int64_t max_path, uint8_t* path_boards,
+                                 uint8_t* path_moves, int64_t* path_scores, int64_t* path_len,
+                                 int64_t* visited, int64_t* expanded, int* success);
+
 /* ---- misc ---- */
 G2048_API const char* g2048_last_error(void);
 G2048_API int g2048_abi_version(void);

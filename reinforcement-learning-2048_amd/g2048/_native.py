@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libg2048.so
 G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOMEM, G2048_EBADINPUT = 0, -1, -2, -3, -4
 P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
+ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
 
 # every symbol include/g2048.h declares, with (restype, argtypes)
 _vp, _i64, _u64, _i32, _u32, _int, _dbl = (C.c_void_p, C.c_int64, C.c_uint64, C.c_int32,
@@ -66,6 +67,8 @@ SIGNATURES = {
     "g2048_dense64_update_workspace": (_i64, [_i64]),
     "g2048_dense64_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
+    "g2048_astar_search": (_int, [_vp, _i64, _int, _u64, _u64, _int, _i64, _i64, _vp, _vp, _vp,
+                                  _vp, _vp, _vp, _vp]),
     "g2048_last_error": (C.c_char_p, []),
     "g2048_abi_version": (_int, []),
 }
