@@ -220,8 +220,9 @@ def bench_rollout(args, world, rank, dev):
 def bench_train(args, world, rank, dev, net):
     """BASELINE configs[2]/[3] (configs[4] at --gpus 8): N boards + Double-DQN, replay 1M,
     B=8192, fp32, graph-captured update with RCCL gradient all-reduce when world > 1.
-    Times (a) learner updates alone and (b) the full loop iteration = Q forward of all boards +
-    fused epsilon-greedy step/append + 1 update."""
+    Times (a) learner updates alone and (b) the full loop iteration = Q forward of the boards
+    on the greedy branch + fused epsilon-greedy step/append + 1 update, early (eps ~ 1) and late
+    (eps = min_epsilon) in the schedule."""
     import g2048
     from g2048.learner import DQNLearner, Trainer, flops_per_update
 
@@ -257,6 +258,21 @@ def bench_train(args, world, rank, dev, net):
     torch.cuda.synchronize()
     barrier(world, dev)
     loop_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
+    # (b) ran at the start of the eps schedule (eps ~ 1: the conv forward runs on the few
+    # greedy-branch boards only, the dense step skips all-explore groups).  (c) the same loop
+    # late in training: every board past eps_decay_episodes, eps = min_epsilon (Q of ~all boards).
+    eps_early = float(T.current_epsilon().mean())
+    env.ep[:, 0] = int(T.eps_decay)
+    T.step()
+    torch.cuda.synchronize()
+    eps_late = float(T.current_epsilon().mean())
+    barrier(world, dev)
+    t0 = time.perf_counter()
+    for _ in range(K2):
+        T.step()
+    torch.cuda.synchronize()
+    barrier(world, dev)
+    late_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
     loss = float(L.last_loss)
     env.check_errors()
     fl = flops_per_update(net, args.batch)
@@ -264,7 +280,10 @@ def bench_train(args, world, rank, dev, net):
             "learner_tflops": fl / (upd_ev / K) / 1e12,
             "loop_iter_ms": loop_wall / K2 * 1e3,
             "loop_env_steps_per_s": sum_over_ranks(n * K2 / loop_wall, world, dev),
-            "loop_updates_per_s": K2 / loop_wall,
+            "loop_updates_per_s": K2 / loop_wall, "loop_epsilon_mean": eps_early,
+            "loop_late_iter_ms": late_wall / K2 * 1e3,
+            "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
+            "loop_late_epsilon_mean": eps_late,
             "batch": args.batch, "replay": C, "dtype": "fp32", "loss": loss,
             "params": L.n_params}
 

@@ -200,6 +200,19 @@ G2048_API int g2048_convnet_forward(const g2048_convnet_params* params, const ui
                                     const int64_t* idx_dev, int64_t n, float* q_out_dev,
                                     void* stream);
 
+/* The rollout forward restricted to the greedy branch: epsilon_greedy_policy evaluates the model
+ * only when it does not explore (src/dqn_lib.py:20-24).  For every board of env the explore draw
+ * of its next g2048_env_step_egreedy / _schedule step is repeated (same Philox block; eps as in
+ * g2048_env_step_egreedy_dense64: eps_decay_episodes > 0 selects the per-board schedule, else
+ * eps_dev (device f64) or eps), and q_out[b] (f32[n][4]) is written only for the boards that
+ * will take the greedy branch -- bitwise the rows g2048_convnet_forward writes.  The other rows
+ * are left as they are: the step does not read them.  Call it between the same two steps as
+ * the forward it replaces, with the same eps arguments as the step. */
+G2048_API int g2048_convnet_forward_greedy(const g2048_convnet_params* params, g2048_env* env,
+                                           const double* eps_dev, double eps,
+                                           double eps_decay_episodes, double eps_min,
+                                           float* q_out_dev, void* stream);
+
 /* Gradient of the graded half of train_step (src/dqn_lib.py:146-161) for the conv net, fp32:
  * q_b = Q(rows[idx[b]])[actions[idx[b]]], loss = sum_b (q_b - y_b)^2 (MSELoss(reduction='sum'))
  * and d loss / d params written to grad_out (f32[33476], torch parameter order and layouts --

@@ -106,7 +106,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     } else if constexpr (MODE == MODE_RANDOM) {
         act = u.x >> 30;
     } else {
-        const bool explore = (double)u.y * (1.0 / 4294967296.0) < eps;
+        const bool explore = explores(u.y, eps);
         const bool fixed = (A.flags & G2048_EGREEDY_FIXED) != 0u;
         if (explore) {
             const uint32_t nl = __popc(legal);
@@ -221,12 +221,11 @@ __global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
     uint4 ep = kPre ? A.ep[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
-        if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board: ep = its episode count
-            const double e = (double)(kPre ? ep.x : reinterpret_cast<const uint32_t*>(A.ep)[4 * i]);
-            eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
-        } else {
-            eps = A.eps_dev ? *A.eps_dev : A.eps;
-        }
+        // src/dqn_lib.py:184-188 per board: ep.x = its episode count
+        const uint32_t e = A.eps_decay > 0.0
+                               ? (kPre ? ep.x : reinterpret_cast<const uint32_t*>(A.ep)[4 * i])
+                               : 0u;
+        eps = step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, e);
     }
     int32_t rew;
     uint32_t done, legal, act;
@@ -271,10 +270,23 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     uint4 m = make_uint4(0u, 0u, 0u, 0u), ep = make_uint4(0u, 0u, 0u, 0u);
     if (live) {
         b = load_board(A.board[i]);
-        if (half == 0) {
+        if (half == 0 || !q_out) {
             m = A.meta[i];
             ep = A.ep[i];
         }
+    }
+    // epsilon_greedy_policy evaluates the model only on its greedy branch (src/dqn_lib.py:20-24):
+    // when no board of the 64 takes it (early in the eps schedule) both waves skip the MLP --
+    // unless q_out asks for every board's Q.  The two waves hold the same boards, so they agree.
+    bool any_greedy = true;
+    if (!q_out) {
+        bool greedy = false;
+        if (live) {
+            const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
+            const uint4 u = draw(A.seed_lo, A.seed_hi, A.board_offset + (uint64_t)i, DOMAIN_STEP, t);
+            greedy = !explores(u.y, step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, ep.x));
+        }
+        any_greedy = __ballot(greedy) != 0ull;
     }
     float x[16];
     const uint32_t rw[4] = {b.r0, b.r1, b.r2, b.r3};
@@ -291,7 +303,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
 #pragma unroll
     for (int a = 0; a < 4; ++a) acc[a] = half == 0 ? b2[a] : 0.f;
 #pragma unroll 4
-    for (int jj = 0; jj < 32; ++jj) {
+    for (int jj = 0; jj < 32 && any_greedy; ++jj) {
         const int j = 2 * jj + half;
         f2 pa = f2{b1[j], 0.f}, pb = f2{0.f, 0.f};
 #pragma unroll
@@ -308,13 +320,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     if (half == 1 || !live) return;
     const float4 o = so[lane];
     const float4 q = make_float4(acc[0] + o.x, acc[1] + o.y, acc[2] + o.z, acc[3] + o.w);
-    double eps;
-    if (A.eps_decay > 0.0) {  // src/dqn_lib.py:184-188 per board
-        const double e = (double)ep.x;
-        eps = fmax((A.eps_decay - e) / A.eps_decay, A.eps_min);
-    } else {
-        eps = A.eps_dev ? *A.eps_dev : A.eps;
-    }
+    const double eps = step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, ep.x);
     if (q_out) reinterpret_cast<float4*>(q_out)[i] = q;
     int32_t rew;
     uint32_t done, legal, act;
@@ -695,6 +701,13 @@ int g2048_env_views(g2048_env* e, uint8_t** board, uint32_t** meta, uint32_t** e
 }
 
 int64_t g2048_env_size(const g2048_env* e) { return e ? e->n : 0; }
+
+int g2048_env_rng(const g2048_env* e, uint64_t* seed, uint64_t* board_offset) {
+    if (!e || !seed || !board_offset) return fail(G2048_EINVAL, "env_rng: NULL argument");
+    *seed = e->seed;
+    *board_offset = e->board_offset;
+    return G2048_OK;
+}
 
 int g2048_env_reset(g2048_env* e, const uint8_t* mask, void* stream) {
     if (!e) return fail(G2048_EINVAL, "env_reset: NULL env");

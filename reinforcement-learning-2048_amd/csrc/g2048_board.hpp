@@ -225,6 +225,21 @@ __device__ __forceinline__ uint4 draw(uint32_t seed_lo, uint32_t seed_hi, uint64
                     seed_lo, seed_hi);
 }
 
+// eps of a board's next eps-greedy step (src/dqn_lib.py:184-188): eps_decay > 0 selects the
+// per-board schedule max((D - episodes) / D, eps_min), else *eps_dev or eps.  Shared by the step
+// kernels and the greedy-only forward (g2048_qnet.hip), which must agree on every draw.
+__device__ __forceinline__ double step_eps(double eps_decay, double eps_min, const double* eps_dev,
+                                           double eps, uint32_t episodes) {
+    if (eps_decay > 0.0) return fmax((eps_decay - (double)episodes) / eps_decay, eps_min);
+    return eps_dev ? *eps_dev : eps;
+}
+
+// The random branch of epsilon_greedy_policy (src/dqn_lib.py:20, np.random.rand() < eps) with
+// word y of the step's Philox block as the uniform.
+__device__ __forceinline__ bool explores(uint32_t uy, double eps) {
+    return (double)uy * (1.0 / 4294967296.0) < eps;
+}
+
 // Two spawns on an empty board (src/board.py:18-20) from ONE Philox block: (u.z, u.w) for the
 // first, (u.z << 4, u.x << 2) for the second -- the words a terminal step leaves unused, so the
 // auto-reset reuses the step's own block.  With 16 empty cells the first is cell u.z >> 28; the

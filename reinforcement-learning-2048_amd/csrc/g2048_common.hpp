@@ -1,8 +1,15 @@
 // g2048_common.hpp -- internal helpers shared by the translation units of libg2048.so.
 #pragma once
 
+#include <stdint.h>
+
 // Record a printf-style message for g2048_last_error() and return `code` (hidden symbol).
 int g2048_fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+// The env's Philox seed and global board offset (kernels outside g2048.hip that must repeat the
+// step's draws: the greedy-only forward of g2048_qnet.hip).  Hidden symbol.
+struct g2048_env;
+extern "C" int g2048_env_rng(const g2048_env* e, uint64_t* seed, uint64_t* board_offset);
 
 #ifdef __HIPCC__
 #include <hip/hip_runtime.h>

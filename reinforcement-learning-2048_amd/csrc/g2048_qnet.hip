@@ -174,6 +174,125 @@ __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
     }
 }
 
+// The rollout's Q restricted to the boards whose next eps-greedy step is greedy
+// (g2048_convnet_forward_greedy).  epsilon_greedy_policy evaluates the model only on that branch
+// (src/dqn_lib.py:20-24), so early in the eps schedule most of the forward is skipped.
+// Workgroup w owns the contiguous boards [w*chunk, (w+1)*chunk).  Per window of GW boards it
+// repeats the step kernel's explore draw for each (same Philox block, same eps), appends the
+// greedy ones to an LDS queue (ballot + popcount), then runs full 16-board tiles of the queue
+// (the next tile's boards loaded during the current one) and scatters Q to the boards' own rows;
+// fewer than 16 left over carry into the next window, and the last window runs a partial tile.
+// The net is staged on the first tile only: a workgroup whose boards all explore never loads
+// it.  Rows of explorers are not written.  Q of a board does not depend on its tile mates, so
+// the rows written are bitwise those of g2048_convnet_forward.
+struct GreedyArgs {
+    ConvNetArgs net;        // rows = the env's boards, n = its size, q = [n][4]
+    const uint4* meta;      // {score, moves, steps_lo, steps_hi}: the draw's counter
+    const uint32_t* ep;     // [n][4]: ep[4i] = episodes (the schedule's e)
+    uint64_t board_offset;  // global id of board 0
+    uint32_t seed_lo, seed_hi;
+    const double* eps_dev;
+    double eps, eps_decay, eps_min;
+    int64_t chunk;
+};
+
+constexpr int GW = 4 * NT;       // boards selected per window (4 per thread)
+constexpr int GQ = GW + 16;      // queue: a window + the carried remainder
+
+__global__ __launch_bounds__(NT) void k_conv_forward_greedy(GreedyArgs G) {
+    namespace P = persist;
+    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
+    __shared__ int32_t queue[GQ];  // board - c0 of each selected board, in board order
+    __shared__ int32_t wcnt[4][4];  // [k][wave] greedy count
+    const ConvNetArgs& A = G.net;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const NetW W{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2};
+    P::Regs R;
+    bool staged = false;
+    const int64_t c0 = (int64_t)blockIdx.x * G.chunk;
+    const int64_t c1 = c0 + G.chunk < A.n ? c0 + G.chunk : A.n;
+    const uint32_t* rows32 = reinterpret_cast<const uint32_t*>(A.rows);
+    float* xs = lds + P::OFF_X;
+    float* qs = lds + P::OFF_Q;
+    // word t & 3 of board t >> 2 of the tile at queue[h], nb boards (thread t < 64)
+    auto load_word = [&](int h, int nb) -> uint32_t {
+        if (t >= P::S * 4 || (t >> 2) >= nb) return 0u;
+        return rows32[(c0 + queue[h + (t >> 2)]) * 4 + (t & 3)];
+    };
+    int qn = 0;  // queue length (uniform)
+    for (int64_t w0 = c0; w0 < c1; w0 += GW) {
+        const bool last = w0 + GW >= c1;
+        uint4 m[4];
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = w0 + k * NT + t;
+            m[k] = make_uint4(0u, 0u, 0u, 0u);
+            e[k] = 0u;
+            if (i < c1) {
+                m[k] = G.meta[i];
+                if (G.eps_decay > 0.0) e[k] = G.ep[4 * i];
+            }
+        }
+        uint64_t bal[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t i = w0 + k * NT + t;
+            bool g = false;
+            if (i < c1) {
+                const uint64_t tt = (uint64_t)m[k].z | ((uint64_t)m[k].w << 32);
+                const uint4 u = g2048::draw(G.seed_lo, G.seed_hi, G.board_offset + (uint64_t)i,
+                                            g2048::DOMAIN_STEP, tt);
+                g = !g2048::explores(u.y, g2048::step_eps(G.eps_decay, G.eps_min, G.eps_dev,
+                                                          G.eps, e[k]));
+            }
+            bal[k] = __ballot(g);
+            if (lane == 0) wcnt[k][wv] = __popcll(bal[k]);
+        }
+        __syncthreads();
+        const uint64_t below = (1ull << lane) - 1ull;
+        int base = qn;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+            for (int ww = 0; ww < 4; ++ww) {
+                const int c = wcnt[k][ww];
+                if (ww == wv && ((bal[k] >> lane) & 1ull))
+                    queue[base + __popcll(bal[k] & below)] = (int32_t)(w0 + k * NT + t - c0);
+                base += c;
+            }
+        }
+        qn = base;
+        __syncthreads();
+        auto runnable = [&](int h) { return qn - h >= P::S || (last && qn - h > 0); };
+        if (!runnable(0)) continue;  // < 16 selected so far: carried as they are
+        int h = 0;
+        uint32_t next_word = load_word(0, qn < P::S ? qn : P::S);
+        if (!staged) {
+            P::stage(W, lds, R);
+            staged = true;
+        }
+        while (true) {
+            const int nb = qn - h < P::S ? qn - h : P::S;
+            if (t < P::S * 4) P::put_word(xs, t, next_word);
+            __syncthreads();
+            const int h2 = h + nb;
+            if (runnable(h2)) next_word = load_word(h2, qn - h2 < P::S ? qn - h2 : P::S);
+            P::tile(xs, lds, R, qs);
+            if (t < P::S * 4 && (t >> 2) < nb)
+                A.q[(c0 + queue[h + (t >> 2)]) * 4 + (t & 3)] = qs[t];
+            h = h2;
+            if (!runnable(h)) break;
+        }
+        const int rem = qn - h;  // < 16 (0 after the last window)
+        const int v = t < rem ? queue[h + t] : 0;
+        __syncthreads();
+        if (t < rem) queue[t] = v;
+        qn = rem;
+        __syncthreads();
+    }
+}
+
 // Double-DQN targets for a minibatch (src/dqn_lib.py:67-68,125-132), one launch:
 //   idx_b = uniform row of the ring (Philox, epoch = the learner's update counter) or idx_in,
 //   a*_b  = argmax_a Q_online(s'_b)  (first index on ties, torch.argmax),
@@ -311,6 +430,45 @@ extern "C" G2048_API int g2048_convnet_forward(const g2048_convnet_params* p, co
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_forward: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int g2048_convnet_forward_greedy(const g2048_convnet_params* p,
+                                                      g2048_env* env, const double* eps_dev,
+                                                      double eps, double eps_decay_episodes,
+                                                      double eps_min, float* q_out, void* stream) {
+    if (!p || !env || !q_out)
+        return g2048_fail(G2048_EINVAL, "convnet_forward_greedy: NULL argument");
+    if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->fc1_w || !p->fc1_b || !p->fc2_w || !p->fc2_b)
+        return g2048_fail(G2048_EINVAL, "convnet_forward_greedy: NULL parameter pointer");
+    uint8_t* board = nullptr;
+    uint32_t *meta = nullptr, *ep = nullptr;
+    uint64_t seed = 0, offset = 0;
+    if (g2048_env_views(env, &board, &meta, &ep) != G2048_OK ||
+        g2048_env_rng(env, &seed, &offset) != G2048_OK)
+        return G2048_EINVAL;
+    const int64_t n = g2048_env_size(env);
+    if (n <= 0) return g2048_fail(G2048_EINVAL, "convnet_forward_greedy: empty env");
+    GreedyArgs G;
+    G.net = ConvNetArgs{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b,
+                        board, nullptr, n, q_out};
+    G.meta = reinterpret_cast<const uint4*>(meta);
+    G.ep = ep;
+    G.board_offset = offset;
+    G.seed_lo = (uint32_t)seed;
+    G.seed_hi = (uint32_t)(seed >> 32);
+    G.eps_dev = eps_dev;
+    G.eps = eps;
+    G.eps_decay = eps_decay_episodes > 0.0 ? eps_decay_episodes : 0.0;
+    G.eps_min = eps_min;
+    const int64_t tiles16 = (n + persist::S - 1) / persist::S;
+    const int64_t grid = tiles16 < 256 ? tiles16 : 256;  // one workgroup per CU
+    G.chunk = (n + grid - 1) / grid;
+    hipLaunchKernelGGL(k_conv_forward_greedy, dim3((unsigned)grid), dim3(NT), 0,
+                       reinterpret_cast<hipStream_t>(stream), G);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "convnet_forward_greedy: %s",
+                                        hipGetErrorString(e));
 }
 
 extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,

@@ -50,6 +50,7 @@ SIGNATURES = {
     "g2048_replay_sample_encode": (_int, [_vp, _vp, _i64, _u64, _u64, _int, _vp, _vp, _vp, _vp,
                                           _vp, _vp, _vp]),
     "g2048_convnet_forward": (_int, [_vp, _vp, _vp, _i64, _vp, _vp]),
+    "g2048_convnet_forward_greedy": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp]),
     "g2048_convnet_train_workspace": (_i64, [_i64]),
     "g2048_convnet_train_grad": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]),
     "g2048_convnet_train_adam": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp,

@@ -225,19 +225,25 @@ class VecEnv2048:
                                                 self._stream()), "g2048_env_step_egreedy")
         return action, reward, done
 
+    def eps_args(self, epsilon, eps_schedule=None):
+        """(eps_dev, eps, eps_decay_episodes, eps_min) of the ABI's eps forms: a schedule
+        (decay_episodes, min_eps), a float64 device scalar tensor, or a float."""
+        if eps_schedule is not None:
+            if not float(eps_schedule[0]) > 0.0:
+                raise ValueError("eps_schedule decay_episodes must be > 0")
+            return None, 0.0, float(eps_schedule[0]), float(eps_schedule[1])
+        if isinstance(epsilon, torch.Tensor):
+            if epsilon.dtype != torch.float64 or epsilon.device != self.device or epsilon.numel() != 1:
+                raise ValueError("epsilon tensor must be one float64 on the env device")
+            return N.ptr(epsilon), 0.0, 0.0, 0.0
+        return None, float(epsilon), 0.0, 0.0
+
     def step_egreedy_dense64(self, params, epsilon=0.0, replay: "ReplayBuffer | None" = None,
                              reward=None, done=None, action=None, eps_schedule=None, q_out=None):
         """play_one_step for every board with the dense 16-64-4 Q-net computed INSIDE the step
         kernel (g2048_env_step_egreedy_dense64): params = qnet.net_params(model) of an fp32
         dense64 net.  Same epsilon forms as step_egreedy.  Returns (action, reward, done)."""
-        if eps_schedule is not None:
-            eps_ptr, eps_val, dec, mn = None, 0.0, float(eps_schedule[0]), float(eps_schedule[1])
-        elif isinstance(epsilon, torch.Tensor):
-            if epsilon.dtype != torch.float64 or epsilon.device != self.device or epsilon.numel() != 1:
-                raise ValueError("epsilon tensor must be one float64 on the env device")
-            eps_ptr, eps_val, dec, mn = N.ptr(epsilon), 0.0, 0.0, 0.0
-        else:
-            eps_ptr, eps_val, dec, mn = None, float(epsilon), 0.0, 0.0
+        eps_ptr, eps_val, dec, mn = self.eps_args(epsilon, eps_schedule)
         if q_out is not None and (q_out.shape != (self.n, 4) or q_out.dtype != torch.float32
                                   or not q_out.is_contiguous()):
             raise ValueError(f"q_out must be a contiguous float32 [{self.n}, 4] tensor")

@@ -281,7 +281,9 @@ class Trainer:
     """Vectorised training_loop (src/dqn_lib.py:167-244).
 
     Per iteration: Q = online(boards) -> fused epsilon-greedy step of all N boards with replay
-    append (for the fp32 dense 16-64-4 net, Q is computed inside the step kernel itself) ->
+    append (for the fp32 dense 16-64-4 net, Q is computed inside the step kernel itself; the fused
+    conv net evaluates only the boards whose step takes the greedy branch, as
+    epsilon_greedy_policy does, src/dqn_lib.py:20-24) ->
     `updates_per_step` learner updates once the ring holds `min_fill` transitions.
     epsilon_b = max((eps_decay_episodes - e_b) / eps_decay_episodes, min_epsilon) with e_b the
     number of episodes board b has finished -- the reference's per-episode schedule (:184-188)
@@ -323,6 +325,9 @@ class Trainer:
         self._action = torch.empty(env.n, dtype=torch.uint8, device=env.device)
         self._reward = torch.empty(env.n, dtype=torch.int32, device=env.device)
         self._done = torch.empty(env.n, dtype=torch.uint8, device=env.device)
+        # fused conv learner: Q of the greedy-branch boards only (rows of explorers unused)
+        self._q = (torch.zeros((env.n, 4), dtype=torch.float32, device=env.device)
+                   if learner.fused and learner.kind == "conv" else None)
         self._numbers = {}  # (board, board_episode) -> Experiment episode number
 
     def prefill(self, steps: int) -> None:
@@ -340,7 +345,11 @@ class Trainer:
                                           reward=self._reward, done=self._done,
                                           action=self._action, eps_schedule=sched)
         else:
-            q = self.learner.q_values(self.env)
+            if self._q is not None:  # the model runs on the greedy branch only (src/dqn_lib.py:20-24)
+                q = qnet.forward_greedy(self.learner.model, self.env, eps_schedule=sched,
+                                        out=self._q, params=self.learner._p_on)
+            else:
+                q = self.learner.q_values(self.env)
             self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward,
                                   done=self._done, action=self._action, eps_schedule=sched)
 

@@ -92,6 +92,26 @@ def forward(model, rows: torch.Tensor, idx: torch.Tensor | None = None,
 conv_forward = forward
 
 
+def forward_greedy(model, env, epsilon=0.0, eps_schedule=None, out: torch.Tensor | None = None,
+                   params=None):
+    """Q-values [n, 4] of env's boards, computed only for the boards whose next eps-greedy step
+    (env.step_egreedy with the same epsilon / eps_schedule) takes the greedy branch -- the only
+    branch where epsilon_greedy_policy evaluates the model (src/dqn_lib.py:20-24).  Those rows
+    are bitwise forward()'s; the other rows of `out` are left as they are.  Conv net only."""
+    if kind_of(model) != "conv":
+        raise ValueError("forward_greedy: conv net only (the dense-64 step computes Q in-kernel)")
+    if out is None:
+        out = torch.empty((env.n, 4), dtype=torch.float32, device=env.device)
+    if out.shape != (env.n, 4) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 [{env.n}, 4] tensor")
+    eps_ptr, eps_val, dec, mn = env.eps_args(epsilon, eps_schedule)
+    p = params if params is not None else net_params(model)
+    N.check(N.load().g2048_convnet_forward_greedy(C.byref(p), env.handle, eps_ptr, eps_val, dec,
+                                                  mn, N.ptr(out), N.stream_of(env.device)),
+            "g2048_convnet_forward_greedy")
+    return out
+
+
 class TrainGrad:
     """Graded half of train_step for a fused net: writes the loss and the gradient of
     sum_b (Q(s_b)[a_b] - y_b)^2 into a flat fp32 buffer laid out like

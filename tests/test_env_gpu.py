@@ -488,3 +488,43 @@ def test_fused_dense64_step_matches_forward_plus_step(g2048, mode):
     g0, g1 = logs[0].read(), logs[1].read()
     for f in g0:
         assert torch.equal(g0[f], g1[f]), f
+
+
+@pytest.mark.parametrize("mode", ["eps1", "schedule"])
+def test_fused_dense64_step_skips_explorers(g2048, mode):
+    """Without q_out the dense-64 step skips the MLP of every 64-board group whose boards all
+    take the explore branch (the model runs only on the greedy branch, src/dqn_lib.py:20-24).
+    Groups of all-new boards (eps = 1) sit next to groups with eps 0.9 and 0.05: the trajectory
+    is still bitwise forward + step, episode q-sums included."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    n = 4096 + 77
+    m = det_init(make_net("dense64", torch.float32, DEV), 0.7)
+    p = qnet.net_params(m)
+    kw = dict(eps_schedule=(30.0, 0.05)) if mode == "schedule" else {}
+    eps = 1.0 if mode == "eps1" else 0.0
+    grp = torch.arange(n, device=DEV) // 64 % 3
+    ep0 = torch.where(grp == 0, 0, torch.where(grp == 1, 3, 100)).to(torch.int32)
+    envs, rbs, logs = [], [], []
+    for _ in range(2):
+        e = g2048.VecEnv2048(n, seed=21, device=DEV)
+        rbs.append(g2048.ReplayBuffer(8 * n, device=DEV))
+        e.rollout(30)
+        e.ep[:, 0] = ep0
+        logs.append(e.attach_episode_log(16))  # (counts from the episodes set here)
+        envs.append(e)
+    for t in range(60):
+        a0, r0, d0 = envs[0].step_egreedy_dense64(p, eps, replay=rbs[0], **kw)
+        q = qnet.forward(m, envs[1].board)
+        a1, r1, d1 = envs[1].step_egreedy(q, eps, replay=rbs[1], **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
+    for name in ("board", "meta", "ep"):
+        assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
+    for name in ("s", "s2", "a", "r", "d", "count"):
+        assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name
+    g0, g1 = logs[0].read(), logs[1].read()
+    for f in g0:
+        assert torch.equal(g0[f], g1[f]), f
+    assert torch.equal(logs[0].qsum, logs[1].qsum)

@@ -378,3 +378,70 @@ def test_fused_learner_kernels_are_deterministic(G, B):
     for o in outs[1:]:
         for a, b in zip(o, outs[0]):
             assert torch.equal(a, b), "dense64 update"
+
+
+def _greedy_mask(env, eps):
+    """Boards whose next eps-greedy step takes the greedy branch: the step's Philox block
+    (counter = step t, global board id; key = seed) from the oracle, u.y / 2^32 >= eps_b."""
+    from oracle import oracle as O
+
+    meta = env.meta.cpu().numpy().view(np.uint32)
+    seed = env.seed & ((1 << 64) - 1)
+    key = [seed & 0xFFFFFFFF, seed >> 32]
+    out = np.zeros(env.n, bool)
+    for i in range(env.n):
+        gid = env.board_offset + i
+        u = O.philox([meta[i, 2], meta[i, 3], gid & 0xFFFFFFFF, gid >> 32], key)
+        out[i] = not (float(u[1]) * (1.0 / 4294967296.0) < eps[i])
+    return torch.from_numpy(out).to(DEV)
+
+
+@pytest.mark.parametrize("n,form", [(1, 0.0), (17, 1.0), (1000, 0.5), (20001, "tensor"),
+                                    (65536 + 37, "schedule")])
+def test_conv_forward_greedy_rows(G, n, form):
+    """g2048_convnet_forward_greedy writes Q only for the boards whose next step is greedy --
+    bitwise forward()'s rows -- and leaves the explorers' rows alone; stepping on it gives the
+    same actions, rewards and boards as stepping on the full forward."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    envs = []
+    ep0 = torch.randint(0, 8, (n,), generator=torch.Generator().manual_seed(n), dtype=torch.int32)
+    for _ in range(2):
+        e = G.VecEnv2048(n, device=DEV, seed=11 + n, board_offset=5 * n)
+        e.rollout(25)
+        e.ep[:, 0] = ep0.to(DEV)
+        envs.append(e)
+    if form == "schedule":
+        kw = dict(eps_schedule=(6.0, 0.1))
+        eps = np.maximum((6.0 - ep0.numpy().astype(np.float64)) / 6.0, 0.1)
+    elif form == "tensor":
+        kw = dict(epsilon=torch.tensor(0.3, dtype=torch.float64, device=DEV))
+        eps = np.full(n, 0.3)
+    else:
+        kw = dict(epsilon=form)
+        eps = np.full(n, float(form))
+    m = det_init(make_net("conv", torch.float32, DEV), 0.3)
+    full = qnet.forward(m, envs[0].board)
+    out = torch.full((n, 4), float("nan"), device=DEV)
+    qnet.forward_greedy(m, envs[0], out=out, **kw)
+    g = _greedy_mask(envs[0], eps)
+    if n > 100:
+        assert 0 < int(g.sum()) < n
+    assert torch.equal(out[g], full[g])
+    assert bool(out[~g].isnan().all())
+    eps_arg = kw.get("epsilon", 0.0)
+    sched = kw.get("eps_schedule")
+    a0, r0, d0 = envs[0].step_egreedy(out, eps_arg, eps_schedule=sched)
+    a1, r1, d1 = envs[1].step_egreedy(full, eps_arg, eps_schedule=sched)
+    assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1)
+    assert torch.equal(envs[0].board, envs[1].board)
+
+
+def test_conv_forward_greedy_rejects_dense(G):
+    from g2048 import qnet
+    from g2048.nets import make_net
+
+    env = G.VecEnv2048(64, device=DEV)
+    with pytest.raises(ValueError):
+        qnet.forward_greedy(make_net("dense64", torch.float32, DEV), env, 0.5)

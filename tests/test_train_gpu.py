@@ -159,3 +159,28 @@ def test_graphed_loop_equals_eager(G, net):
                 assert torch.equal(x, y), k
         else:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_greedy_forward_loop_equals_full_forward(G):
+    """The fused conv Trainer evaluates the net only for the boards whose step takes the greedy
+    branch (qnet.forward_greedy); with every other board's Q computed as well (a full forward
+    per step) the trajectory is bitwise the same.  Boards start at mixed episode counts, so
+    eps spans 1 .. min_epsilon from the first step."""
+    outs = []
+    for greedy in (True, False):
+        tr = _small(G, "conv", min_fill=3 * 1024, target_sync_every=3, track_boards=0)
+        assert tr._q is not None
+        if not greedy:
+            tr._q = None
+        grp = torch.arange(tr.env.n, device=DEV) % 5
+        tr.env.ep[:, 0] = grp.to(torch.int32)
+        for _ in range(25):
+            tr.step()
+        outs.append(_fingerprint(tr))
+    a, b = outs
+    for k in a:
+        if k in ("params", "target"):
+            for x, y in zip(a[k], b[k]):
+                assert torch.equal(x, y), k
+        else:
+            assert torch.equal(a[k], b[k]), k
