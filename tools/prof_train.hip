@@ -94,5 +94,53 @@ int main() {
     const char* n2[4] = {"bwd stage", "bwd dM ld", "bwd dV", "bwd epi"};
     for (int k = 8; k < 12; ++k)
         printf("%-10s %9.0f ticks/%s\n", n2[k - 8], ph[k] / (k == 8 ? N : tiles), k == 8 ? "launch" : "tile");
+
+    // Timing only (the reduction races with bwd here): do graph branches overlap?  Graph 1 =
+    // fwd, bwd, reduce in one stream; graph 2 = fwd, then bwd and reduce on two forked streams.
+    hipStream_t s0, s1;
+    (void)hipStreamCreateWithFlags(&s0, hipStreamNonBlocking);
+    (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
+    hipEvent_t fork, join;
+    (void)hipEventCreateWithFlags(&fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&join, hipEventDisableTiming);
+    hipGraphExec_t gx[2];
+    for (int v = 0; v < 2; ++v) {
+        hipGraph_t g;
+        (void)hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal);
+        for (int rep = 0; rep < 10; ++rep) {
+            hipLaunchKernelGGL(k_conv_train_fwd, dim3(grid), dim3(NT), 0, s0, A);
+            hipStream_t rs = s0;
+            if (v == 1) {
+                (void)hipEventRecord(fork, s0);
+                (void)hipStreamWaitEvent(s1, fork, 0);
+                rs = s1;
+            }
+            hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, rs, ws,
+                               grid, grad, loss, R);
+            hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, s0, A);
+            if (v == 1) {
+                (void)hipEventRecord(join, s1);
+                (void)hipStreamWaitEvent(s0, join, 0);
+            }
+        }
+        (void)hipStreamEndCapture(s0, &g);
+        (void)hipGraphInstantiate(&gx[v], g, nullptr, nullptr, 0);
+    }
+    for (int v = 0; v < 2; ++v) {
+        (void)hipGraphLaunch(gx[v], s0);
+        (void)hipStreamSynchronize(s0);
+        float best = 1e30f;
+        for (int r = 0; r < 5; ++r) {
+            (void)hipEventRecord(ev[0], s0);
+            (void)hipGraphLaunch(gx[v], s0);
+            (void)hipEventRecord(ev[1], s0);
+            (void)hipEventSynchronize(ev[1]);
+            float ms;
+            (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+            best = ms < best ? ms : best;
+        }
+        printf("graph %s: fwd + bwd + reduce %.2f us per update\n",
+               v ? "bwd || reduce (forked)" : "serial", best * 1e3f / 10);
+    }
     return 0;
 }
