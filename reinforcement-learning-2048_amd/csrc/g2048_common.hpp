@@ -36,16 +36,23 @@ __device__ __forceinline__ AdamCoef adam_coef(double t, double lr, double b1, do
     return c;
 }
 
+// One element on values: m, v updated; returns the updated parameter.
+__device__ __forceinline__ float adam_update(const AdamCoef& c, float g, float& m, float& v,
+                                             float p) {
+    m = m + c.w1 * (g - m);                      // lerp(m, g, 1 - b1), weight < 0.5 branch
+    v = v * c.b2 + c.w2 * g * g;                 // mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    return p + (-c.step_size) * (m / denom);     // addcdiv_(m, denom, value=-step_size)
+}
+
 // returns the updated parameter; m / v updated in place
 __device__ __forceinline__ float adam_apply(const AdamCoef& c, float g, float* m_, float* v_,
                                             float p) {
-    float m = *m_;
-    m = m + c.w1 * (g - m);                      // lerp(m, g, 1 - b1), weight < 0.5 branch
-    const float v = *v_ * c.b2 + c.w2 * g * g;   // mul_(b2).addcmul_(g, g, 1 - b2)
+    float m = *m_, v = *v_;
+    const float np = adam_update(c, g, m, v, p);
     *m_ = m;
     *v_ = v;
-    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
-    return p + (-c.step_size) * (m / denom);     // addcdiv_(m, denom, value=-step_size)
+    return np;
 }
 
 }  // namespace g2048

@@ -473,6 +473,18 @@ __global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
     __shared__ float part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
+    // Adam operands (wave 0) loaded with the slabs: independent of the sums
+    const bool adam = A.adam && wave == 0 && pos < P_N;
+    const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
+    const int base[4] = {P_W1, P_B1, P_W2, P_B2};
+    float am = 0.f, av = 0.f, ap = 0.f;
+    unsigned long long t = 0;
+    if (adam) {
+        t = *A.step_next;
+        am = A.m[pos];
+        av = A.v[pos];
+        ap = A.p[k][pos - base[k]];
+    }
     float r[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
@@ -492,14 +504,12 @@ __global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
             if (A.loss) *A.loss = sum;
         } else {
             if (A.grad) A.grad[pos] = sum;
-            if (A.adam) {
-                const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
-                const int base[4] = {P_W1, P_B1, P_W2, P_B2};
-                float* p = A.p[k] + (pos - base[k]);
-                const unsigned long long t = *A.step_next;
+            if (adam) {
                 const g2048::AdamCoef c = g2048::adam_coef((double)t, A.lr, A.b1, A.b2, A.eps);
-                const float np = g2048::adam_apply(c, sum, A.m + pos, A.v + pos, *p);
-                *p = np;
+                const float np = g2048::adam_update(c, sum, am, av, ap);
+                A.m[pos] = am;
+                A.v[pos] = av;
+                A.p[k][pos - base[k]] = np;
                 if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
             }
         }

@@ -585,6 +585,31 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int p4 = blockIdx.x * 64 + lane;  // float4 index within a slab
     const bool in = p4 * 4 <= SL_LOSS;
+    // Adam operands of this lane's 4 positions (wave 0), loaded with the slabs: they do not
+    // depend on the sums, so the update costs no memory round trip of its own.
+    const bool adam = R.on && wave == 0 && in;
+    int kt[4], ei[4];
+    float am[4], av[4], ap[4];
+    unsigned long long t = 0;
+    if (adam) {
+        t = *R.step;
+        constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int pos = p4 * 4 + e;
+            kt[e] = -1;
+            if (pos >= SL_LOSS) continue;
+            const int pi = slab_to_param(pos);
+            int k = 0;
+#pragma unroll
+            for (int j = 1; j < 8; ++j) k += pi >= off[j] ? 1 : 0;
+            kt[e] = k;
+            ei[e] = pi - off[k];
+            am[e] = R.m[pi];
+            av[e] = R.v[pi];
+            ap[e] = R.p[k][ei[e]];
+        }
+    }
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
         float4 r[16];
@@ -615,6 +640,8 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         sv.w += part[k][lane].w;
     }
     const float se[4] = {sv.x, sv.y, sv.z, sv.w};
+    g2048::AdamCoef c{};
+    if (adam) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int pos = p4 * 4 + e;
@@ -625,18 +652,12 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         } else {
             const int pi = slab_to_param(pos);
             if (grad) grad[pi] = s;
-            if (R.on) {
-                constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
-                int kt = 0;
-#pragma unroll
-                for (int j = 1; j < 8; ++j) kt += pi >= off[j] ? 1 : 0;
-                const int ei = pi - off[kt];
-                const unsigned long long t = *R.step;
-                const g2048::AdamCoef c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
-                float* pp = R.p[kt] + ei;
-                const float np = g2048::adam_apply(c, s, R.m + pi, R.v + pi, *pp);
-                *pp = np;
-                if (R.sync_every && t % R.sync_every == 0ull) R.tp[kt][ei] = np;
+            if (adam) {
+                const float np = g2048::adam_update(c, s, am[e], av[e], ap[e]);
+                R.m[pi] = am[e];
+                R.v[pi] = av[e];
+                R.p[kt[e]][ei[e]] = np;
+                if (R.sync_every && t % R.sync_every == 0ull) R.tp[kt[e]][ei[e]] = np;
             }
         }
     }
