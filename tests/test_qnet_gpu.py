@@ -397,11 +397,12 @@ def _greedy_mask(env, eps):
 
 
 @pytest.mark.parametrize("n,form", [(1, 0.0), (17, 1.0), (1000, 0.5), (20001, "tensor"),
-                                    (65536 + 37, "schedule")])
+                                    (65536 + 37, "schedule"), (300001, 0.5)])
 def test_conv_forward_greedy_rows(G, n, form):
     """g2048_convnet_forward_greedy writes Q only for the boards whose next step is greedy --
     bitwise forward()'s rows -- and leaves the explorers' rows alone; stepping on it gives the
-    same actions, rewards and boards as stepping on the full forward."""
+    same actions, rewards and boards as stepping on the full forward.  n = 300001 gives every
+    workgroup 1172 boards: two selection windows, with a partial tile carried between them."""
     from g2048 import qnet
     from g2048.nets import det_init, make_net
 
