@@ -372,9 +372,11 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
     P::Regs R;
     float* qon = lds + P::OFF_Q;               // [TMAX][16][4]
     float* qtg = qon + P::TMAX * P::S * 4;     // [16][4]
-    P::stage(A.on, lds, R);  // (starts with __syncthreads: the s' boards are visible)
-    for (int k = 0; k < T; ++k)
-        P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qon + k * P::S * 4);
+    if (A.double_dqn) {  // (vanilla DQN needs no online Q of s')
+        P::stage(A.on, lds, R);  // (starts with __syncthreads: the s' boards are visible)
+        for (int k = 0; k < T; ++k)
+            P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qon + k * P::S * 4);
+    }
     P::stage(A.tg, lds, R);
     for (int k = 0; k < T; ++k) {
         P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qtg);
