@@ -254,6 +254,25 @@ G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,
                                     const uint64_t* epoch_dev, float gamma, int double_dqn,
                                     int64_t* idx_out_dev, float* y_out_dev, void* stream);
 
+/* One whole conv train_step (src/dqn_lib.py:119-164; + the target sync of :227-228): the
+ * targets of g2048_convnet_targets and the gradient of g2048_convnet_train_grad on the sampled
+ * rows, then -- when exp_avg / exp_avg_sq are given -- Adam applied in place as in
+ * g2048_convnet_train_adam (grad_out may then be NULL); without them the summed gradient goes to
+ * grad_out (a data-parallel all-reduce and g2048_adam_step follow).  step_dev is the sampler
+ * epoch and Adam's t (incremented once).  y_out receives the Bellman targets.  For Double DQN
+ * the targets launch splits its grid into an online-net half (a*) and a target-net half
+ * (Q_target, r, discount), each staging one net, and the train launch forms y from them (the
+ * same float as g2048_convnet_targets).  workspace: f32[g2048_convnet_train_workspace(batch)].
+ * 4 launches per update. */
+G2048_API int g2048_convnet_update(const g2048_convnet_params* online,
+                                   const g2048_convnet_params* target, g2048_replay* rb,
+                                   const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                   uint64_t* step_dev, float gamma, int double_dqn,
+                                   int64_t* idx_out_dev, float* y_out_dev, float* workspace_dev,
+                                   float* grad_out_dev, float* loss_out_dev, float* exp_avg_dev,
+                                   float* exp_avg_sq_dev, double lr, double beta1, double beta2,
+                                   double eps, uint64_t sync_every, void* stream);
+
 /* One-launch Adam (torch.optim.Adam semantics, amsgrad off, no weight decay) over n_tensors
  * (<= 16) fp32 parameter tensors whose gradients are packed back to back in grad_dev; exp_avg /
  * exp_avg_sq are flat state buffers of the same length; the step t is read from *step_dev. */

@@ -223,6 +223,25 @@ __device__ __forceinline__ void fc1_f(const float* h2, const float* wf1s, const 
         fa[(4 * g + i) * FS + jc] = fmaxf((c0[i] + c1[i]) + sbf1[jc], 0.f);
 }
 
+// Split-role target scratch (g2048_convnet_update), in floats from its base: a* i32[B], then
+// Q_target f32[B][4] (16-byte aligned), then (r, disc) f32[B][2].
+__host__ __device__ constexpr int64_t conv_split_qtg_offset(int64_t batch) {
+    return (batch + 3) & ~int64_t(3);
+}
+__host__ __device__ constexpr int64_t conv_split_rd_offset(int64_t batch) {
+    return conv_split_qtg_offset(batch) + 4 * batch;
+}
+__host__ __device__ constexpr int64_t conv_split_floats(int64_t batch) {
+    return conv_split_rd_offset(batch) + 2 * batch;
+}
+
+// The Bellman target y = r + disc * next, disc = (1 - d) * float32(gamma), rounded after the
+// product (no FMA contraction): the same float in the targets launch and the train launch.
+__device__ __forceinline__ float bellman_y(float r, float disc, float next) {
+#pragma clang fp contract(off)
+    return r + disc * next;
+}
+
 // One board word (t < 64: word t&3 of board t>>2) -> 4 exponent floats in xs[S][16].
 __device__ __forceinline__ void put_word(float* xs, int t, uint32_t v) {
     float* dst = xs + (t >> 2) * 16 + (t & 3) * 4;

@@ -311,19 +311,44 @@ struct TargetArgs {
     int double_dqn;
     int64_t* idx_out;
     float* y;
+    // split roles (g2048_convnet_update, Double DQN): workgroups [0, G) run the online net and
+    // write a*, workgroups [G, 2G) the target net and write Q_target(s') with (float)r and the
+    // discount; the train launch forms y from them.  nullptr: each workgroup runs both nets.
+    int32_t* astar;   // [B]
+    float4* qtg;      // [B] Q_target(s'_b, .)
+    float2* rdisc;    // [B] ((float)r_b, (1 - d_b) * gamma)
 };
+
+// torch.argmax over 4 Q-values: the first index wins ties.
+__device__ __forceinline__ int argmax4_first(const float* q) {
+    int a = 0;
+    float best = q[0];
+    for (int e = 1; e < 4; ++e)
+        if (q[e] > best) {
+            best = q[e];
+            a = e;
+        }
+    return a;
+}
 
 // Each workgroup owns up to TMAX 16-sample tiles (tile = blockIdx.x + k*gridDim.x): it draws
 // their indices and loads their s' rows once, runs them through the online net (Q kept in
-// LDS), stages the target net and runs them again, then writes y.
+// LDS), stages the target net and runs them again, then writes y.  With split roles (A.qtg)
+// the grid is two halves over the same tiles, each staging ONE net for twice the tiles: one
+// staging per workgroup instead of two.
 __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
     namespace P = persist;
     __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
     __shared__ int64_t sidx[P::TMAX * P::S];
     const int t = threadIdx.x;
+    // roles: 0 = online net only, 1 = target net only, 2 = both (no split)
+    const bool split = A.qtg != nullptr;
+    const int G = split ? (int)gridDim.x / 2 : (int)gridDim.x;
+    const int role = split ? (int)blockIdx.x / G : 2;
+    const int grp = split ? (int)blockIdx.x % G : (int)blockIdx.x;
     const int64_t ntiles = (A.batch + P::S - 1) / P::S;
     int T = 0;
-    for (int64_t tl = blockIdx.x; tl < ntiles && T < P::TMAX; tl += gridDim.x) ++T;
+    for (int64_t tl = grp; tl < ntiles && T < P::TMAX; tl += G) ++T;
     // sampler: thread t < 64 owns word t&3 of sample t>>2 of every tile; it draws the sample's
     // ring row itself (same draw as k_sample / o2048_replay_sample_f64, domain 3; the four
     // threads of a sample agree) and loads that word of s' at once
@@ -343,7 +368,7 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
         for (int k = 0; k < P::TMAX; ++k) {
             w[k] = 0u;
             if (k >= T) continue;
-            const int64_t b = (blockIdx.x + (int64_t)k * gridDim.x) * P::S + s;
+            const int64_t b = (grp + (int64_t)k * G) * P::S + s;
             int64_t j = 0;
             if (b < A.batch) {
                 if (A.idx_in) {
@@ -356,12 +381,14 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
                     const unsigned long long x = ((unsigned long long)u.y << 32) | u.x;
                     j = (int64_t)__umul64hi(x, cnt);
                 }
-                if ((t & 3) == 0) A.idx_out[b] = j;
+                if ((t & 3) == 0 && role != 1) A.idx_out[b] = j;
             }
             if ((t & 3) == 0) {
                 sidx[k * P::S + s] = j;
-                rv[k] = A.r[j];
-                dv[k] = A.d[j];
+                if (role != 0) {
+                    rv[k] = A.r[j];
+                    dv[k] = A.d[j];
+                }
             }
             w[k] = reinterpret_cast<const uint32_t*>(A.s2)[j * 4 + (t & 3)];
         }
@@ -372,32 +399,34 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
     P::Regs R;
     float* qon = lds + P::OFF_Q;               // [TMAX][16][4]
     float* qtg = qon + P::TMAX * P::S * 4;     // [16][4]
-    if (A.double_dqn) {  // (vanilla DQN needs no online Q of s')
+    if (A.double_dqn && role != 1) {  // (vanilla DQN needs no online Q of s')
         P::stage(A.on, lds, R);  // (starts with __syncthreads: the s' boards are visible)
         for (int k = 0; k < T; ++k)
             P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qon + k * P::S * 4);
+    }
+    if (role == 0) {  // a* of every sample for the train launch
+        for (int k = 0; k < T; ++k) {
+            const int64_t b = (grp + (int64_t)k * G) * P::S + t;
+            if (t < P::S && b < A.batch) A.astar[b] = argmax4_first(qon + (k * P::S + t) * 4);
+        }
+        return;
     }
     P::stage(A.tg, lds, R);
     for (int k = 0; k < T; ++k) {
         P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qtg);
         const int sm = t >> 2;  // sample of this thread (t < 64, t & 3 == 0)
-        const int64_t b = (blockIdx.x + (int64_t)k * gridDim.x) * P::S + sm;
+        const int64_t b = (grp + (int64_t)k * G) * P::S + sm;
         if (t < P::S * 4 && (t & 3) == 0 && b < A.batch) {
-#pragma clang fp contract(off)
-            const float* qo = qon + (k * P::S + sm) * 4;
             const float* qt = qtg + sm * 4;
-            float next;
-            if (A.double_dqn) {
-                int a = 0;
-                float best = qo[0];
-                for (int e = 1; e < 4; ++e)
-                    if (qo[e] > best) { best = qo[e]; a = e; }
-                next = qt[a];
-            } else {
-                next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
-            }
             const float disc = (float)(1 - (int)dv[k]) * A.gamma;
-            A.y[b] = (float)rv[k] + disc * next;
+            if (role == 1) {
+                A.qtg[b] = make_float4(qt[0], qt[1], qt[2], qt[3]);
+                A.rdisc[b] = make_float2((float)rv[k], disc);
+            } else {
+                const float next = A.double_dqn ? qt[argmax4_first(qon + (k * P::S + sm) * 4)]
+                                                : fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+                A.y[b] = g2048::cnet::bellman_y((float)rv[k], disc, next);
+            }
         }
         // qtg is rewritten by the next tile only after that tile's internal barriers
     }
@@ -473,15 +502,14 @@ extern "C" G2048_API int g2048_convnet_forward_greedy(const g2048_convnet_params
                                         hipGetErrorString(e));
 }
 
-extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,
-                                               const g2048_convnet_params* target,
-                                               g2048_replay* rb, const int64_t* idx_in,
-                                               int64_t batch, uint64_t seed,
-                                               const uint64_t* epoch_dev, float gamma,
-                                               int double_dqn, int64_t* idx_out, float* y_out,
-                                               void* stream) {
-    if (!online || !target || !rb || batch <= 0 || !idx_out || !y_out || (!idx_in && !epoch_dev))
-        return g2048_fail(G2048_EINVAL, "convnet_targets: NULL argument or batch <= 0");
+// Shared by g2048_convnet_targets (y_out) and g2048_convnet_update (g2048_qtrain.hip: split
+// roles when split_ws is given -- a* i32[B] | Q_target f32[B][4] | (r, disc) f32[B][2]).
+extern "C" int g2048_conv_targets_launch(const g2048_convnet_params* online,
+                                         const g2048_convnet_params* target, g2048_replay* rb,
+                                         const int64_t* idx_in, int64_t batch, uint64_t seed,
+                                         const uint64_t* epoch_dev, float gamma, int double_dqn,
+                                         int64_t* idx_out, float* y_out, float* split_ws,
+                                         void* stream) {
     uint8_t *s2 = nullptr, *d = nullptr;
     int32_t* r = nullptr;
     uint64_t* count = nullptr;
@@ -505,12 +533,38 @@ extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* onlin
     A.double_dqn = double_dqn;
     A.idx_out = idx_out;
     A.y = y_out;
+    A.astar = nullptr;
+    A.qtg = nullptr;
+    A.rdisc = nullptr;
     const int64_t ntiles = (batch + persist::S - 1) / persist::S;
-    int64_t grid = ntiles < 256 ? ntiles : 256;
-    if (grid * persist::TMAX < ntiles) grid = (ntiles + persist::TMAX - 1) / persist::TMAX;
+    int64_t grid;
+    if (split_ws && double_dqn) {  // 2 x G workgroups, G <= 128 so both halves fit the 256 CUs
+        int64_t G = ntiles < 128 ? ntiles : 128;
+        if (G * persist::TMAX < ntiles) G = (ntiles + persist::TMAX - 1) / persist::TMAX;
+        A.astar = reinterpret_cast<int32_t*>(split_ws);
+        A.qtg = reinterpret_cast<float4*>(split_ws + g2048::cnet::conv_split_qtg_offset(batch));
+        A.rdisc = reinterpret_cast<float2*>(split_ws + g2048::cnet::conv_split_rd_offset(batch));
+        grid = 2 * G;
+    } else {
+        grid = ntiles < 256 ? ntiles : 256;
+        if (grid * persist::TMAX < ntiles) grid = (ntiles + persist::TMAX - 1) / persist::TMAX;
+    }
     hipLaunchKernelGGL(k_conv_targets_persist, dim3((unsigned)grid), dim3(NT), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_targets: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int g2048_convnet_targets(const g2048_convnet_params* online,
+                                               const g2048_convnet_params* target,
+                                               g2048_replay* rb, const int64_t* idx_in,
+                                               int64_t batch, uint64_t seed,
+                                               const uint64_t* epoch_dev, float gamma,
+                                               int double_dqn, int64_t* idx_out, float* y_out,
+                                               void* stream) {
+    if (!online || !target || !rb || batch <= 0 || !idx_out || !y_out || (!idx_in && !epoch_dev))
+        return g2048_fail(G2048_EINVAL, "convnet_targets: NULL argument or batch <= 0");
+    return g2048_conv_targets_launch(online, target, rb, idx_in, batch, seed, epoch_dev, gamma,
+                                     double_dqn, idx_out, y_out, nullptr, stream);
 }

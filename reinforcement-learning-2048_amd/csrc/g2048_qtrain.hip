@@ -76,7 +76,13 @@ struct TrainArgs {
     const uint8_t* rows;     // replay s rows [*][16]
     const uint8_t* actions;  // replay a [*]
     const int64_t* idx;      // [B]
-    const float* y;          // [B] Bellman targets
+    const float* y;          // [B] Bellman targets (unless the split inputs below are given)
+    // split targets (g2048_convnet_update): y_b = r_b + disc_b * Q_target(s'_b)[a*_b], formed
+    // here from the two halves of the targets launch and written to y_out
+    const int32_t* astar;    // [B] (nullptr: read y)
+    const float4* qtg;       // [B]
+    const float2* rdisc;     // [B]
+    float* y_out;            // [B]
     int64_t batch;
     float* slab;             // [gridDim.x][SLAB]
     float* dm;               // [ntiles][DM_TILE]
@@ -144,7 +150,16 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
             bw[k] = board_word(A, b0, t);
             if (t < S && b0 + t < A.batch) {
                 av[k] = A.actions[A.idx[b0 + t]];
-                yv[k] = A.y[b0 + t];
+                if (A.astar) {
+                    const int a = A.astar[b0 + t];
+                    const float4 q = A.qtg[b0 + t];
+                    const float2 rd = A.rdisc[b0 + t];
+                    const float next = a == 0 ? q.x : a == 1 ? q.y : a == 2 ? q.z : q.w;
+                    yv[k] = bellman_y(rd.x, rd.y, next);
+                    A.y_out[b0 + t] = yv[k];
+                } else {
+                    yv[k] = A.y[b0 + t];
+                }
             }
         }
     }
@@ -675,19 +690,30 @@ static int64_t train_grid(int64_t batch) {
 extern "C" G2048_API int64_t g2048_convnet_train_workspace(int64_t batch) {
     if (batch <= 0) return 0;
     const int64_t ntiles = (batch + S - 1) / S;
-    return train_grid(batch) * SLAB + ntiles * DM_TILE;  // slabs | dM of every tile
+    // slabs | dM of every tile | split-target scratch of g2048_convnet_update
+    return train_grid(batch) * SLAB + ntiles * DM_TILE + conv_split_floats(batch);
+}
+
+static float* split_scratch(float* workspace, int64_t batch) {
+    const int64_t ntiles = (batch + S - 1) / S;
+    return workspace + train_grid(batch) * SLAB + ntiles * DM_TILE;
 }
 
 static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
                         const uint8_t* actions, const int64_t* idx, const float* y, int64_t batch,
                         float* workspace, float* grad_out, float* loss_out, uint64_t* step_dev,
-                        const ReduceAdam& R, void* stream) {
+                        const ReduceAdam& R, void* stream, const float* split = nullptr,
+                        float* y_out = nullptr) {
     TrainArgs A;
     A.W = NetW{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b};
     A.rows = rows;
     A.actions = actions;
     A.idx = idx;
     A.y = y;
+    A.astar = split ? reinterpret_cast<const int32_t*>(split) : nullptr;
+    A.qtg = split ? reinterpret_cast<const float4*>(split + conv_split_qtg_offset(batch)) : nullptr;
+    A.rdisc = split ? reinterpret_cast<const float2*>(split + conv_split_rd_offset(batch)) : nullptr;
+    A.y_out = y_out;
     A.batch = batch;
     A.slab = workspace;
     const int grid = (int)train_grid(batch);
@@ -725,6 +751,66 @@ extern "C" G2048_API int g2048_convnet_train_grad(const g2048_convnet_params* p,
                         R, stream);
 }
 
+static void fill_adam(ReduceAdam& R, const g2048_convnet_params* p,
+                      const g2048_convnet_params* target, uint64_t sync_every, float* m, float* v,
+                      const uint64_t* step_dev, double lr, double beta1, double beta2,
+                      double eps) {
+    memset(&R, 0, sizeof(R));
+    const g2048_convnet_params* nets[2] = {p, sync_every ? target : nullptr};
+    for (int h = 0; h < 2; ++h) {
+        if (!nets[h]) continue;
+        const float* ps[8] = {nets[h]->w1, nets[h]->b1, nets[h]->w2, nets[h]->b2,
+                              nets[h]->fc1_w, nets[h]->fc1_b, nets[h]->fc2_w, nets[h]->fc2_b};
+        for (int k = 0; k < 8; ++k) (h ? R.tp : R.p)[k] = const_cast<float*>(ps[k]);
+    }
+    R.m = m;
+    R.v = v;
+    R.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    R.lr = lr;
+    R.b1 = beta1;
+    R.b2 = beta2;
+    R.eps = eps;
+    R.sync_every = sync_every;
+    R.on = 1;
+}
+
+extern "C" int g2048_conv_targets_launch(const g2048_convnet_params* online,
+                                         const g2048_convnet_params* target, g2048_replay* rb,
+                                         const int64_t* idx_in, int64_t batch, uint64_t seed,
+                                         const uint64_t* epoch_dev, float gamma, int double_dqn,
+                                         int64_t* idx_out, float* y_out, float* split_ws,
+                                         void* stream);
+
+extern "C" G2048_API int g2048_convnet_update(
+    const g2048_convnet_params* online, const g2048_convnet_params* target, g2048_replay* rb,
+    const int64_t* idx_in, int64_t batch, uint64_t seed, uint64_t* step_dev, float gamma,
+    int double_dqn, int64_t* idx_out, float* y_out, float* workspace, float* grad_out,
+    float* loss_out, float* exp_avg, float* exp_avg_sq, double lr, double beta1, double beta2,
+    double eps, uint64_t sync_every, void* stream) {
+    if (!ok_params(online) || !ok_params(target) || !rb || batch <= 0 || !step_dev ||
+        !idx_out || !y_out || !workspace)
+        return g2048_fail(G2048_EINVAL, "convnet_update: NULL argument or batch <= 0");
+    const bool adam = exp_avg && exp_avg_sq;
+    if (!adam && !grad_out)
+        return g2048_fail(G2048_EINVAL, "convnet_update: no Adam state and no grad_out");
+    uint8_t* s = nullptr;
+    uint8_t* a = nullptr;
+    if (g2048_replay_views(rb, &s, nullptr, &a, nullptr, nullptr, nullptr) != G2048_OK)
+        return G2048_EINVAL;
+    float* split = double_dqn ? split_scratch(workspace, batch) : nullptr;
+    int rc = g2048_conv_targets_launch(online, target, rb, idx_in, batch, seed, step_dev, gamma,
+                                       double_dqn, idx_out, y_out, split, stream);
+    if (rc != G2048_OK) return rc;
+    ReduceAdam R;
+    if (adam)
+        fill_adam(R, online, target, sync_every, exp_avg, exp_avg_sq, step_dev, lr, beta1, beta2,
+                  eps);
+    else
+        memset(&R, 0, sizeof(R));
+    return train_launch(online, s, a, idx_out, y_out, batch, workspace, grad_out, loss_out,
+                        step_dev, R, stream, split, split ? y_out : nullptr);
+}
+
 extern "C" G2048_API int g2048_convnet_train_adam(
     const g2048_convnet_params* p, const uint8_t* rows, const uint8_t* actions,
     const int64_t* idx, const float* y, int64_t batch, float* workspace, float* grad_out,
@@ -737,23 +823,7 @@ extern "C" G2048_API int g2048_convnet_train_adam(
     if (sync_every && !ok_params(target))
         return g2048_fail(G2048_EINVAL, "convnet_train_adam: sync_every > 0 needs the target net");
     ReduceAdam R;
-    memset(&R, 0, sizeof(R));
-    const g2048_convnet_params* nets[2] = {p, sync_every ? target : nullptr};
-    for (int h = 0; h < 2; ++h) {
-        if (!nets[h]) continue;
-        const float* ps[8] = {nets[h]->w1, nets[h]->b1, nets[h]->w2, nets[h]->b2,
-                              nets[h]->fc1_w, nets[h]->fc1_b, nets[h]->fc2_w, nets[h]->fc2_b};
-        for (int k = 0; k < 8; ++k) (h ? R.tp : R.p)[k] = const_cast<float*>(ps[k]);
-    }
-    R.m = exp_avg;
-    R.v = exp_avg_sq;
-    R.step = reinterpret_cast<const unsigned long long*>(step_dev);
-    R.lr = lr;
-    R.b1 = beta1;
-    R.b2 = beta2;
-    R.eps = eps;
-    R.sync_every = sync_every;
-    R.on = 1;
+    fill_adam(R, p, target, sync_every, exp_avg, exp_avg_sq, step_dev, lr, beta1, beta2, eps);
     return train_launch(p, rows, actions, idx, y, batch, workspace, grad_out, loss_out, step_dev,
                         R, stream);
 }

@@ -68,6 +68,8 @@ SIGNATURES = {
     "g2048_dense64_update_workspace": (_i64, [_i64]),
     "g2048_dense64_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
+    "g2048_convnet_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
     "g2048_astar_search": (_int, [_vp, _i64, _int, _u64, _u64, _int, _i64, _i64, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp]),
     "g2048_last_error": (C.c_char_p, []),

@@ -68,10 +68,10 @@ class DQNLearner:
         if self.fused:
             self._p_on = qnet.net_params(self.model)
             self._p_tgt = qnet.net_params(self.target)
-            # graded half (forward + MSE + backward) as one HIP launch + a slab reduction that
-            # writes the flat gradient bucket directly (csrc/g2048_qtrain.hip); targets (sampler,
-            # both target-side forwards, Bellman) as one launch; Adam as one launch.  The device
-            # update counter is the sampler epoch and Adam's t (bumped by the train launch).
+            # targets (sampler, both target-side forwards, Bellman), the graded half (forward +
+            # MSE + backward) and a fixed-order slab reduction that writes the flat gradient
+            # bucket or applies Adam (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip).  The
+            # device update counter is the sampler epoch and Adam's t (bumped by the train launch).
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
@@ -80,16 +80,13 @@ class DQNLearner:
             # the device update counter: no host decision between graph replays
             if self.target_sync_every:
                 self._adam.attach_target(list(self.target.parameters()), self.target_sync_every)
-            # conv, single process: Adam (+ target sync) folded into the gradient reduction --
-            # targets, train, reduce+Adam = 3 launches per update
-            self._fold_adam = self.kind == "conv" and self.world == 1
-            self._train_grad = qnet.TrainGrad(self.model, self.B,
-                                              adam=self._adam if self._fold_adam else None)
-            # dense64: sampler + targets + gradient in ONE launch, and (single process) Adam
-            # folded into the gradient reduction -- 2 launches per update
-            self._upd = (qnet.Dense64Update(self.model, self.target, self.B,
-                                            adam=self._adam if self.world == 1 else None)
-                         if self.kind == "dense64" else None)
+            # one whole update per call; single process: Adam (+ target sync) folded into the
+            # gradient reduction.  conv: targets (two half-grids, one net each), train forward,
+            # train backward, reduce+Adam = 4 launches; dense64: sampler + targets + gradient in
+            # ONE launch + reduce+Adam = 2 launches
+            upd = qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate
+            self._upd = upd(self.model, self.target, self.B,
+                            adam=self._adam if self.world == 1 else None)
             rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
             self.sample_seed = (int(seed) * 0x9E3779B9 + 0x2048 + (rank << 40)) & ((1 << 64) - 1)
 
@@ -109,16 +106,9 @@ class DQNLearner:
         idx = None if self.fused else self._sample_idx()
         if self.fused:
             idx_in = self.sampler(self.B, self.replay) if self.sampler is not None else None
-            if self._upd is not None:
-                self._upd(self.replay, self._idx, self._y, self.step_dev, self.gamma,
-                          self.use_double_dqn, self.sample_seed, idx_in,
-                          grad_out=self.grad_flat, loss_out=self.last_loss)
-                return
-            qnet.targets(self.kind, self._p_on, self._p_tgt, self.replay, self.B, self._idx,
-                         self._y, self.gamma, self.use_double_dqn, self.sample_seed, self.step_dev,
-                         idx_in)
-            self._train_grad(self.replay.s, self.replay.a, self._idx, self._y, self.grad_flat,
-                             self.last_loss, self.step_dev)
+            self._upd(self.replay, self._idx, self._y, self.step_dev, self.gamma,
+                      self.use_double_dqn, self.sample_seed, idx_in,
+                      grad_out=self.grad_flat, loss_out=self.last_loss)
             return
         else:
             s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
@@ -133,9 +123,7 @@ class DQNLearner:
 
     def _apply(self):
         if self._upd is not None and self._upd.adam is not None:
-            return  # applied inside the dense64 update's reduction
-        if self.fused and self._fold_adam:
-            return  # applied inside the conv gradient reduction
+            return  # applied inside the update's gradient reduction
         if self.fused:
             self._adam.step(self.grad_flat, self.step_dev)
         else:

@@ -169,6 +169,40 @@ class TrainGrad:
 ConvTrainGrad = TrainGrad
 
 
+class ConvUpdate:
+    """One whole Double-DQN update of the fp32 conv net (g2048_convnet_update): targets (sampler,
+    both target-side forwards; for Double DQN split over two half-grids that each stage one net)
+    and the train launches, then Adam applied in the gradient reduction (adam given) or the
+    summed gradient left in grad_out (adam=None).  Same call as Dense64Update."""
+
+    def __init__(self, model, target, batch: int, adam=None):
+        if kind_of(model) != "conv" or kind_of(target) != "conv":
+            raise TypeError("ConvUpdate needs the conv net for online and target")
+        self.on, self.tg = net_params(model), net_params(target)
+        self.batch = int(batch)
+        self.adam = adam
+        dev = next(model.parameters()).device
+        n = N.load().g2048_convnet_train_workspace(self.batch)
+        self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
+
+    def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
+                 idx_in=None, grad_out=None, loss_out=None):
+        if idx_out.numel() != self.batch or y_out.numel() != self.batch:
+            raise ValueError("idx_out / y_out must have `batch` elements")
+        if self.adam is None and grad_out is None:
+            raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        a = self.adam
+        m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
+        lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)
+        N.check(N.load().g2048_convnet_update(
+            C.byref(self.on), C.byref(self.tg), replay.handle, N.ptr(idx_in), self.batch,
+            int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)), N.ptr(idx_out),
+            N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(m),
+            N.ptr(v), float(lr), float(b1), float(b2), float(eps),
+            int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
+            "g2048_convnet_update")
+
+
 class Dense64Update:
     """One whole Double-DQN update of an fp32 dense 16-64-4 net in two launches
     (g2048_dense64_update): sampler + both target-side forwards + Bellman + MSE gradient per

@@ -221,6 +221,62 @@ def test_conv_train_adam_equals_grad_then_adam(G, sync_every):
         assert not all(torch.equal(p, q) for p, q in zip(t2.parameters(), nets[0].parameters()))
 
 
+@pytest.mark.parametrize("B,double_dqn,sampled,adam,sync_every",
+                         [(8192, True, True, True, 2), (2048, True, False, True, 0),
+                          (1000, False, True, True, 3), (8192, True, True, False, 0),
+                          (33, True, True, True, 0)])
+def test_conv_update_equals_targets_then_train(G, B, double_dqn, sampled, adam, sync_every):
+    """g2048_convnet_update (Double DQN: the targets launch split into an online half and a
+    target half, y formed in the train launch) is bitwise conv_targets followed by
+    ConvTrainGrad (+ Adam folded in, + target sync) over 3 updates: indices, y, loss, gradient
+    (adam=False), online / target weights and Adam state."""
+    from g2048 import qnet
+    from g2048.nets import make_net
+    from g2048.optim import FusedAdam
+
+    C = 16384
+    rb = _filled_ring(G, 17, C=C)
+    torch.manual_seed(B)
+    nets = [make_net("conv", torch.float32, DEV) for _ in range(4)]
+    with torch.no_grad():  # online pair 0 / 2, target pair 1 / 3 (differs from the online net)
+        nets[2].load_state_dict(nets[0].state_dict())
+        for p, q in zip(nets[1].parameters(), nets[0].parameters()):
+            p.copy_(q * 0.9)
+        nets[3].load_state_dict(nets[1].state_dict())
+    (m1, t1), (m2, t2) = (nets[0], nets[1]), (nets[2], nets[3])
+    a1, a2 = FusedAdam(list(m1.parameters()), lr=1e-2), FusedAdam(list(m2.parameters()), lr=1e-2)
+    if sync_every:
+        a1.attach_target(list(t1.parameters()), sync_every)
+        a2.attach_target(list(t2.parameters()), sync_every)
+    tr1 = qnet.ConvTrainGrad(m1, B, adam=a1 if adam else None)
+    upd = qnet.ConvUpdate(m2, t2, B, adam=a2 if adam else None)
+    p1on, p1tg = qnet.net_params(m1), qnet.net_params(t1)
+    kw = dict(device=DEV)
+    s1, s2 = torch.zeros(1, dtype=torch.int64, **kw), torch.zeros(1, dtype=torch.int64, **kw)
+    i1, i2 = torch.zeros(B, dtype=torch.int64, **kw), torch.zeros(B, dtype=torch.int64, **kw)
+    y1, y2 = torch.zeros(B, **kw), torch.zeros(B, **kw)
+    g1, g2 = torch.zeros(33476, **kw), torch.zeros(33476, **kw)
+    l1, l2 = torch.zeros((), **kw), torch.zeros((), **kw)
+    for it in range(3):
+        idx_in = None if sampled else torch.randint(0, C, (B,), **kw)
+        qnet.conv_targets(p1on, p1tg, rb, B, i1, y1, 0.8, double_dqn, seed=7, epoch=s1,
+                          idx_in=idx_in)
+        tr1(rb.s, rb.a, i1, y1, g1, l1, s1)
+        if not adam:
+            a1.step(g1, s1)
+        upd(rb, i2, y2, s2, 0.8, double_dqn, seed=7, idx_in=idx_in,
+            grad_out=None if adam else g2, loss_out=l2)
+        if not adam:
+            a2.step(g2, s2)
+            assert torch.equal(g1, g2), it
+        assert torch.equal(i1, i2) and torch.equal(y1, y2) and torch.equal(l1, l2), it
+    assert int(s1) == int(s2) == 3
+    for p1, p2 in zip(list(m1.parameters()) + list(t1.parameters()),
+                      list(m2.parameters()) + list(t2.parameters())):
+        assert torch.equal(p1, p2)
+    assert torch.equal(a1.exp_avg, a2.exp_avg) and torch.equal(a1.exp_avg_sq, a2.exp_avg_sq)
+
+
 # ------------------------------------------------------------------ dense 16-64-4 (configs[2])
 def test_dense64_forward_and_targets(G):
     from g2048 import dqn_lib
