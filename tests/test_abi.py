@@ -63,3 +63,19 @@ def test_c_caller_compiles_and_links(tmp_path):
                     os.path.join(ROOT, "examples", "abi_demo.c"), "-L", libdir, "-l:libg2048.so",
                     "-Wl,-rpath," + libdir, "-o", str(tmp_path / "abi_demo")], check=True)
     assert (tmp_path / "abi_demo").exists()
+
+
+def test_entry_points_reject_bad_arguments():
+    """Argument checks run before any device work: NULL / empty arguments come back as
+    G2048_EINVAL with a message (here, without a GPU)."""
+    import g2048._native as N
+
+    lib = N.load()
+    rc = lib.g2048_convnet_update(None, None, None, None, 8192, 0, None, 0.8, 1, None, None, None,
+                                  None, None, None, None, 1e-2, 0.9, 0.999, 1e-8, 0, None)
+    assert rc == N.G2048_EINVAL and b"convnet_update" in lib.g2048_last_error()
+    rc = lib.g2048_convnet_forward_greedy(None, None, None, 0.5, 0.0, 0.0, None, None)
+    assert rc == N.G2048_EINVAL and b"forward_greedy" in lib.g2048_last_error()
+    rc = lib.g2048_convnet_targets(None, None, None, None, 0, 0, None, 0.8, 1, None, None, None)
+    assert rc == N.G2048_EINVAL
+    assert lib.g2048_convnet_train_workspace(0) == 0
