@@ -19,6 +19,9 @@
 //   k_reduce_slabs    fixed-order sum of the slabs (deterministic) -> the flat gradient bucket,
 //                     optionally with Adam folded in.
 //
+// g2048_convnet_update puts the targets launch (g2048_qnet.hip) in front: one whole train_step
+// per call; with Double DQN, k_conv_train_fwd forms y from the targets' online / target halves.
+//
 // dM has to change register layout between the two data-gradient GEMMs (dU contracts over
 // boards, dV over output channels), and U is needed in both orientations; one workgroup cannot
 // hold both (144 VGPRs each), hence the two launches and the 36 KB-per-tile dM round trip.
