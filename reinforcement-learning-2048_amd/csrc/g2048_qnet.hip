@@ -145,9 +145,101 @@ __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R,
 }
 }  // namespace persist
 
-// The rollout's Q over all n boards (g2048_convnet_forward for n >= 16k): 256 workgroups stage
-// the net once and loop over 16-board tiles; the next tile's boards are loaded during the
-// current one.
+// fc2 of a tile straight to global Q: thread (o = t >> 2, part p = t & 3) sums 16 units; the
+// float sequence of tile()'s fc2.
+__device__ __forceinline__ void persist_fc2_store(const float* lds, float* q, int64_t b0,
+                                                  int64_t n) {
+    namespace P = persist;
+    const int t = threadIdx.x;
+    const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
+    const P::f32x4* fr = reinterpret_cast<const P::f32x4*>(lds + P::OFF_F + s * P::FS + 16 * p);
+    const P::f32x4* wr = reinterpret_cast<const P::f32x4*>(lds + P::OFF_WF2 + a * P::WF2S + 16 * p);
+    P::f32x4 pv = P::f32x4{0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const P::f32x4 f = fr[j], w = wr[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
+    }
+    float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    if (p == 0 && b0 + s < n) q[b0 * 4 + o] = v + lds[P::OFF_BF2 + a];
+}
+
+// The same fc2 with board s of the tile at global row c0 + rows[s] (s < nb).
+__device__ __forceinline__ void persist_fc2_scatter(const float* lds, float* q, int64_t c0,
+                                                    const int32_t* rows, int nb) {
+    namespace P = persist;
+    const int t = threadIdx.x;
+    const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
+    const P::f32x4* fr = reinterpret_cast<const P::f32x4*>(lds + P::OFF_F + s * P::FS + 16 * p);
+    const P::f32x4* wr = reinterpret_cast<const P::f32x4*>(lds + P::OFF_WF2 + a * P::WF2S + 16 * p);
+    P::f32x4 pv = P::f32x4{0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const P::f32x4 f = fr[j], w = wr[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
+    }
+    float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    if (p == 0 && s < nb) q[(c0 + rows[s]) * 4 + a] = v + lds[P::OFF_BF2 + a];
+}
+
+// The rollout's Q over all n boards (g2048_convnet_forward): 256 workgroups stage the net once
+// and loop over 16-board tiles, software-pipelined over two barriers per tile instead of four:
+//   [conv2(k) ; fc2(k-1) -> Q]  sync  [fc1(k) ; conv1 + V(k+1)]  sync
+// (V is free once conv2(k) has read it, h2 once fc1(k) has; fc2 reads f, which the next fc1
+// rewrites only after the next sync).  Boards are double-buffered in xs and loaded two tiles
+// ahead.  Same float sequence per board as tile().
+__global__ __launch_bounds__(NT) void k_conv_forward_pipe(ConvNetArgs A) {
+    namespace P = persist;
+    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
+    const int t = threadIdx.x;
+    const NetW W{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2};
+    P::Regs R;
+    const int64_t ntiles = (A.n + P::S - 1) / P::S;
+    const int64_t G = gridDim.x;
+    auto load_word = [&](int64_t tile) -> uint32_t {
+        const int64_t b = tile * P::S + (t >> 2);
+        if (t >= P::S * 4 || tile >= ntiles || b >= A.n) return 0u;
+        return reinterpret_cast<const uint32_t*>(A.rows)[(A.idx ? A.idx[b] : b) * 4 + (t & 3)];
+    };
+    float* xs0 = lds + P::OFF_X;
+    float* xs1 = lds + P::OFF_X + P::S * 16;
+    int64_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    uint32_t w0 = load_word(tile), w1 = load_word(tile + G);
+    P::stage(W, lds, R);
+    if (t < P::S * 4) {
+        P::put_word(xs0, t, w0);
+        P::put_word(xs1, t, w1);
+    }
+    uint32_t wn = load_word(tile + 2 * G);  // boards of the tile after next
+    __syncthreads();
+    P::conv1_v(xs0, lds + P::OFF_V, R);
+    __syncthreads();
+    int64_t prev = -1;  // tile whose fc2 is pending
+    for (int k = 0; tile < ntiles; ++k, tile += G) {
+        P::conv2_h2(lds + P::OFF_V, lds + P::OFF_H2, lds + P::OFF_B2, R);
+        if (prev >= 0) persist_fc2_store(lds, A.q, prev * P::S, A.n);
+        __syncthreads();
+        P::fc1_f(lds + P::OFF_H2, lds + P::OFF_WF1, lds + P::OFF_BF1, lds + P::OFF_F);
+        if (tile + G < ntiles) P::conv1_v((k & 1) ? xs0 : xs1, lds + P::OFF_V, R);
+        // xs of tile k is free: it takes the tile after next
+        if (t < P::S * 4) P::put_word((k & 1) ? xs1 : xs0, t, wn);
+        wn = load_word(tile + 3 * G);
+        __syncthreads();
+        prev = tile;
+    }
+    persist_fc2_store(lds, A.q, prev * P::S, A.n);
+}
+
+// The rollout's Q over all n boards (earlier form, kept for tools/prof_forward.hip's per-phase
+// probes): 256 workgroups stage the net once and loop over 16-board tiles; the next tile's
+// boards are loaded during the current one.
 __global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
     namespace P = persist;
     __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
@@ -212,8 +304,8 @@ __global__ __launch_bounds__(NT) void k_conv_forward_greedy(GreedyArgs G) {
     const int64_t c0 = (int64_t)blockIdx.x * G.chunk;
     const int64_t c1 = c0 + G.chunk < A.n ? c0 + G.chunk : A.n;
     const uint32_t* rows32 = reinterpret_cast<const uint32_t*>(A.rows);
-    float* xs = lds + P::OFF_X;
-    float* qs = lds + P::OFF_Q;
+    float* xs0 = lds + P::OFF_X;
+    float* xs1 = lds + P::OFF_X + P::S * 16;
     // word t & 3 of board t >> 2 of the tile at queue[h], nb boards (thread t < 64)
     auto load_word = [&](int h, int nb) -> uint32_t {
         if (t >= P::S * 4 || (t >> 2) >= nb) return 0u;
@@ -264,26 +356,37 @@ __global__ __launch_bounds__(NT) void k_conv_forward_greedy(GreedyArgs G) {
         }
         qn = base;
         __syncthreads();
-        auto runnable = [&](int h) { return qn - h >= P::S || (last && qn - h > 0); };
-        if (!runnable(0)) continue;  // < 16 selected so far: carried as they are
-        int h = 0;
-        uint32_t next_word = load_word(0, qn < P::S ? qn : P::S);
+        // the window's tiles: full ones, plus the partial rest in the last window
+        const int nt = last ? (qn + P::S - 1) / P::S : qn / P::S;
+        if (nt == 0) continue;  // < 16 selected so far: carried as they are
+        auto nb_of = [&](int j) { return qn - j * P::S < P::S ? qn - j * P::S : P::S; };
+        auto word_of = [&](int j) -> uint32_t { return j < nt ? load_word(j * P::S, nb_of(j)) : 0u; };
+        // pipelined as k_conv_forward_pipe: [conv2(j) ; fc2(j-1) -> Q] sync [fc1(j) ; conv1(j+1)]
+        const uint32_t wa = word_of(0), wb = word_of(1);
         if (!staged) {
             P::stage(W, lds, R);
             staged = true;
         }
-        while (true) {
-            const int nb = qn - h < P::S ? qn - h : P::S;
-            if (t < P::S * 4) P::put_word(xs, t, next_word);
-            __syncthreads();
-            const int h2 = h + nb;
-            if (runnable(h2)) next_word = load_word(h2, qn - h2 < P::S ? qn - h2 : P::S);
-            P::tile(xs, lds, R, qs);
-            if (t < P::S * 4 && (t >> 2) < nb)
-                A.q[(c0 + queue[h + (t >> 2)]) * 4 + (t & 3)] = qs[t];
-            h = h2;
-            if (!runnable(h)) break;
+        if (t < P::S * 4) {
+            P::put_word(xs0, t, wa);
+            P::put_word(xs1, t, wb);
         }
+        uint32_t wn = word_of(2);
+        __syncthreads();
+        P::conv1_v(xs0, lds + P::OFF_V, R);
+        __syncthreads();
+        for (int j = 0; j < nt; ++j) {
+            P::conv2_h2(lds + P::OFF_V, lds + P::OFF_H2, lds + P::OFF_B2, R);
+            if (j > 0) persist_fc2_scatter(lds, A.q, c0, queue + (j - 1) * P::S, nb_of(j - 1));
+            __syncthreads();
+            P::fc1_f(lds + P::OFF_H2, lds + P::OFF_WF1, lds + P::OFF_BF1, lds + P::OFF_F);
+            if (j + 1 < nt) P::conv1_v((j & 1) ? xs0 : xs1, lds + P::OFF_V, R);
+            if (t < P::S * 4) P::put_word((j & 1) ? xs1 : xs0, t, wn);
+            wn = word_of(j + 3);
+            __syncthreads();
+        }
+        persist_fc2_scatter(lds, A.q, c0, queue + (nt - 1) * P::S, nb_of(nt - 1));
+        const int h = qn < nt * P::S ? qn : nt * P::S;
         const int rem = qn - h;  // < 16 (0 after the last window)
         const int v = t < rem ? queue[h + t] : 0;
         __syncthreads();
@@ -457,7 +560,7 @@ extern "C" G2048_API int g2048_convnet_forward(const g2048_convnet_params* p, co
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const int64_t tiles16 = (n + persist::S - 1) / persist::S;
     const unsigned grid = (unsigned)(tiles16 < 256 ? tiles16 : 256);  // one workgroup per CU
-    hipLaunchKernelGGL(k_conv_forward_persist, dim3(grid), dim3(NT), 0, st, A);
+    hipLaunchKernelGGL(k_conv_forward_pipe, dim3(grid), dim3(NT), 0, st, A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_forward: %s", hipGetErrorString(e));
