@@ -75,8 +75,8 @@ constexpr int OFF_WF1 = OFF_BF2 + 4;              // [64][WF1S]
 constexpr int OFF_V = OFF_WF1 + 64 * WF1S;        // [9][S][VS]
 constexpr int OFF_H2 = OFF_V + 9 * VXI;
 constexpr int OFF_F = OFF_H2 + S * H2S;
-constexpr int OFF_Q = OFF_F + S * FS;             // [TMAX + 1][S][4] Q of a tile
-constexpr int FLOATS = OFF_Q + (TMAX + 1) * S * 4;
+constexpr int OFF_Q = OFF_F + S * FS;             // [2 TMAX][S][4] Q of the tiles (two nets)
+constexpr int FLOATS = OFF_Q + 2 * TMAX * S * 4;
 static_assert(OFF_WF1 % 4 == 0 && OFF_V % 4 == 0 && OFF_H2 % 4 == 0 && OFF_F % 4 == 0 &&
                   OFF_WF2 % 4 == 0 && OFF_Q % 4 == 0,
               "b128 alignment");
@@ -142,6 +142,42 @@ __device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R,
     }
     __syncthreads();
     PHASE(3);
+}
+// fc2 of the tile whose f is in LDS -> qs[16][4] (LDS), the float sequence of tile()'s fc2.
+__device__ __forceinline__ void fc2_lds(const float* lds, float* qs) {
+    const int t = threadIdx.x;
+    const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
+    const f32x4* fr = reinterpret_cast<const f32x4*>(lds + OFF_F + s * FS + 16 * p);
+    const f32x4* wr = reinterpret_cast<const f32x4*>(lds + OFF_WF2 + a * WF2S + 16 * p);
+    f32x4 pv = f32x4{0};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const f32x4 f = fr[j], w = wr[j];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
+    }
+    float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
+    v += __shfl_xor(v, 1);
+    v += __shfl_xor(v, 2);
+    if (p == 0) qs[o] = v + lds[OFF_BF2 + a];
+}
+
+// Q of T >= 1 tiles whose boards sit in xs (tile k at k*S*16; visible, net staged) -> qdst + k*S*4,
+// pipelined as k_conv_forward_pipe (two barriers per tile).  Ends with __syncthreads().
+__device__ __forceinline__ void tiles_pipe(float* lds, const Regs& R, int T, float* qdst) {
+    const float* xs = lds + OFF_X;
+    conv1_v(xs, lds + OFF_V, R);
+    __syncthreads();
+    for (int k = 0; k < T; ++k) {
+        conv2_h2(lds + OFF_V, lds + OFF_H2, lds + OFF_B2, R);
+        if (k > 0) fc2_lds(lds, qdst + (k - 1) * S * 4);
+        __syncthreads();
+        fc1_f(lds + OFF_H2, lds + OFF_WF1, lds + OFF_BF1, lds + OFF_F);
+        if (k + 1 < T) conv1_v(xs + (k + 1) * S * 16, lds + OFF_V, R);
+        __syncthreads();
+    }
+    fc2_lds(lds, qdst + (T - 1) * S * 4);
+    __syncthreads();
 }
 }  // namespace persist
 
@@ -452,6 +488,7 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
     const int64_t ntiles = (A.batch + P::S - 1) / P::S;
     int T = 0;
     for (int64_t tl = grp; tl < ntiles && T < P::TMAX; tl += G) ++T;
+    if (T == 0) return;  // (uniform; the host sizes the grid so that it does not happen)
     // sampler: thread t < 64 owns word t&3 of sample t>>2 of every tile; it draws the sample's
     // ring row itself (same draw as k_sample / o2048_replay_sample_f64, domain 3; the four
     // threads of a sample agree) and loads that word of s' at once
@@ -501,11 +538,10 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
     }
     P::Regs R;
     float* qon = lds + P::OFF_Q;               // [TMAX][16][4]
-    float* qtg = qon + P::TMAX * P::S * 4;     // [16][4]
+    float* qtg = qon + P::TMAX * P::S * 4;     // [TMAX][16][4]
     if (A.double_dqn && role != 1) {  // (vanilla DQN needs no online Q of s')
         P::stage(A.on, lds, R);  // (starts with __syncthreads: the s' boards are visible)
-        for (int k = 0; k < T; ++k)
-            P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qon + k * P::S * 4);
+        P::tiles_pipe(lds, R, T, qon);
     }
     if (role == 0) {  // a* of every sample for the train launch
         for (int k = 0; k < T; ++k) {
@@ -515,12 +551,12 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
         return;
     }
     P::stage(A.tg, lds, R);
+    P::tiles_pipe(lds, R, T, qtg);
     for (int k = 0; k < T; ++k) {
-        P::tile(lds + P::OFF_X + k * P::S * 16, lds, R, qtg);
         const int sm = t >> 2;  // sample of this thread (t < 64, t & 3 == 0)
         const int64_t b = (grp + (int64_t)k * G) * P::S + sm;
         if (t < P::S * 4 && (t & 3) == 0 && b < A.batch) {
-            const float* qt = qtg + sm * 4;
+            const float* qt = qtg + (k * P::S + sm) * 4;
             const float disc = (float)(1 - (int)dv[k]) * A.gamma;
             if (role == 1) {
                 A.qtg[b] = make_float4(qt[0], qt[1], qt[2], qt[3]);
@@ -531,7 +567,6 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
                 A.y[b] = g2048::cnet::bellman_y((float)rv[k], disc, next);
             }
         }
-        // qtg is rewritten by the next tile only after that tile's internal barriers
     }
 }
 

@@ -173,7 +173,7 @@ int main(int argc, char** argv) {
         const unsigned long long hc = C;
         (void)hipMemcpy(cnt, &hc, 8, hipMemcpyHostToDevice);
         for (long i = 0; i < 16; ++i) (void)hipMemcpy(s2 + i * n * 16, rows, n * 16 > C * 16 - i * n * 16 ? 0 : n * 16, hipMemcpyDeviceToDevice);
-        TargetArgs T;
+        TargetArgs T{};  // (no split outputs: each workgroup runs both nets)
         T.on = NetW{w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
         T.tg = T.on;
         T.s2 = s2;
@@ -198,6 +198,20 @@ int main(int argc, char** argv) {
             (void)hipEventElapsedTime(&ms, a, b);
         }
         printf("targets B=%d  %.2f us/launch\n", B, ms * 1e3 / 20);
+        float* split;  // split roles: 128 online + 128 target workgroups
+        (void)hipMalloc(&split, g2048::cnet::conv_split_floats(B) * 4);
+        T.astar = reinterpret_cast<int32_t*>(split);
+        T.qtg = reinterpret_cast<float4*>(split + g2048::cnet::conv_split_qtg_offset(B));
+        T.rdisc = reinterpret_cast<float2*>(split + g2048::cnet::conv_split_rd_offset(B));
+        for (int rep = 0; rep < 2; ++rep) {
+            (void)hipEventRecord(a, nullptr);
+            for (int it = 0; it < 20; ++it)
+                hipLaunchKernelGGL(k_conv_targets_persist, dim3(256), dim3(NT), 0, nullptr, T);
+            (void)hipEventRecord(b, nullptr);
+            (void)hipEventSynchronize(b);
+            (void)hipEventElapsedTime(&ms, a, b);
+        }
+        printf("targets B=%d split  %.2f us/launch\n", B, ms * 1e3 / 20);
     }
     return 0;
 }
