@@ -707,7 +707,7 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
                         float* workspace, float* grad_out, float* loss_out, uint64_t* step_dev,
                         const ReduceAdam& R, void* stream, const float* split = nullptr,
                         float* y_out = nullptr) {
-    TrainArgs A;
+    TrainArgs A{};
     A.W = NetW{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b};
     A.rows = rows;
     A.actions = actions;
