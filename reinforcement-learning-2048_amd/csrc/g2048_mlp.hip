@@ -78,7 +78,30 @@ __device__ __forceinline__ void stage_boards(Tile<S>& T, const uint8_t* rows, co
     put_word(T.x + s * XS + w * 4, v);
 }
 
-// weights + boards staged (caller syncs); leaves h (post-ReLU) and q in LDS, ends with a sync
+// Q = h W2^T + b2 over the tile (h post-ReLU in LDS, visible); ends with a sync.
+template <int S>
+__device__ __forceinline__ void layer2_tile(Tile<S>& T, const LW& W) {
+    const int t = threadIdx.x;
+    if (t < 4 * S) {
+        const int s = t >> 2, a = t & 3;
+        const float4* hr = reinterpret_cast<const float4*>(T.h + s * HS);
+        const float4* wr = reinterpret_cast<const float4*>(W.w2 + a * W2S);
+        float e = W.b2[a], o = 0.f;  // even / odd j, same order as k_step_dense64
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const float4 hv = hr[u], wv = wr[u];
+            e = fmaf(wv.x, hv.x, e);
+            o = fmaf(wv.y, hv.y, o);
+            e = fmaf(wv.z, hv.z, e);
+            o = fmaf(wv.w, hv.w, o);
+        }
+        T.q[t] = e + o;
+    }
+    __syncthreads();
+}
+
+// weights + boards staged (caller syncs); leaves h (post-ReLU) and q in LDS, ends with a sync.
+// VALU, in the float order of the fused step kernel (the rollout forward).
 template <int S>
 __device__ __forceinline__ void forward_tile(Tile<S>& T, const LW& W) {
     const int t = threadIdx.x;
@@ -109,22 +132,40 @@ __device__ __forceinline__ void forward_tile(Tile<S>& T, const LW& W) {
         }
     }
     __syncthreads();
-    if (t < 4 * S) {
-        const int s = t >> 2, a = t & 3;
-        const float4* hr = reinterpret_cast<const float4*>(T.h + s * HS);
-        const float4* wr = reinterpret_cast<const float4*>(W.w2 + a * W2S);
-        float e = W.b2[a], o = 0.f;  // even / odd j, same order as k_step_dense64
+    layer2_tile<S>(T, W);
+}
+
+// ---- MFMA form of layer 1 for the learner kernels (targets, gradient).  v_mfma_f32_16x16x4_f32:
+// lane (l16 = lane & 15, g = lane >> 4) supplies A[m = l16][k = g] and B[k = g][n = l16]; D lane
+// holds D[m = 4g + i][n = l16].  Wave w owns hidden units 16w .. 16w+15; the K index of step u is
+// input 4g + u, so a lane's A (its board's inputs) and B (its unit's weights) are float4s.
+typedef float f32x4m __attribute__((ext_vector_type(4)));
+
+// this lane's layer-1 weights W1[16w + l16][4g .. 4g+3] (registers, from global)
+__device__ __forceinline__ float4 w1_lane(const MlpW& W) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    return reinterpret_cast<const float4*>(W.w1)[(16 * wave + (lane & 15)) * 4 + (lane >> 4)];
+}
+
+// h = relu(x W1^T + b1) on MFMA, then layer 2 as forward_tile.  Ends with a sync.
+template <int S>
+__device__ __forceinline__ void forward_tile_mfma(Tile<S>& T, const LW& W, float4 w1v) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l16 = lane & 15;
+    const int j = 16 * wave + l16;
+    const float bj = W.b1[j];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const float4 hv = hr[u], wv = wr[u];
-            e = fmaf(wv.x, hv.x, e);
-            o = fmaf(wv.y, hv.y, o);
-            e = fmaf(wv.z, hv.z, e);
-            o = fmaf(wv.w, hv.w, o);
-        }
-        T.q[t] = e + o;
+    for (int mb = 0; mb < S / 16; ++mb) {
+        const float4 xv = *reinterpret_cast<const float4*>(T.x + (16 * mb + l16) * XS + 4 * g);
+        f32x4m acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.x, w1v.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.y, w1v.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.z, w1v.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xv.w, w1v.w, acc, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T.h[(16 * mb + 4 * g + i) * HS + j] = fmaxf(acc[i] + bj, 0.f);
     }
     __syncthreads();
+    layer2_tile<S>(T, W);
 }
 
 // Double-DQN target of board t of the tile (src/dqn_lib.py:125-132): qo = Q_online(s'),
@@ -157,15 +198,16 @@ __device__ __forceinline__ int64_t sample_row(int64_t b, unsigned long long ep,
 }
 
 struct GradAcc {  // per-thread gradient accumulators, persistent across a workgroup's tiles
-    float w1[4] = {0.f, 0.f, 0.f, 0.f};
+    f32x4m w1a = {0.f, 0.f, 0.f, 0.f};  // dW1[16w + 4g + i][l16], even / odd K-steps
+    f32x4m w1b = {0.f, 0.f, 0.f, 0.f};
     float b1 = 0.f, w2 = 0.f, b2 = 0.f, loss = 0.f;
 };
 
 // forward + MSE + backward of one staged tile (x, a, y and the validity mask g in LDS, synced)
 template <int S>
-__device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, GradAcc& G) {
+__device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, float4 w1v, GradAcc& G) {
     const int t = threadIdx.x;
-    forward_tile<S>(T, W);
+    forward_tile_mfma<S>(T, W, w1v);
     if (t < S) {  // loss and dq = 2 (q - y) at the taken action
         const float d = (T.q[t * 4 + (int)T.a[t]] - T.y[t]) * T.g[t];
         G.loss = fmaf(d, d, G.loss);
@@ -196,16 +238,17 @@ __device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, GradAcc& G) {
         }
     }
     __syncthreads();
-    {  // dW1[j][i0..i0+3]: thread (j = t>>2, i0 = 4*(t&3)); db1 by threads j < 64
-        const int j = t >> 2, i0 = (t & 3) * 4;
-#pragma unroll 8
-        for (int s = 0; s < S; ++s) {
-            const float dh = T.h[s * HS + j];
-            const float4 xv = *reinterpret_cast<const float4*>(T.x + s * XS + i0);
-            G.w1[0] = fmaf(dh, xv.x, G.w1[0]);
-            G.w1[1] = fmaf(dh, xv.y, G.w1[1]);
-            G.w1[2] = fmaf(dh, xv.z, G.w1[2]);
-            G.w1[3] = fmaf(dh, xv.w, G.w1[3]);
+    {  // dW1 += dh^T x on MFMA (m = unit, n = input, k = board: 4 boards per step, two chains);
+       // db1 by threads j < 64
+        const int lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
+        const float* hc = T.h + 16 * wave + l16;
+        const float* xc = T.x + l16;
+#pragma unroll
+        for (int st = 0; st < S / 4; st += 2) {
+            G.w1a = __builtin_amdgcn_mfma_f32_16x16x4f32(hc[(4 * st + g) * HS], xc[(4 * st + g) * XS],
+                                                         G.w1a, 0, 0, 0);
+            G.w1b = __builtin_amdgcn_mfma_f32_16x16x4f32(hc[(4 * st + 4 + g) * HS],
+                                                         xc[(4 * st + 4 + g) * XS], G.w1b, 0, 0, 0);
         }
         if (t < H) {
             float v = 0.f;
@@ -220,10 +263,10 @@ __device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, GradAcc& G) {
 template <int S>
 __device__ __forceinline__ void write_slab(const GradAcc& G, Tile<S>& T, float* slab) {
     const int t = threadIdx.x;
-    {
-        const int j = t >> 2, i0 = (t & 3) * 4;
+    {  // dW1[16w + 4g + i][l16]
+        const int lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) slab[P_W1 + j * 16 + i0 + u] = G.w1[u];
+        for (int i = 0; i < 4; ++i) slab[P_W1 + (16 * wave + 4 * g + i) * 16 + l16] = G.w1a[i] + G.w1b[i];
     }
     if (t < H) slab[P_B1 + t] = G.b1;
     slab[P_W2 + t] = G.w2;  // t = a*64 + j
@@ -292,15 +335,16 @@ __global__ __launch_bounds__(NT) void k_mlp_targets(TargetArgs A) {
         }
         sidx[t] = j;
     }
+    const float4 w1on = w1_lane(A.on), w1tg = w1_lane(A.tg);
     stage_weights(A.on, W);
     __syncthreads();
     stage_boards<S>(T, A.s2, sidx, 0, S);
     __syncthreads();
-    forward_tile<S>(T, W);
+    forward_tile_mfma<S>(T, W, w1on);
     qon[t] = T.q[t];
     stage_weights(A.tg, W);  // forward_tile ended with a sync: the online weights are dead
     __syncthreads();
-    forward_tile<S>(T, W);
+    forward_tile_mfma<S>(T, W, w1tg);
     if (t < S && b0 + t < A.batch) {
         const int64_t j = sidx[t];
         A.y[b0 + t] = bellman(qon + t * 4, T.q + t * 4, A.r[j], A.d[j], A.gamma, A.double_dqn);
@@ -325,6 +369,7 @@ __global__ __launch_bounds__(NT) void k_mlp_train(TrainArgs A) {
     const int t = threadIdx.x;
     if (A.step && blockIdx.x == 0 && t == 0) *A.step += 1ull;
     stage_weights(A.W, W);
+    const float4 w1v = w1_lane(A.W);
     GradAcc G;
     const int64_t ntiles = (A.batch + S - 1) / S;
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -339,7 +384,7 @@ __global__ __launch_bounds__(NT) void k_mlp_train(TrainArgs A) {
             T.g[t] = ok ? 1.f : 0.f;
         }
         __syncthreads();
-        grad_tile<S>(T, W, G);
+        grad_tile<S>(T, W, w1v, G);
     }
     write_slab<S>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
 }
@@ -388,6 +433,7 @@ __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
     if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
     stage_weights(A.on, Won);
     stage_weights(A.tg, Wtg);
+    const float4 w1on = w1_lane(A.on), w1tg = w1_lane(A.tg);
     GradAcc G;
     const int64_t ntiles = (A.batch + S - 1) / S;
     const int sl = t >> 2, w = t & 3;  // threads t < 4S: board sl of the tile, word w
@@ -423,9 +469,9 @@ __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
         }
         __syncthreads();
         MPHASE(2);
-        forward_tile<S>(T, Wtg);
+        forward_tile_mfma<S>(T, Wtg, w1tg);
         if (t < 4 * S) qtg[t] = T.q[t];
-        forward_tile<S>(T, Won);
+        forward_tile_mfma<S>(T, Won, w1on);
         if (t < 4 * S && w == 0) {
             const float y = bellman(T.q + sl * 4, qtg + sl * 4, rj, dj, A.gamma, A.double_dqn);
             T.y[sl] = y;
@@ -436,7 +482,7 @@ __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
         if (t < 4 * S) put_word(T.x + sl * XS + w * 4, sw);
         __syncthreads();
         MPHASE(4);
-        grad_tile<S>(T, Won, G);
+        grad_tile<S>(T, Won, w1on, G);
 #ifdef G2048_MLP_PHASE
         __syncthreads();
 #endif
