@@ -32,6 +32,12 @@ using namespace g2048;
 namespace {
 
 constexpr int kBlock = 256;
+// k_step's workgroup below kStepSmallMaxBoards: one wave per workgroup.  At 64k boards the step
+// is bound by its launch floor, and 1 024 one-wave workgroups finish sooner than 256 four-wave
+// ones (tools/blockbench.py, cold process: 2.75 us vs 2.96 us per step; 128: 3.36, 512: 3.24,
+// 1 024: 4.22).  HBM-bound sizes keep 256.
+constexpr int kStepBlockSmall = 64;
+constexpr int64_t kStepSmallMaxBoards = 1 << 20;
 enum : int {
     MODE_ACTIONS = 0,
     MODE_RANDOM = 1,
@@ -212,9 +218,9 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
 
 // kFull: every block is full (n % kBlock == 0), so there is no bounds test and every kernel
 // argument load can be issued at once (with the test, the pointer loads wait for n's round trip).
-template <int MODE, bool kFull, bool kPre>
-__global__ __launch_bounds__(kBlock) void k_step(StepArgs A) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+template <int MODE, bool kFull, bool kPre, int BS>
+__global__ __launch_bounds__(BS) void k_step(StepArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     if (!kFull && i >= A.n) return;
     Board b = load_board(A.board[i]);
     uint4 m = A.meta[i];
@@ -576,10 +582,20 @@ constexpr int64_t kPrefetchMaxBoards = 1 << 18;
 
 template <int MODE, bool kPre>
 void launch_step_k(g2048_env* e, const StepArgs& A, hipStream_t st) {
-    if (e->n % kBlock == 0)
-        hipLaunchKernelGGL((k_step<MODE, true, kPre>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
-    else
-        hipLaunchKernelGGL((k_step<MODE, false, kPre>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+    if (e->n <= kStepSmallMaxBoards) {
+        constexpr int BS = kStepBlockSmall;
+        const unsigned grid = (unsigned)((e->n + BS - 1) / BS);
+        if (e->n % BS == 0)
+            hipLaunchKernelGGL((k_step<MODE, true, kPre, BS>), dim3(grid), dim3(BS), 0, st, A);
+        else
+            hipLaunchKernelGGL((k_step<MODE, false, kPre, BS>), dim3(grid), dim3(BS), 0, st, A);
+    } else if (e->n % kBlock == 0) {
+        hipLaunchKernelGGL((k_step<MODE, true, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock), 0,
+                           st, A);
+    } else {
+        hipLaunchKernelGGL((k_step<MODE, false, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock),
+                           0, st, A);
+    }
 }
 
 template <int MODE>
