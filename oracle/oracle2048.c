@@ -7,6 +7,7 @@
  */
 #include "oracle2048.h"
 
+#include <math.h>
 #include <string.h>
 
 /* ------------------------------------------------------------------ slide / score */
@@ -113,50 +114,53 @@ static void draw(uint64_t seed, uint64_t gid, uint32_t domain, uint64_t t, uint3
 /* ------------------------------------------------------------------ policy */
 
 /* src/dqn_lib.py:25-29.  compat: Qn = Q - min(Q)*max(Q) - min(Q); argmax(avail * Qn), first
- * index on ties (torch.argmax).  fixed: argmax of Q over legal moves only, 0 if none. */
-int o2048_greedy_f64(const double q[4], uint8_t legal, int fixed) {
-    int best = 0;
-    if (fixed) {
-        int found = 0;
-        for (int j = 0; j < 4; ++j) {
-            if (!((legal >> j) & 1)) continue;
-            if (!found || q[j] > q[best]) { best = j; found = 1; }
-        }
-        return best;
+ * index on ties (torch.argmax).  torch semantics for non-finite Q: torch.min / torch.max are NaN
+ * as soon as one element is NaN, and torch.argmax ranks NaN above every number (the FIRST NaN
+ * wins).  0 * inf = NaN and inf - inf = NaN arise from the formula itself.
+ * fixed: argmax of Q over legal moves only, 0 if none. */
+#define O2048_GREEDY(NAME, T)                                                                 \
+    int NAME(const T q[4], uint8_t legal, int fixed) {                                        \
+        int best = 0;                                                                         \
+        if (fixed) {                                                                          \
+            int found = 0;                                                                    \
+            for (int j = 0; j < 4; ++j) {                                                     \
+                if (!((legal >> j) & 1)) continue;                                            \
+                if (!found || q[j] > q[best]) { best = j; found = 1; }                        \
+            }                                                                                 \
+            return best;                                                                      \
+        }                                                                                     \
+        T mn = q[0], mx = q[0];                                                               \
+        int anynan = isnan(q[0]);                                                             \
+        for (int j = 1; j < 4; ++j) {                                                         \
+            if (q[j] < mn) mn = q[j];                                                         \
+            if (q[j] > mx) mx = q[j];                                                         \
+            anynan |= isnan(q[j]);                                                            \
+        }                                                                                     \
+        if (anynan) { mn = (T)NAN; mx = (T)NAN; }                                             \
+        T prod = mn * mx;                                                                     \
+        T bestv = 0;                                                                          \
+        for (int j = 0; j < 4; ++j) {                                                         \
+            T qn = (q[j] - prod) - mn;                                                        \
+            T v = (T)(float)((legal >> j) & 1) * qn;                                          \
+            if (j == 0 || (!isnan(bestv) && (isnan(v) || v > bestv))) { best = j; bestv = v; } \
+        }                                                                                     \
+        return best;                                                                          \
     }
-    double mn = q[0], mx = q[0];
-    for (int j = 1; j < 4; ++j) { if (q[j] < mn) mn = q[j]; if (q[j] > mx) mx = q[j]; }
-    double prod = mn * mx;
-    double bestv = 0;
-    for (int j = 0; j < 4; ++j) {
-        double qn = (q[j] - prod) - mn;
-        double v = (double)(float)((legal >> j) & 1) * qn;
-        if (j == 0 || v > bestv) { best = j; bestv = v; }
-    }
-    return best;
-}
+O2048_GREEDY(o2048_greedy_f64, double)
+O2048_GREEDY(o2048_greedy_f32, float)
 
-int o2048_greedy_f32(const float q[4], uint8_t legal, int fixed) {
-    int best = 0;
-    if (fixed) {
-        int found = 0;
-        for (int j = 0; j < 4; ++j) {
-            if (!((legal >> j) & 1)) continue;
-            if (!found || q[j] > q[best]) { best = j; found = 1; }
-        }
-        return best;
+/* torch.max over the 4 Q values (src/dqn_lib.py:29): NaN if any element is NaN. */
+#define O2048_QMAX(NAME, T)                                                                   \
+    static T NAME(const T q[4]) {                                                             \
+        T m = q[0];                                                                           \
+        for (int j = 1; j < 4; ++j) {                                                         \
+            if (isnan(m)) break;                                                              \
+            m = (isnan(q[j]) || q[j] > m) ? q[j] : m;                                         \
+        }                                                                                     \
+        return m;                                                                             \
     }
-    float mn = q[0], mx = q[0];
-    for (int j = 1; j < 4; ++j) { if (q[j] < mn) mn = q[j]; if (q[j] > mx) mx = q[j]; }
-    float prod = mn * mx;
-    float bestv = 0;
-    for (int j = 0; j < 4; ++j) {
-        float qn = (q[j] - prod) - mn;
-        float v = (float)((legal >> j) & 1) * qn;
-        if (j == 0 || v > bestv) { best = j; bestv = v; }
-    }
-    return best;
-}
+O2048_QMAX(qmax_f64, double)
+O2048_QMAX(qmax_f32, float)
 
 /* ------------------------------------------------------------------ spawn */
 
@@ -248,15 +252,11 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             } else if (mode == 2) {
                 const float* qi = (const float*)q + 4 * i;
                 a = o2048_greedy_f32(qi, legal, fixed);
-                float mq = qi[0];                         /* torch.max(Q), dqn_lib.py:29 */
-                for (int j = 1; j < 4; ++j) mq = qi[j] > mq ? qi[j] : mq;
-                qs += (double)mq;
+                qs += (double)qmax_f32(qi);               /* torch.max(Q), dqn_lib.py:29 */
             } else {
                 const double* qi = (const double*)q + 4 * i;
                 a = o2048_greedy_f64(qi, legal, fixed);
-                double mq = qi[0];
-                for (int j = 1; j < 4; ++j) mq = qi[j] > mq ? qi[j] : mq;
-                qs += mq;
+                qs += qmax_f64(qi);
             }
         }
 

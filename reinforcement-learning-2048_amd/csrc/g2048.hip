@@ -123,13 +123,13 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
             else q = reinterpret_cast<const float4*>(A.q)[i];
             act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
                         : greedy_compat(q.x, q.y, q.z, q.w, legal);
-            qs += (double)fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w));  // torch.max(Q) (:29)
+            qs += (double)qmax4_torch(q.x, q.y, q.z, q.w);  // torch.max(Q) (:29)
         } else {
             const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
             const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
             act = fixed ? greedy_fixed(q01.x, q01.y, q23.x, q23.y, legal)
                         : greedy_compat(q01.x, q01.y, q23.x, q23.y, legal);
-            qs += fmax(fmax(q01.x, q01.y), fmax(q23.x, q23.y));
+            qs += qmax4_torch(q01.x, q01.y, q23.x, q23.y);
         }
     }
 

@@ -257,7 +257,34 @@ __device__ __forceinline__ Board fresh_board(uint4 u, uint32_t p4_thresh) {
 // ------------------------------------------------------------------ policy (src/dqn_lib.py:16-30)
 // compat: Qn = Q - min(Q)*max(Q) - min(Q) (the reference's operator precedence, F5),
 // a = argmax(avail * Qn) with the first index winning ties; no FMA contraction so the products
-// round exactly like torch's separate kernels.
+// round exactly like torch's separate kernels.  Non-finite Q follows torch: torch.min/torch.max
+// are NaN once any element is NaN, 0 * inf and inf - inf are NaN, and torch.argmax ranks NaN
+// above every number (the first NaN wins).
+template <typename T>
+__device__ __forceinline__ bool is_nan(T x) {
+    return __builtin_isnan(x);
+}
+
+// torch.argmax over 4 values: first NaN if any, else the first maximum.
+template <typename T>
+__device__ __forceinline__ uint32_t argmax4_torch(T v0, T v1, T v2, T v3) {
+    uint32_t a = 0;
+    T best = v0;
+    bool bn = is_nan(v0);
+    if (!bn && (is_nan(v1) || v1 > best)) { a = 1; best = v1; bn = is_nan(v1); }
+    if (!bn && (is_nan(v2) || v2 > best)) { a = 2; best = v2; bn = is_nan(v2); }
+    if (!bn && (is_nan(v3) || v3 > best)) { a = 3; }
+    return a;
+}
+
+// torch.max over 4 values (src/dqn_lib.py:29, the Q-sum of the episode log): NaN if any is NaN.
+template <typename T>
+__device__ __forceinline__ T qmax4_torch(T q0, T q1, T q2, T q3) {
+    const T m = q0 > q1 ? q0 : q1, n = q2 > q3 ? q2 : q3;
+    const T mx = m > n ? m : n;
+    return (is_nan(q0) || is_nan(q1) || is_nan(q2) || is_nan(q3)) ? (T)__builtin_nan("") : mx;
+}
+
 template <typename T>
 __device__ __forceinline__ uint32_t greedy_compat(T q0, T q1, T q2, T q3, uint32_t legal) {
 #pragma clang fp contract(off)
@@ -265,17 +292,16 @@ __device__ __forceinline__ uint32_t greedy_compat(T q0, T q1, T q2, T q3, uint32
     mn = q1 < mn ? q1 : mn; mx = q1 > mx ? q1 : mx;
     mn = q2 < mn ? q2 : mn; mx = q2 > mx ? q2 : mx;
     mn = q3 < mn ? q3 : mn; mx = q3 > mx ? q3 : mx;
+    if (is_nan(q0) || is_nan(q1) || is_nan(q2) || is_nan(q3)) {
+        mn = (T)__builtin_nan("");
+        mx = mn;
+    }
     const T prod = mn * mx;
     const T v0 = (T)(legal & 1u) * ((q0 - prod) - mn);
     const T v1 = (T)((legal >> 1) & 1u) * ((q1 - prod) - mn);
     const T v2 = (T)((legal >> 2) & 1u) * ((q2 - prod) - mn);
     const T v3 = (T)((legal >> 3) & 1u) * ((q3 - prod) - mn);
-    uint32_t a = 0;
-    T best = v0;
-    if (v1 > best) { a = 1; best = v1; }
-    if (v2 > best) { a = 2; best = v2; }
-    if (v3 > best) { a = 3; best = v3; }
-    return a;
+    return argmax4_torch(v0, v1, v2, v3);
 }
 
 // fixed: argmax of Q over legal moves only (first index on ties), 0 if no move is legal.

@@ -175,13 +175,9 @@ __device__ __forceinline__ float bellman(const float* qo, const float* qt, int32
 #pragma clang fp contract(off)
     float next;
     if (double_dqn) {
-        int a = 0;
-        float best = qo[0];
-        for (int k = 1; k < 4; ++k)
-            if (qo[k] > best) { best = qo[k]; a = k; }
-        next = qt[a];
+        next = qt[g2048::argmax4_torch(qo[0], qo[1], qo[2], qo[3])];  // torch.argmax: NaN first
     } else {
-        next = fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+        next = g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);          // torch.max: NaN wins
     }
     const float disc = (float)(1 - (int)d) * gamma;
     return (float)r + disc * next;

@@ -108,42 +108,8 @@ __device__ __forceinline__ void stage(const NetW& W, float* lds, Regs& R) {
     PHASE(5);
 }
 
-// Q[16][4] of the 16 boards in xs (exponents as floats, visible to all threads) -> qs (LDS).
-// Ends with __syncthreads() (qs visible; V / h2 / fa free for the next tile).
-__device__ __forceinline__ void tile(const float* xs, float* lds, const Regs& R, float* qs) {
-    const int t = threadIdx.x;
-    float* fa = lds + OFF_F;
-    PHASE_BEGIN();
-    conv1_v(xs, lds + OFF_V, R);
-    __syncthreads();
-    PHASE(0);
-    conv2_h2(lds + OFF_V, lds + OFF_H2, lds + OFF_B2, R);
-    __syncthreads();
-    PHASE(1);
-    fc1_f(lds + OFF_H2, lds + OFF_WF1, lds + OFF_BF1, fa);
-    __syncthreads();
-    PHASE(2);
-    // ---- fc2: output o = t >> 2 (board o >> 2, action o & 3), part p = t & 3 sums 16 units
-    {
-        const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
-        const f32x4* fr = reinterpret_cast<const f32x4*>(fa + s * FS + 16 * p);
-        const f32x4* wr = reinterpret_cast<const f32x4*>(lds + OFF_WF2 + a * WF2S + 16 * p);
-        f32x4 pv = f32x4{0};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const f32x4 f = fr[j], w = wr[j];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) pv[e] = fmaf(w[e], f[e], pv[e]);
-        }
-        float v = (pv[0] + pv[1]) + (pv[2] + pv[3]);
-        v += __shfl_xor(v, 1);
-        v += __shfl_xor(v, 2);
-        if (p == 0) qs[o] = v + lds[OFF_BF2 + a];
-    }
-    __syncthreads();
-    PHASE(3);
-}
-// fc2 of the tile whose f is in LDS -> qs[16][4] (LDS), the float sequence of tile()'s fc2.
+// fc2 of the tile whose f is in LDS -> qs[16][4] (LDS): output o = t >> 2 (board o >> 2, action
+// o & 3), part p = t & 3 sums 16 units, then a 4-lane shuffle sum.
 __device__ __forceinline__ void fc2_lds(const float* lds, float* qs) {
     const int t = threadIdx.x;
     const int o = t >> 2, p = t & 3, s = o >> 2, a = o & 3;
@@ -182,7 +148,7 @@ __device__ __forceinline__ void tiles_pipe(float* lds, const Regs& R, int T, flo
 }  // namespace persist
 
 // fc2 of a tile straight to global Q: thread (o = t >> 2, part p = t & 3) sums 16 units; the
-// float sequence of tile()'s fc2.
+// float sequence of fc2_lds.
 __device__ __forceinline__ void persist_fc2_store(const float* lds, float* q, int64_t b0,
                                                   int64_t n) {
     namespace P = persist;
@@ -229,7 +195,7 @@ __device__ __forceinline__ void persist_fc2_scatter(const float* lds, float* q, 
 //   [conv2(k) ; fc2(k-1) -> Q]  sync  [fc1(k) ; conv1 + V(k+1)]  sync
 // (V is free once conv2(k) has read it, h2 once fc1(k) has; fc2 reads f, which the next fc1
 // rewrites only after the next sync).  Boards are double-buffered in xs and loaded two tiles
-// ahead.  Same float sequence per board as tile().
+// ahead.  Same float sequence per board as conv1_v, conv2_h2, fc1_f and fc2_lds in sequence.
 __global__ __launch_bounds__(NT) void k_conv_forward_pipe(ConvNetArgs A) {
     namespace P = persist;
     __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
@@ -271,35 +237,6 @@ __global__ __launch_bounds__(NT) void k_conv_forward_pipe(ConvNetArgs A) {
         prev = tile;
     }
     persist_fc2_store(lds, A.q, prev * P::S, A.n);
-}
-
-// The rollout's Q over all n boards (earlier form, kept for tools/prof_forward.hip's per-phase
-// probes): 256 workgroups stage the net once and loop over 16-board tiles; the next tile's
-// boards are loaded during the current one.
-__global__ __launch_bounds__(NT) void k_conv_forward_persist(ConvNetArgs A) {
-    namespace P = persist;
-    __shared__ __attribute__((aligned(16))) float lds[P::FLOATS];
-    const int t = threadIdx.x;
-    const NetW W{A.w1, A.b1, A.w2, A.b2, A.wf1, A.bf1, A.wf2, A.bf2};
-    P::Regs R;
-    const int64_t ntiles = (A.n + P::S - 1) / P::S;
-    auto load_word = [&](int64_t tile) -> uint32_t {
-        const int64_t b = tile * P::S + (t >> 2);
-        if (t >= P::S * 4 || tile >= ntiles || b >= A.n) return 0u;
-        return reinterpret_cast<const uint32_t*>(A.rows)[(A.idx ? A.idx[b] : b) * 4 + (t & 3)];
-    };
-    uint32_t next_word = load_word(blockIdx.x);
-    P::stage(W, lds, R);
-    float* xs = lds + P::OFF_X;
-    float* qs = lds + P::OFF_Q;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t b0 = tile * P::S;
-        if (t < P::S * 4) P::put_word(xs, t, next_word);
-        __syncthreads();
-        next_word = load_word(tile + gridDim.x);  // in flight during this tile
-        P::tile(xs, lds, R, qs);
-        if (t < P::S * 4 && b0 + (t >> 2) < A.n) A.q[b0 * 4 + t] = qs[t];
-    }
 }
 
 // The rollout's Q restricted to the boards whose next eps-greedy step is greedy
@@ -458,16 +395,9 @@ struct TargetArgs {
     float2* rdisc;    // [B] ((float)r_b, (1 - d_b) * gamma)
 };
 
-// torch.argmax over 4 Q-values: the first index wins ties.
+// torch.argmax over 4 Q-values: the first index wins ties, the first NaN wins over numbers.
 __device__ __forceinline__ int argmax4_first(const float* q) {
-    int a = 0;
-    float best = q[0];
-    for (int e = 1; e < 4; ++e)
-        if (q[e] > best) {
-            best = q[e];
-            a = e;
-        }
-    return a;
+    return (int)g2048::argmax4_torch(q[0], q[1], q[2], q[3]);
 }
 
 // Each workgroup owns up to TMAX 16-sample tiles (tile = blockIdx.x + k*gridDim.x): it draws
@@ -563,7 +493,7 @@ __global__ __launch_bounds__(NT) void k_conv_targets_persist(TargetArgs A) {
                 A.rdisc[b] = make_float2((float)rv[k], disc);
             } else {
                 const float next = A.double_dqn ? qt[argmax4_first(qon + (k * P::S + sm) * 4)]
-                                                : fmaxf(fmaxf(qt[0], qt[1]), fmaxf(qt[2], qt[3]));
+                                                : g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);
                 A.y[b] = g2048::cnet::bellman_y((float)rv[k], disc, next);
             }
         }

@@ -18,6 +18,8 @@ Fixtures (all boards are stored as log2 exponents, 0 = empty, row-major):
                        (src/board.py:41-51) so the env can be replayed with injected spawns
   egreedy.npz          dqn_lib.epsilon_greedy_policy(eps=0) on fixed Q rows / legal masks
                        (src/dqn_lib.py:16-30, operator-precedence formula at :25-27)
+  egreedy_nonfinite.npz  the same policy on Q rows holding NaN / +-inf / f32-overflowing values
+                       (torch's NaN-propagating min/max and first-NaN argmax) + torch.max(Q)
   learner_<net>.npz    dqn_lib.train_step on a seeded buffer, B=512, deterministic weights
                        (src/dqn_lib.py:119-164) + restated intermediates, correct-order
                        grads and one Adam step (lr 1e-2)
@@ -233,6 +235,40 @@ def gen_egreedy(n=4000, seed=7):
                         action_f32=action32, done=done)
 
 
+def gen_egreedy_nonfinite(n=3000, seed=11):
+    """Rows with NaN, +inf, -inf and values whose min*max overflows float32 (finite in float64):
+    the reference's epsilon_greedy_policy (src/dqn_lib.py:24-30) in f64 and f32, with the
+    torch.max(Q) it returns (the Q-sum of the episode log)."""
+    rng = np.random.default_rng(seed)
+    pool = np.array([np.nan, np.inf, -np.inf, 0.0, -0.0, 1.0, -2.0, 0.5, 3.0, 1e30, -1e30, 7e-39],
+                    dtype=np.float64)
+    q = rng.normal(size=(n, 4))
+    pick = rng.random(size=(n, 4)) < 0.45
+    q[pick] = pool[rng.integers(0, len(pool), size=int(pick.sum()))]
+    # every row has at least one non-finite or overflowing entry
+    first = rng.integers(0, 4, size=n)
+    q[np.arange(n), first] = pool[rng.integers(0, 3, size=n)]
+    q[n - 16:] = np.nan                                   # all-NaN rows
+    mask = rng.integers(0, 16, size=n).astype(np.uint8)
+    mask[n - 16:] = np.arange(16)
+    out = {"q": q, "mask": mask}
+    for dt, suf in [(torch.float64, ""), (torch.float32, "_f32")]:
+        action = np.zeros(n, dtype=np.uint8)
+        qmax = np.zeros(n, dtype=np.float64)
+        for i in range(n):
+            qt = torch.tensor(q[i], dtype=dt)
+            a, d, mq = dqn_lib.epsilon_greedy_policy(
+                _StubBoard(int(mask[i])), 0.0, lambda x, qt=qt: qt, "cpu",
+                board_to_tensor_function=lambda b, dev: None)
+            action[i] = a
+            qmax[i] = float(mq)
+        out["action" + suf] = action
+        out["qmax" + suf] = qmax
+    out["done"] = (mask == 0).astype(np.uint8)
+    np.savez_compressed(os.path.join(OUT, "egreedy_nonfinite.npz"), **out)
+    print("egreedy_nonfinite", n, "rows;", int(np.isnan(q).any(axis=1).sum()), "with NaN")
+
+
 # ---------------------------------------------------------------- learner_<net>.npz
 def det_init(model, phase: float):
     """Deterministic weights: p.flat[k] = sin(1.3 k + phase) / sqrt(fan_in)."""
@@ -342,6 +378,7 @@ if __name__ == "__main__":
     gen_row_lut()
     gen_trajectories()
     gen_egreedy()
+    gen_egreedy_nonfinite()
     buf, arrs = build_buffer()
     for k in ["conv", "dense", "dense64"]:
         gen_learner(k, buf, arrs)

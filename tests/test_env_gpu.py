@@ -9,6 +9,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from oracle import oracle as O  # noqa: E402
+from boards import boards_for_masks, mask_boards  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -49,18 +50,7 @@ def _random_boards(n, seed):
 
 
 def _mask_boards():
-    """Boards realising all 16 legal masks: a terminal board with 1-2 holes / equal pairs, plus
-    one empty edge row/column for the four single-direction masks."""
-    T = np.array([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 1], np.uint8)
-    out = []
-    for i in range(16):
-        b = T.copy(); b[i] = 0; out.append(b)
-        for j in range(16):
-            b2 = b.copy(); b2[j] = 0; out.append(b2)
-            b3 = T.copy(); b3[j] = T[i]; out.append(b3)
-    for cells in ([0, 1, 2, 3], [12, 13, 14, 15], [0, 4, 8, 12], [3, 7, 11, 15]):
-        b = T.copy(); b[cells] = 0; out.append(b)
-    return out
+    return mask_boards()
 
 
 # ------------------------------------------------------------------ slide / score / legal
@@ -252,6 +242,23 @@ def test_egreedy_golden_rows(g2048, golden_dir):
         a, _, d = env.step_egreedy(torch.from_numpy(g["q"].astype(dt)).to(DEV), 0.0)
         assert np.array_equal(_np(a), g[field])
         assert np.array_equal(_np(d), g["done"])
+
+
+def test_egreedy_nonfinite_golden_rows(g2048, golden_dir):
+    """Q rows with NaN / +-inf / f32-overflowing products: the actions the reference's
+    epsilon_greedy_policy takes (torch's NaN-propagating min/max, first-NaN argmax) and the
+    torch.max(Q) it adds to the episode's Q-sum (src/dqn_lib.py:24-30)."""
+    g = np.load(os.path.join(golden_dir, "egreedy_nonfinite.npz"))
+    boards = boards_for_masks(g["mask"], O.legal_mask)
+    live = g["mask"] != 0  # a terminal step resets the running Q-sum to 0
+    for dt, suf in [(np.float64, ""), (np.float32, "_f32")]:
+        env = _env_with(g2048, boards)
+        log = env.attach_episode_log(2)
+        a, _, d = env.step_egreedy(torch.from_numpy(g["q"].astype(dt)).to(DEV), 0.0)
+        assert np.array_equal(_np(a), g["action" + suf])
+        assert np.array_equal(_np(d), g["done"])
+        qs = _np(log.qsum)
+        assert np.array_equal(qs[live], g["qmax" + suf][live], equal_nan=True)
 
 
 def test_rollout_equals_single_steps(g2048):

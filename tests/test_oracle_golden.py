@@ -14,6 +14,8 @@ import pytest
 
 from oracle import oracle as O
 
+from boards import boards_for_masks
+
 
 def _exps(vals):
     v = np.asarray(vals, dtype=np.int64)
@@ -93,6 +95,32 @@ def test_egreedy_compat(golden_dir, field, dtype):
     for i in range(len(q)):
         assert O.greedy(q[i], int(g["mask"][i])) == g[field][i], i
     assert np.array_equal(g["done"], (g["mask"] == 0).astype(np.uint8))
+
+
+@pytest.mark.parametrize("suf,dtype", [("", np.float64), ("_f32", np.float32)])
+def test_egreedy_compat_nonfinite(golden_dir, suf, dtype):
+    """NaN / +-inf rows: torch.min/max propagate NaN, torch.argmax takes the first NaN."""
+    g = np.load(os.path.join(golden_dir, "egreedy_nonfinite.npz"))
+    q = g["q"].astype(dtype)
+    assert np.isnan(q).any() and np.isinf(q).any()
+    for i in range(len(q)):
+        assert O.greedy(q[i], int(g["mask"][i])) == g["action" + suf][i], (i, q[i], g["mask"][i])
+
+
+@pytest.mark.parametrize("suf,mode", [("", O.MODE_EGREEDY_F64), ("_f32", O.MODE_EGREEDY_F32)])
+def test_oracle_env_qsum_nonfinite(golden_dir, suf, mode):
+    """The oracle env step's Q-sum (episode log) adds the reference's torch.max(Q)."""
+    g = np.load(os.path.join(golden_dir, "egreedy_nonfinite.npz"))
+    boards = boards_for_masks(g["mask"], O.legal_mask)
+    env = O.OracleEnv(len(boards), seed=1, flags=O.NO_AUTORESET, reset=False)
+    env.board[:] = boards
+    env.attach_episode_log(2)
+    q = g["q"].astype(np.float64 if mode == O.MODE_EGREEDY_F64 else np.float32)
+    out = env.step(mode, q=q, eps=0.0)
+    assert np.array_equal(out["action"], g["action" + suf])
+    assert np.array_equal(out["done"], g["done"])
+    live = g["mask"] != 0
+    assert np.array_equal(env.qsum[live], g["qmax" + suf][live], equal_nan=True)
 
 
 def test_philox_known_answer():

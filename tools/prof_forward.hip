@@ -1,4 +1,4 @@
-// f32 MFMA / VALU calibration and k_conv_forward_persist timing + per-phase ticks, built only for
+// f32 MFMA / VALU calibration and conv forward/targets timing + per-phase ticks, built only for
 // kernel tuning:  hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_forward.hip -o tools/prof_forward
 #define G2048_PHASE_PROF 1
 #include <cstdarg>
