@@ -73,8 +73,27 @@ def parse():
 BACKEND = os.environ.get("G2048_BENCH_BACKEND", "nccl")
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a torchrun environment: start N ranks (one process per GPU)
+    through torch.distributed.run as a CHILD process -- nothing here has touched the GPU -- and
+    return its exit code."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    import subprocess
+
+    return subprocess.call(cmd)
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
@@ -141,7 +160,11 @@ def bench_env(args, world, rank, dev):
     if args.steps % G:
         graphs.append((capture(one_step, args.steps % G), 1))
     # warm-up: the W untimed steps run as graph replays too, so the timed region starts with the
-    # GPU already in its steady state (eager launches leave it idle between steps)
+    # GPU already in its steady state (eager launches leave it idle between steps); every captured
+    # graph is replayed at least once whatever W is, so the timed region never holds the first
+    # replay of a fresh graph
+    for g, _ in graphs:
+        g.replay()
     for _ in range(args.warmup // G):
         graphs[0][0].replay()
     for _ in range(args.warmup % G):
@@ -309,6 +332,8 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world, rank, dev = setup_dist(args)
     torch.cuda.set_device(dev)
     # the extra fields run first: the headline env-step timing then starts on a GPU that has

@@ -21,8 +21,10 @@
  *  - Randomness is counter-based Philox4x32-10.  Board g (global id = board_offset + i) owns
  *    rocRAND philox4x32_10 subsequence g: its step draw at step t is the 4-word block
  *    rocrand_init(seed, g, 4t) would return first (domain bits 30-31 of the subsequence word
- *    select step / auto-reset / explicit-reset / sampler draws).  No per-lane state in HBM
- *    beyond the per-board step counter.
+ *    select step / random-policy / explicit-reset / sampler draws).  The random policy
+ *    (actions == NULL, g2048_env_rollout) spends half a block per step: step t takes words
+ *    (x, y) (t even) or (z, w) (t odd) of block t >> 1 of the random-policy domain.  No per-lane
+ *    RNG state in HBM: the counter t is the env's step clock (one u64 per 64 boards).
  */
 #ifndef G2048_H
 #define G2048_H
@@ -33,7 +35,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 1
+#define G2048_ABI_VERSION 2
 
 #ifndef G2048_API
 #define G2048_API __attribute__((visibility("default")))
@@ -75,22 +77,31 @@ typedef struct {
 } g2048_episode;
 
 /* ---- environment -------------------------------------------------------------------------
- * State per board i: board u8[16]; meta u32[4] = {score, moves, steps_lo, steps_hi} (score =
- * Board2048._mergescore, moves = len(_action_history) of the running episode, steps = RNG
- * step counter); ep u32[4] = {episodes finished, last score, last moves, last max exponent}
- * (the Experiment.add_episode fields, src/experiments.py:112-122). */
+ * State per board i: board u8[16]; meta u32[2] = {score, moves} (score = Board2048._mergescore,
+ * moves = len(_action_history) of the running episode); ep u32[4] = {episodes finished, last
+ * score, last moves, last max exponent} (the Experiment.add_episode fields,
+ * src/experiments.py:112-122).  Per group of 64 boards (boards 64g .. 64g+63): clock u64[g] =
+ * the number of steps taken, i.e. the Philox counter of the next step and the replay row it
+ * appends to.  Every step call advances every board, so all clocks of an env hold the same
+ * value; each group is read and advanced only by the wavefront that steps its boards, so no
+ * kernel needs a grid-wide barrier to advance it. */
+#define G2048_CLOCK_GROUP 64
+#define G2048_CLOCK_WORDS(n) (((n) + G2048_CLOCK_GROUP - 1) / G2048_CLOCK_GROUP)
 
 /* Replaces `Board2048()` x n_boards (src/board.py:10-20): allocates and resets n boards. */
 G2048_API int g2048_env_create(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,
                      int device_id, uint32_t flags, void* stream);
-/* Same, over caller-owned device buffers board u8[n][16], meta u32[n][4], ep u32[n][4]
- * (16-byte aligned).  If reset != 0 the boards are reset (2 spawns each), else left as given. */
+/* Same, over caller-owned device buffers board u8[n][16], meta u32[n][2], ep u32[n][4],
+ * clock u64[G2048_CLOCK_WORDS(n)] (board/ep 16-byte, meta/clock 8-byte aligned).  If reset != 0
+ * the boards are reset (2 spawns each), else left as given; the clock is used as given (all
+ * words equal: zero for a fresh env). */
 G2048_API int g2048_env_wrap(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,
                    int device_id, uint32_t flags, uint8_t* board_dev, uint32_t* meta_dev,
-                   uint32_t* ep_dev, int reset, void* stream);
+                   uint32_t* ep_dev, uint64_t* clock_dev, int reset, void* stream);
 G2048_API void g2048_env_destroy(g2048_env* env);
-/* Device views of the env state (library-owned or wrapped). */
-G2048_API int g2048_env_views(g2048_env* env, uint8_t** board_dev, uint32_t** meta_dev, uint32_t** ep_dev);
+/* Device views of the env state (library-owned or wrapped); any out-pointer may be NULL. */
+G2048_API int g2048_env_views(g2048_env* env, uint8_t** board_dev, uint32_t** meta_dev,
+                              uint32_t** ep_dev, uint64_t** clock_dev);
 G2048_API int64_t g2048_env_size(const g2048_env* env);
 
 /* Re-deal fresh boards (2 spawns, src/board.py:18-20) where reset_mask_dev[i] != 0 (all if NULL). */
@@ -154,7 +165,9 @@ G2048_API int g2048_env_step_inject(g2048_env* env, const uint8_t* actions_dev, 
 
 /* k_steps random-policy env steps per launch with the board held in registers (replay pre-fill,
  * env-only throughput).  Identical results to k_steps calls of g2048_env_step(actions=NULL).
- * reward_sum_dev (i64[n], accumulated, or NULL). */
+ * reward_sum_dev (i64[n], accumulated, or NULL).  A step's transition is appended with five
+ * stores whose per-step offset is a scalar (row * n), the board never leaves the VGPRs, and the
+ * Philox block of a step pair is drawn once. */
 G2048_API int g2048_env_rollout(g2048_env* env, int32_t k_steps, g2048_replay* rb, int64_t* reward_sum_dev,
                       void* stream);
 

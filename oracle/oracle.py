@@ -28,7 +28,7 @@ def build() -> str:
 class _Env(C.Structure):
     _fields_ = [("n", C.c_int64), ("board_offset", C.c_uint64), ("seed", C.c_uint64),
                 ("flags", C.c_uint32), ("board", C.c_void_p), ("meta", C.c_void_p),
-                ("ep", C.c_void_p), ("qsum", C.c_void_p), ("log", C.c_void_p),
+                ("ep", C.c_void_p), ("clock", C.c_void_p), ("qsum", C.c_void_p), ("log", C.c_void_p),
                 ("log_slots", C.c_int64)]
 
 
@@ -145,11 +145,12 @@ class OracleEnv:
     def __init__(self, n: int, seed: int, flags: int = 0, board_offset: int = 0, reset=True):
         self.n = n
         self.board = np.zeros((n, 16), np.uint8)
-        self.meta = np.zeros((n, 4), np.uint32)
+        self.meta = np.zeros((n, 2), np.uint32)
         self.ep = np.zeros((n, 4), np.uint32)
+        self.clock = np.zeros((n + 63) // 64, np.uint64)
         self.epoch = 0
         self._c = _Env(n, board_offset, seed, flags, _p(self.board), _p(self.meta), _p(self.ep),
-                       None, None, 0)
+                       _p(self.clock), None, None, 0)
         if reset:
             self.reset()
 

@@ -191,14 +191,31 @@ static void fresh_board(uint8_t b[16], const uint32_t u[4], uint32_t flags) {
     spawn(b, u[2] << 4, u[0] << 2, flags);
 }
 
+/* Auto-reset of a terminal random-policy step from its two words (wa, wb) (include/g2048.h,
+ * g2048_board.hpp random_block): a tile at cell (wa >> 26) & 15, then one at the k2-th of the 15
+ * remaining empty cells in row-major order, k2 = floor((wa << 6) * 15 / 2^32); each a 4 iff its
+ * 16-bit half of wb is below p4 * 2^16 (rounded). */
+static void fresh_board_random(uint8_t b[16], uint32_t wa, uint32_t wb, uint32_t flags) {
+    const uint32_t thresh = (flags & 1u) ? 429496730u : 2147483648u;
+    const uint32_t th16 = (thresh + 0x8000u) >> 16;
+    memset(b, 0, 16);
+    b[(wa >> 26) & 15u] = ((wb & 0xFFFFu) < th16) ? 2 : 1;
+    uint32_t k = (uint32_t)(((uint64_t)(uint32_t)(wa << 6) * 15u) >> 32);
+    for (int i = 0; i < 16; ++i) {
+        if (b[i] != 0) continue;
+        if (k == 0) { b[i] = ((wb >> 16) < th16) ? 2 : 1; return; }
+        --k;
+    }
+}
+
 void o2048_env_reset(o2048_env* e, const uint8_t* mask, uint32_t epoch) {
     for (int64_t i = 0; i < e->n; ++i) {
         if (mask && !mask[i]) continue;
         uint32_t u[4];
         draw(e->seed, e->board_offset + (uint64_t)i, 2u, epoch, u);
         fresh_board(e->board + 16 * i, u, e->flags);
-        uint32_t* m = e->meta + 4 * i;
-        m[0] = 0; m[1] = 0;  /* score, moves; the step counter keeps running */
+        uint32_t* m = e->meta + 2 * i;
+        m[0] = 0; m[1] = 0;  /* score, moves; the step clock keeps running */
     }
 }
 
@@ -213,11 +230,20 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
     int64_t bad = 0;
     for (int64_t i = 0; i < e->n; ++i) {
         uint8_t* b = e->board + 16 * i;
-        uint32_t* m = e->meta + 4 * i;
+        uint32_t* m = e->meta + 2 * i;
         const uint64_t gid = e->board_offset + (uint64_t)i;
-        const uint64_t t = (uint64_t)m[2] | ((uint64_t)m[3] << 32);
+        const uint64_t t = e->clock[i / 64];   /* the board's group clock (64 boards per word) */
         uint32_t u[4];
-        draw(e->seed, gid, 0u, t, u);
+        /* random policy: words (x, y) or (z, w) of block t/2 of domain 1; other modes: block t
+         * of domain 0 (include/g2048.h) */
+        uint32_t wa = 0, wb = 0;
+        if (mode == 1) {
+            draw(e->seed, gid, 1u, t >> 1, u);
+            wa = (t & 1) ? u[2] : u[0];
+            wb = (t & 1) ? u[3] : u[1];
+        } else {
+            draw(e->seed, gid, 0u, t, u);
+        }
         double qs = e->qsum ? e->qsum[i] : 0.0;
 
         const uint8_t legal = o2048_legal_mask(b);   /* dqn_lib.py:17 */
@@ -226,7 +252,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
         if (mode == 0 || mode == 4) {
             a = actions[i];
         } else if (mode == 1) {
-            a = (int)(u[0] >> 30);
+            a = (int)(wa >> 30);                     /* np.random.randint(4) */
         } else {
             double eps_i = eps;
             if (eps_decay > 0) {  /* dqn_lib.py:184-188, ep = this board's episode count */
@@ -273,6 +299,8 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
                     int si = spawn_idx[i];
                     if (si >= 0 && si < 16 && nb[si] == 0) nb[si] = spawn_exp[i];
                     else ++bad;
+                } else if (mode == 1) {
+                    spawn(nb, wa << 2, wb, e->flags);
                 } else {
                     spawn(nb, u[2], u[3], e->flags);
                 }
@@ -316,15 +344,14 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             qs = 0.0;
             ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;
             if (autoreset) {
-                fresh_board(b, u, e->flags);   /* the step's own block (see fresh_board) */
+                if (mode == 1) fresh_board_random(b, wa, wb, e->flags);
+                else fresh_board(b, u, e->flags);   /* the step's own block (see fresh_board) */
                 m[0] = 0; m[1] = 0;
             }
         }
         if (e->qsum) e->qsum[i] = qs;
-        const uint64_t t1 = t + 1;
-        m[2] = (uint32_t)t1;
-        m[3] = (uint32_t)(t1 >> 32);
     }
+    for (int64_t g = 0; g < (e->n + 63) / 64; ++g) e->clock[g] += 1;  /* every board stepped */
     return bad;
 }
 

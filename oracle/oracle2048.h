@@ -35,8 +35,9 @@ int o2048_greedy_f32(const float q[4], uint8_t legal, int fixed);
 /* Batched env step, mirroring g2048_env_step* exactly (see include/g2048.h for the contract).
  * mode: 0 = actions in, 1 = random, 2 = eps-greedy over q_f32, 3 = eps-greedy over q_f64,
  *       4 = actions in + injected spawns.
- * meta: uint32[N][4] = {score, moves, steps_lo, steps_hi}; ep: uint32[N][4] = {episodes,
- * last_score, last_moves, last_max_exp}.  Replay pointers may be NULL (no append). */
+ * meta: uint32[N][2] = {score, moves}; ep: uint32[N][4] = {episodes, last_score, last_moves,
+ * last_max_exp}; clock: uint64[ceil(N/64)] step counters (board i uses clock[i/64]).  Replay
+ * pointers may be NULL (no append). */
 /* One finished episode, the layout of include/g2048.h g2048_episode (40 B). */
 typedef struct {
     uint64_t step;
@@ -50,8 +51,9 @@ typedef struct {
     uint64_t seed;
     uint32_t flags;
     uint8_t* board;          /* [n][16] */
-    uint32_t* meta;          /* [n][4]  */
+    uint32_t* meta;          /* [n][2]  */
     uint32_t* ep;            /* [n][4]  */
+    uint64_t* clock;         /* [ceil(n/64)] */
     double* qsum;            /* [n] running max-Q sum, or NULL (episode log off) */
     o2048_episode* log;      /* [n][log_slots]: board i's episode e at i*S + e%S, or NULL */
     int64_t log_slots;

@@ -1,20 +1,25 @@
 // g2048.hip -- batched 2048 env step / rollout / reset and replay sample-encode kernels for
 // gfx950, plus the extern "C" ABI declared in include/g2048.h.
 //
-// HBM layout (one env = one shard of boards, SoA, 16-byte records so every lane moves whole
-// dwordx4s):
+// HBM layout (one env = one shard of boards, SoA):
 //   board u8[N][16]   exponents                       (one uint4 per board)
-//   meta  u32[N][4]   {score, moves, steps_lo, steps_hi}
-//   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (touched on done only)
+//   meta  u32[N][2]   {score, moves}                  (one uint2 per board)
+//   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (read with the board
+//                     only where the step needs it; written on done)
+//   clock u64[N/64]   the step counter of each 64-board group (all equal: every call steps every
+//                     board).  The wavefront that steps group g is the only reader-writer of
+//                     clock[g], so the counter needs no grid-wide ordering, and it reaches the
+//                     kernel as a scalar: Philox counters, ring rows and ring offsets of a step
+//                     are SALU work.
 // Replay ring (capacity C): s u8[C][16], s2 u8[C][16], a u8[C], r i32[C], d u8[C], count u64.
 // Optional episode log (g2048_env_set_episode_log): g2048_episode records [N][S], board i's
 // episode e in slot i*S + e%S, written on its terminal step + qsum f64[N] (running sum of
 // max_a Q over the board's episode).
 //
-// One lane owns one board for the whole launch: load board + meta (2 x dwordx4), do the
-// legal-mask / select / slide / spawn / reset arithmetic in VGPRs (g2048_board.hpp), store them
-// back.  Consecutive blocks own consecutive board ranges, so a board's lines stay in the same
-// XCD L2 from one step to the next (blocks are dealt round-robin over the 8 XCDs).
+// One lane owns one board for the whole launch: load board + meta, do the legal-mask / select /
+// slide / spawn / reset arithmetic in VGPRs (g2048_board.hpp), store them back.  Consecutive
+// blocks own consecutive board ranges, so a board's lines stay in the same XCD L2 from one step
+// to the next (blocks are dealt round-robin over the 8 XCDs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -38,6 +43,8 @@ constexpr int kBlock = 256;
 // 1 024: 4.22).  HBM-bound sizes keep 256.
 constexpr int kStepBlockSmall = 64;
 constexpr int64_t kStepSmallMaxBoards = 1 << 20;
+static_assert(kBlock % G2048_CLOCK_GROUP == 0 && kStepBlockSmall % G2048_CLOCK_GROUP == 0,
+              "a wavefront must own whole clock groups");
 enum : int {
     MODE_ACTIONS = 0,
     MODE_RANDOM = 1,
@@ -60,8 +67,9 @@ struct ReplayDev {
 
 struct StepArgs {
     uint4* board;
-    uint4* meta;
+    uint2* meta;
     uint4* ep;
+    uint64_t* clock;
     int64_t n;
     uint64_t board_offset;
     uint32_t seed_lo, seed_hi;
@@ -90,70 +98,128 @@ struct StepArgs {
 
 __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v.y, v.z, v.w}; }
 
-// One transition of board i (global id gid).  Mirrors o2048_env_step (oracle/oracle2048.c),
-// which restates src/dqn_lib.py:91-107 + src/board.py.
+// The step counter of board i's 64-board group as a wave-uniform (SGPR) value.  Every lane of the
+// wave loads the same word; the wave's first lane is always live (groups start at 64-aligned
+// board indices and a wave never straddles two groups).
+__device__ __forceinline__ uint64_t load_clock(const uint64_t* clock, int64_t i) {
+    const uint64_t c = clock[i >> 6];
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)c);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// Ring row of step t (t mod rows) -- wave-uniform.
+__device__ __forceinline__ uint64_t ring_row(uint64_t t, int64_t rows) {
+    return (t >> 32) ? (t % (uint64_t)rows) : (uint64_t)((uint32_t)t % (uint32_t)rows);
+}
+
+// End of board i's episode on its terminal step t: the Experiment.add_episode fields
+// (src/experiments.py:112-122) into ep[i] and, with a log attached, one record in the board's own
+// slot ring (no atomics, fixed order).  The caller re-deals the board.
+template <bool kGreedy>
+__device__ __forceinline__ void end_episode(const StepArgs& A, int64_t i, uint64_t gid, uint64_t t,
+                                            const Board& b, const uint2& m, uint4& ep, double& qs) {
+    const uint32_t mx = max_exp(b);
+    const uint32_t ep_idx = ep.x;
+    ep = make_uint4(ep.x + 1u, m.x, m.y, mx);
+    A.ep[i] = ep;
+    if (A.log) {
+        g2048_episode rec;
+        rec.step = t;
+        rec.q_sum = qs;
+        rec.board = (uint32_t)gid;
+        rec.episode = ep_idx;
+        rec.score = m.x;
+        rec.moves = m.y;
+        rec.max_exp = mx;
+        rec.reserved = 0u;
+        A.log[i * A.log_slots + (int64_t)(ep_idx % (uint32_t)A.log_slots)] = rec;
+    }
+    qs = 0.0;
+    if constexpr (!kGreedy) {  // non-greedy steps add 0 to the sum: reset it on done
+        if (A.qsum) A.qsum[i] = 0.0;
+    }
+}
+
+// One transition of board i (global id gid) at step t (the group clock).  Mirrors o2048_env_step
+// (oracle/oracle2048.c), which restates src/dqn_lib.py:91-107 + src/board.py.
 // kPre: the caller loaded ep (and qs, when a q-sum buffer is attached) together with the board.
 // Otherwise they are loaded here on done only -- 16 B less traffic per board, at the price of a
 // dependent memory round trip for every wave that holds a terminal board.
 template <int MODE, bool kPre = true>
-__device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, Board& b,
-                                         uint4& m, double eps, double& qs, int32_t& rew_out,
-                                         uint32_t& done_out, uint32_t& legal_out,
+__device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t gid, uint64_t t,
+                                         Board& b, uint2& m, double eps, double& qs,
+                                         int32_t& rew_out, uint32_t& done_out, uint32_t& legal_out,
                                          uint32_t& act_out, uint4& ep,
                                          float4 qreg = float4{0, 0, 0, 0}) {
-    const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
-    const uint4 u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
-    const uint32_t legal = legal_mask(b);
-    const bool done = legal == 0u;
-
-    uint32_t act;
-    if constexpr (MODE == MODE_ACTIONS || MODE == MODE_INJECT) {
-        act = A.actions[i];
-    } else if constexpr (MODE == MODE_RANDOM) {
-        act = u.x >> 30;
-    } else {
-        const bool explore = explores(u.y, eps);
-        const bool fixed = (A.flags & G2048_EGREEDY_FIXED) != 0u;
-        if (explore) {
-            const uint32_t nl = __popc(legal);
-            act = (fixed && nl) ? kth_bit4(legal, __umulhi(u.x, nl)) : (u.x >> 30);
-        } else if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_REG) {
-            float4 q;
-            if constexpr (MODE == MODE_EG_REG) q = qreg;
-            else q = reinterpret_cast<const float4*>(A.q)[i];
-            act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
-                        : greedy_compat(q.x, q.y, q.z, q.w, legal);
-            qs += (double)qmax4_torch(q.x, q.y, q.z, q.w);  // torch.max(Q) (:29)
-        } else {
-            const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
-            const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
-            act = fixed ? greedy_fixed(q01.x, q01.y, q23.x, q23.y, legal)
-                        : greedy_compat(q01.x, q01.y, q23.x, q23.y, legal);
-            qs += qmax4_torch(q01.x, q01.y, q23.x, q23.y);
-        }
-    }
-
+    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG;
     const Board s_old = b;
-    uint32_t r = 0;
-    if (act > 3u) {
-        atomicAdd(A.err, 1ull);  // src/board.py:192 IndexError -> counted, no-op here
-    } else if (!done && ((legal >> act) & 1u)) {
-        r = apply_move(b, act);
-        if constexpr (MODE == MODE_INJECT) {
-            const int si = A.spawn_idx[i];
-            if (si >= 0 && si < 16 && cell_empty(b, (uint32_t)si)) set_cell(b, (uint32_t)si, A.spawn_exp[i]);
-            else atomicAdd(A.err, 1ull);
+    uint32_t legal = 0u, act, r = 0u;
+    bool done;
+    uint4 u;
+    uint32_t wa = 0u, wb = 0u;
+    if constexpr (MODE == MODE_RANDOM) {
+        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, t >> 1);
+        wa = (t & 1u) ? blk.z : blk.x;
+        wb = (t & 1u) ? blk.w : blk.y;
+        act = wa >> 30;
+        if (A.legal_out) {  // the mask is wanted anyway: it decides done and the move's legality
+            legal = legal_mask(b);
+            done = legal == 0u;
+            if (!done && ((legal >> act) & 1u)) {
+                r = apply_move(b, act);
+                spawn(b, wa << 2, wb, A.p4_thresh);
+            }
         } else {
-            spawn(b, u.z, u.w, A.p4_thresh);
+            r = random_step(b, wa, wb, A.p4_thresh, done);
+        }
+    } else {
+        u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
+        legal = legal_mask(b);
+        done = legal == 0u;
+        if constexpr (MODE == MODE_ACTIONS || MODE == MODE_INJECT) {
+            act = A.actions[i];
+        } else {
+            const bool explore = explores(u.y, eps);
+            const bool fixed = (A.flags & G2048_EGREEDY_FIXED) != 0u;
+            if (explore) {
+                const uint32_t nl = __popc(legal);
+                act = (fixed && nl) ? kth_bit4(legal, __umulhi(u.x, nl)) : (u.x >> 30);
+            } else if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_REG) {
+                float4 q;
+                if constexpr (MODE == MODE_EG_REG) q = qreg;
+                else q = reinterpret_cast<const float4*>(A.q)[i];
+                act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
+                            : greedy_compat(q.x, q.y, q.z, q.w, legal);
+                qs += (double)qmax4_torch(q.x, q.y, q.z, q.w);  // torch.max(Q) (:29)
+            } else {
+                const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
+                const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
+                act = fixed ? greedy_fixed(q01.x, q01.y, q23.x, q23.y, legal)
+                            : greedy_compat(q01.x, q01.y, q23.x, q23.y, legal);
+                qs += qmax4_torch(q01.x, q01.y, q23.x, q23.y);
+            }
+        }
+        if (act > 3u) {
+            atomicAdd(A.err, 1ull);  // src/board.py:192 IndexError -> counted, no-op here
+        } else if (!done && ((legal >> act) & 1u)) {
+            r = apply_move(b, act);
+            if constexpr (MODE == MODE_INJECT) {
+                const int si = A.spawn_idx[i];
+                if (si >= 0 && si < 16 && cell_empty(b, (uint32_t)si))
+                    set_cell(b, (uint32_t)si, A.spawn_exp[i]);
+                else
+                    atomicAdd(A.err, 1ull);
+            } else {
+                spawn(b, u.z, u.w, A.p4_thresh);
+            }
         }
     }
     m.x += r;
     m.y += 1u;
 
     if (A.rb.rows) {
-        const uint64_t row = (t >> 32) ? (t % (uint64_t)A.rb.rows)
-                                       : (uint64_t)((uint32_t)t % (uint32_t)A.rb.rows);
-        const int64_t slot = (int64_t)row * A.n + i;
+        const int64_t slot = (int64_t)ring_row(t, A.rb.rows) * A.n + i;
         A.rb.s[slot] = make_uint4(s_old.r0, s_old.r1, s_old.r2, s_old.r3);
         A.rb.s2[slot] = make_uint4(b.r0, b.r1, b.r2, b.r3);  // terminal: s' = s (F6)
         A.rb.a[slot] = (uint8_t)act;
@@ -161,8 +227,6 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         A.rb.d[slot] = (uint8_t)done;
     }
 
-    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG;
-    uint32_t ep_idx = 0u, mx = 0u, fin_score = 0u, fin_moves = 0u;
     if (done) {
         if constexpr (!kPre) {
             ep = A.ep[i];
@@ -170,40 +234,15 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
                 if (A.qsum) qs = A.qsum[i];
             }
         }
-        mx = max_exp(b);
-        ep_idx = ep.x;
-        ep = make_uint4(ep.x + 1u, m.x, m.y, mx);
-        A.ep[i] = ep;
-        fin_score = m.x;
-        fin_moves = m.y;
+        end_episode<kGreedy>(A, i, gid, t, b, m, ep, qs);
         if (!(A.flags & G2048_NO_AUTORESET)) {
-            b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
-            m.x = 0u;
-            m.y = 0u;
+            if constexpr (MODE == MODE_RANDOM)
+                b = fresh_board_random(wa, wb, p4_thresh16(A.p4_thresh));
+            else
+                b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
+            m = make_uint2(0u, 0u);
         }
     }
-    if (done && A.log) {  // Experiment.add_episode (src/experiments.py:112-122): one record per
-                          // episode, in the board's own slot ring (no atomics, fixed order)
-        g2048_episode rec;
-        rec.step = t;
-        rec.q_sum = qs;
-        rec.board = (uint32_t)gid;
-        rec.episode = ep_idx;
-        rec.score = fin_score;
-        rec.moves = fin_moves;
-        rec.max_exp = mx;
-        rec.reserved = 0u;
-        A.log[i * A.log_slots + (int64_t)(ep_idx % (uint32_t)A.log_slots)] = rec;
-    }
-    if (done) {
-        qs = 0.0;
-        if constexpr (!kGreedy) {
-            if (A.qsum) A.qsum[i] = 0.0;
-        }
-    }
-    const uint64_t t1 = t + 1u;
-    m.z = (uint32_t)t1;
-    m.w = (uint32_t)(t1 >> 32);
     rew_out = (int32_t)r;
     done_out = done;
     legal_out = legal;
@@ -216,14 +255,15 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
     atomicMax(A.rb.count, (unsigned long long)c);
 }
 
-// kFull: every block is full (n % kBlock == 0), so there is no bounds test and every kernel
-// argument load can be issued at once (with the test, the pointer loads wait for n's round trip).
+// kFull: every block is full (n % BS == 0), so there is no bounds test and every kernel argument
+// load can be issued at once (with the test, the pointer loads wait for n's round trip).
 template <int MODE, bool kFull, bool kPre, int BS>
 __global__ __launch_bounds__(BS) void k_step(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     if (!kFull && i >= A.n) return;
+    const uint64_t t = load_clock(A.clock, i);
     Board b = load_board(A.board[i]);
-    uint4 m = A.meta[i];
+    uint2 m = A.meta[i];
     uint4 ep = kPre ? A.ep[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
@@ -237,16 +277,17 @@ __global__ __launch_bounds__(BS) void k_step(StepArgs A) {
     uint32_t done, legal, act;
     constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
     double qs = ((kPre || kGreedy) && A.qsum) ? A.qsum[i] : 0.0;
-    step_one<MODE, kPre>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act,
-                         ep);
+    step_one<MODE, kPre>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
+                         act, ep);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
+    if ((i & 63) == 0) A.clock[i >> 6] = t + 1u;
     if (kGreedy && A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
     if (A.legal_out) A.legal_out[i] = (uint8_t)legal;
     if (A.action_out) A.action_out[i] = (uint8_t)act;
-    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+    if (A.rb.rows && i == 0) bump_count(A, t + 1u);
 }
 
 // The fused rollout step of the dense 16-64-4 net (BASELINE configs[2]): Q(s) of each board
@@ -273,7 +314,10 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     const int64_t i = (int64_t)blockIdx.x * 64 + lane;
     const bool live = kFull || i < A.n;
     Board b{0u, 0u, 0u, 0u};
-    uint4 m = make_uint4(0u, 0u, 0u, 0u), ep = make_uint4(0u, 0u, 0u, 0u);
+    uint2 m = make_uint2(0u, 0u);
+    uint4 ep = make_uint4(0u, 0u, 0u, 0u);
+    // both waves hold the same 64 boards (one clock group); lane 0 is live in every workgroup
+    const uint64_t t = load_clock(A.clock, (int64_t)blockIdx.x * 64);
     if (live) {
         b = load_board(A.board[i]);
         if (half == 0 || !q_out) {
@@ -288,7 +332,6 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     if (!q_out) {
         bool greedy = false;
         if (live) {
-            const uint64_t t = (uint64_t)m.z | ((uint64_t)m.w << 32);
             const uint4 u = draw(A.seed_lo, A.seed_hi, A.board_offset + (uint64_t)i, DOMAIN_STEP, t);
             greedy = !explores(u.y, step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, ep.x));
         }
@@ -331,40 +374,145 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     int32_t rew;
     uint32_t done, legal, act;
     double qs = A.qsum ? A.qsum[i] : 0.0;
-    step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, b, m, eps, qs, rew, done, legal, act,
-                          ep, q);
+    step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
+                          act, ep, q);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
+    if (lane == 0) A.clock[blockIdx.x] = t + 1u;  // wave 1 read it before the barrier
     if (A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
     if (A.action_out) A.action_out[i] = (uint8_t)act;
-    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+    if (A.rb.rows && i == 0) bump_count(A, t + 1u);
 }
 
-// k_steps random-policy steps with the board resident in VGPRs.
+// The ring as buffer resources: a step's five stores take the lane's constant byte offset
+// (i * size) in voffset and the row's offset (row * n * size, wave-uniform) in soffset, so a
+// step spends no VALU on addresses.  Used when every section of the ring is below 4 GiB.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// g2048_env_rollout: k_steps random-policy steps of every board with the board, score, moves and
+// episode counters held in registers; step t of the launch draws its two words from the Philox
+// block of its step pair (one block per two steps, see random_block) and appends (s, a, r, s', d)
+// to the ring.  Identical to k_steps g2048_env_step(actions = NULL) calls.  Issue-bound at 64k
+// boards (one wave per SIMD, so SALU instructions cost issue turns like VALU ones): the loop
+// keeps its scalar bookkeeping to a 32-bit ring row and a 64-bit pair counter, and the episode
+// counters are stored once at the end (only the last finished episode's record survives in ep;
+// the log, when attached, gets every one).  See DESIGN.md section 4.1.
+//   kRing: a replay ring is attached; kBuf: its sections are below 2 GiB (buffer stores);
+//   kSum: per-board reward sums are accumulated.
+template <bool kRing, bool kBuf, bool kSum>
 __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= A.n) return;
+    const uint64_t t0 = load_clock(A.clock, i);
     Board b = load_board(A.board[i]);
-    uint4 m = A.meta[i];
-    uint4 ep = A.ep[i];  // kept in registers across the K steps
+    uint2 m = A.meta[i];
+    uint4 ep = A.ep[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
+    const uint32_t p4_16 = p4_thresh16(A.p4_thresh);
+    const bool autoreset = !(A.flags & G2048_NO_AUTORESET);
     long long rsum = 0;
-    double qs = A.qsum ? A.qsum[i] : 0.0;  // random policy: written back (0) on done only
-    for (int s = 0; s < A.k_steps; ++s) {
-        int32_t rew;
-        uint32_t done, legal, act;
-        step_one<MODE_RANDOM>(A, i, gid, b, m, 0.0, qs, rew, done, legal, act, ep);
-        rsum += rew;
+    double qs = A.qsum ? A.qsum[i] : 0.0;  // random policy: reset (0) on done only
+    const uint32_t rows = kRing ? (uint32_t)A.rb.rows : 1u;
+    uint32_t row = kRing ? (uint32_t)ring_row(t0, A.rb.rows) : 0u;
+    const uint32_t n32 = (uint32_t)A.n;
+    // (the global-store instance -- ring sections past 2 GiB -- builds empty descriptors)
+    const uint32_t cap = kBuf ? (uint32_t)A.rb.capacity : 0u;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(A.rb.s, 0, (int)(16u * cap), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs2 =
+        __builtin_amdgcn_make_buffer_rsrc(A.rb.s2, 0, (int)(16u * cap), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(A.rb.a, 0, (int)cap, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr =
+        __builtin_amdgcn_make_buffer_rsrc(A.rb.r, 0, (int)(4u * cap), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(A.rb.d, 0, (int)cap, 0x00020000);
+    const uint32_t lane_off = (uint32_t)i;
+    bool ended = false;  // some episode of this board ended in the launch
+    Board last = b;      // the final board of that episode (its max tile goes to ep.w at the end)
+    // one transition with the words (wa, wb) of step t
+    auto one = [&](uint32_t wa, uint32_t wb, uint64_t t) {
+        const Board so = b;
+        bool done;
+        const uint32_t r = random_step(b, wa, wb, A.p4_thresh, done);
+        m.x += r;
+        m.y += 1u;
+        if constexpr (kSum) rsum += r;
+        if constexpr (kRing) {
+            if constexpr (kBuf) {
+                const uint32_t soff = row * n32;
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{so.r0, so.r1, so.r2, so.r3}, rs,
+                                                       lane_off * 16u, soff * 16u, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rs2,
+                                                       lane_off * 16u, soff * 16u, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), ra, lane_off, soff, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(r, rr, lane_off * 4u, soff * 4u, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rd, lane_off, soff, 0);
+            } else {
+                const int64_t slot = (int64_t)row * A.n + i;
+                A.rb.s[slot] = make_uint4(so.r0, so.r1, so.r2, so.r3);
+                A.rb.s2[slot] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+                A.rb.a[slot] = (uint8_t)(wa >> 30);
+                A.rb.r[slot] = (int32_t)r;
+                A.rb.d[slot] = (uint8_t)done;
+            }
+            row = row + 1u == rows ? 0u : row + 1u;
+        }
+        if (done) {  // taken by some lane of the wave on roughly 40 % of the steps
+            if (A.log) {
+                g2048_episode rec;
+                rec.step = t;
+                rec.q_sum = qs;
+                rec.board = (uint32_t)gid;
+                rec.episode = ep.x;
+                rec.score = m.x;
+                rec.moves = m.y;
+                rec.max_exp = max_exp(b);
+                rec.reserved = 0u;
+                A.log[i * A.log_slots + (int64_t)(ep.x % (uint32_t)A.log_slots)] = rec;
+            }
+            ep = make_uint4(ep.x + 1u, m.x, m.y, 0u);
+            last = b;
+            qs = 0.0;
+            ended = true;
+            if (autoreset) {
+                b = fresh_board_random(wa, wb, p4_16);
+                m = make_uint2(0u, 0u);
+            }
+        }
+    };
+    const int K = A.k_steps;
+    uint64_t pair = t0 >> 1;
+    int s = 0;
+    if (K > 0 && (t0 & 1u)) {  // odd start: the second half of the current pair
+        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+        one(blk.z, blk.w, t0);
+        ++pair;
+        s = 1;
     }
+    for (; s + 1 < K; s += 2, ++pair) {
+        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+        one(blk.x, blk.y, 2u * pair);
+        one(blk.z, blk.w, 2u * pair + 1u);
+    }
+    if (s < K) {
+        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+        one(blk.x, blk.y, 2u * pair);
+    }
+    const uint64_t t1 = t0 + (uint64_t)(K > 0 ? K : 0);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
-    if (A.reward_sum) A.reward_sum[i] += rsum;
-    if (A.rb.rows && i == 0) bump_count(A, (uint64_t)m.z | ((uint64_t)m.w << 32));
+    if (ended) {
+        ep.w = max_exp(last);
+        A.ep[i] = ep;
+        if (A.qsum) A.qsum[i] = 0.0;
+    }
+    if ((i & 63) == 0) A.clock[i >> 6] = t1;
+    if constexpr (kSum) A.reward_sum[i] += rsum;
+    if (kRing && i == 0) bump_count(A, t1);
 }
 
-__global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint4* meta, int64_t n,
+__global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint2* meta, int64_t n,
                                                   uint64_t board_offset, uint32_t seed_lo,
                                                   uint32_t seed_hi, uint32_t p4_thresh,
                                                   uint32_t epoch, const uint8_t* mask) {
@@ -374,10 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint4* meta, int
     const Board b = fresh_board(
         draw(seed_lo, seed_hi, board_offset + (uint64_t)i, DOMAIN_RESET, epoch), p4_thresh);
     board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    uint4 m = meta[i];
-    m.x = 0u;
-    m.y = 0u;
-    meta[i] = m;
+    meta[i] = make_uint2(0u, 0u);  // score, moves; the step clock keeps running
 }
 
 // available_moves_as_torch_unit_vector (src/board.py:128-135) of every board, as a bit mask.
@@ -501,6 +646,7 @@ struct g2048_env {
     uint8_t* board = nullptr;
     uint32_t* meta = nullptr;
     uint32_t* ep = nullptr;
+    uint64_t* clock = nullptr;
     unsigned long long* err = nullptr;
     bool owns = false;
     uint32_t epoch = 0;
@@ -533,7 +679,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
     DeviceGuard g(e->device);
     hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), 0, st,
-                       reinterpret_cast<uint4*>(e->board), reinterpret_cast<uint4*>(e->meta), e->n,
+                       reinterpret_cast<uint4*>(e->board), reinterpret_cast<uint2*>(e->meta), e->n,
                        e->board_offset, (uint32_t)e->seed, (uint32_t)(e->seed >> 32),
                        p4_thresh(e->flags), e->epoch, mask);
     G_HIP(hipGetLastError());
@@ -544,8 +690,9 @@ int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
 int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
     std::memset(&A, 0, sizeof(A));
     A.board = reinterpret_cast<uint4*>(e->board);
-    A.meta = reinterpret_cast<uint4*>(e->meta);
+    A.meta = reinterpret_cast<uint2*>(e->meta);
     A.ep = reinterpret_cast<uint4*>(e->ep);
+    A.clock = e->clock;
     A.n = e->n;
     A.board_offset = e->board_offset;
     A.seed_lo = (uint32_t)e->seed;
@@ -624,11 +771,15 @@ const char* g2048_last_error(void) { return g_err.c_str(); }
 int g2048_abi_version(void) { return G2048_ABI_VERSION; }
 
 int g2048_env_wrap(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_offset, int device_id,
-                   uint32_t flags, uint8_t* board, uint32_t* meta, uint32_t* ep, int reset,
-                   void* stream) {
+                   uint32_t flags, uint8_t* board, uint32_t* meta, uint32_t* ep, uint64_t* clock,
+                   int reset, void* stream) {
     if (!out || n <= 0) return fail(G2048_EINVAL, "env_wrap: need out != NULL and n > 0");
-    if (!board || !meta || !ep || !aligned16(board) || !aligned16(meta) || !aligned16(ep))
-        return fail(G2048_EINVAL, "env_wrap: board/meta/ep must be non-NULL and 16-byte aligned");
+    if (n > ((int64_t)1 << 32) - G2048_CLOCK_GROUP)
+        return fail(G2048_EINVAL, "env_wrap: n = %lld boards exceeds 2^32 - 64", (long long)n);
+    if (!board || !meta || !ep || !clock || !aligned16(board) || !aligned16(ep) ||
+        ((uintptr_t)meta & 7u) || ((uintptr_t)clock & 7u))
+        return fail(G2048_EINVAL, "env_wrap: board/meta/ep/clock must be non-NULL, board/ep "
+                                  "16-byte and meta/clock 8-byte aligned");
     if (flags & ~(uint32_t)(G2048_P4_10 | G2048_EGREEDY_FIXED | G2048_NO_AUTORESET))
         return fail(G2048_EINVAL, "env_wrap: unknown flags 0x%x", flags);
     DeviceGuard g(device_id);
@@ -642,6 +793,7 @@ int g2048_env_wrap(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_off
     e->board = board;
     e->meta = meta;
     e->ep = ep;
+    e->clock = clock;
     hipError_t he = hipMalloc(&e->err, sizeof(unsigned long long));
     if (he != hipSuccess) {
         delete e;
@@ -667,29 +819,34 @@ int g2048_env_create(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_o
                      int device_id, uint32_t flags, void* stream) {
     if (!out || n <= 0) return fail(G2048_EINVAL, "env_create: need out != NULL and n > 0");
     DeviceGuard g(device_id);
+    if (n > ((int64_t)1 << 32) - G2048_CLOCK_GROUP)
+        return fail(G2048_EINVAL, "env_create: n = %lld boards exceeds 2^32 - 64", (long long)n);
     uint8_t* board = nullptr;
     uint32_t *meta = nullptr, *ep = nullptr;
-    if (hipMalloc(&board, 16 * n) != hipSuccess || hipMalloc(&meta, 16 * n) != hipSuccess ||
-        hipMalloc(&ep, 16 * n) != hipSuccess) {
+    uint64_t* clock = nullptr;
+    const int64_t groups = G2048_CLOCK_WORDS(n);
+    auto release = [&]() {
         (void)hipFree(board);
         (void)hipFree(meta);
         (void)hipFree(ep);
+        (void)hipFree(clock);
+    };
+    if (hipMalloc(&board, 16 * n) != hipSuccess || hipMalloc(&meta, 8 * n) != hipSuccess ||
+        hipMalloc(&ep, 16 * n) != hipSuccess || hipMalloc(&clock, 8 * groups) != hipSuccess) {
+        release();
         return fail(G2048_ENOMEM, "env_create: hipMalloc of %lld boards failed", (long long)n);
     }
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(meta, 0, 16 * n, st) != hipSuccess ||
-        hipMemsetAsync(ep, 0, 16 * n, st) != hipSuccess) {
-        (void)hipFree(board);
-        (void)hipFree(meta);
-        (void)hipFree(ep);
+    if (hipMemsetAsync(meta, 0, 8 * n, st) != hipSuccess ||
+        hipMemsetAsync(ep, 0, 16 * n, st) != hipSuccess ||
+        hipMemsetAsync(clock, 0, 8 * groups, st) != hipSuccess) {
+        release();
         return fail(G2048_EHIP, "env_create: hipMemsetAsync failed");
     }
-    int rc = g2048_env_wrap(out, n, seed, board_offset, device_id, flags, board, meta, ep, 1,
-                            stream);
+    int rc = g2048_env_wrap(out, n, seed, board_offset, device_id, flags, board, meta, ep, clock,
+                            1, stream);
     if (rc) {
-        (void)hipFree(board);
-        (void)hipFree(meta);
-        (void)hipFree(ep);
+        release();
         return rc;
     }
     (*out)->owns = true;
@@ -703,16 +860,19 @@ void g2048_env_destroy(g2048_env* e) {
         (void)hipFree(e->board);
         (void)hipFree(e->meta);
         (void)hipFree(e->ep);
+        (void)hipFree(e->clock);
     }
     (void)hipFree(e->err);
     delete e;
 }
 
-int g2048_env_views(g2048_env* e, uint8_t** board, uint32_t** meta, uint32_t** ep) {
+int g2048_env_views(g2048_env* e, uint8_t** board, uint32_t** meta, uint32_t** ep,
+                    uint64_t** clock) {
     if (!e) return fail(G2048_EINVAL, "env_views: NULL env");
     if (board) *board = e->board;
     if (meta) *meta = e->meta;
     if (ep) *ep = e->ep;
+    if (clock) *clock = e->clock;
     return G2048_OK;
 }
 
@@ -877,8 +1037,19 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
     A.k_steps = k_steps;
     A.reward_sum = reinterpret_cast<long long*>(reward_sum);
     DeviceGuard g(e->device);
-    hipLaunchKernelGGL(k_rollout, dim3(grid_for(e->n)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), A);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // buffer-resource stores while every ring section (16 B per row at most) stays below 2^31 B
+    const dim3 grid(grid_for(e->n)), block(kBlock);
+    if (!rb) {
+        if (reward_sum) hipLaunchKernelGGL((k_rollout<false, false, true>), grid, block, 0, st, A);
+        else hipLaunchKernelGGL((k_rollout<false, false, false>), grid, block, 0, st, A);
+    } else if (rb->capacity <= ((int64_t)1 << 27)) {
+        if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);
+        else hipLaunchKernelGGL((k_rollout<true, true, false>), grid, block, 0, st, A);
+    } else {
+        if (reward_sum) hipLaunchKernelGGL((k_rollout<true, false, true>), grid, block, 0, st, A);
+        else hipLaunchKernelGGL((k_rollout<true, false, false>), grid, block, 0, st, A);
+    }
     G_HIP(hipGetLastError());
     return G2048_OK;
 }

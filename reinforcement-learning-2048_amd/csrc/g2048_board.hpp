@@ -200,23 +200,41 @@ __device__ __forceinline__ uint32_t max_exp(const Board& b) {
 }
 
 // ------------------------------------------------------------------ Philox4x32-10
+// a ^ b ^ k in ONE v_bitop3_b32 (truth table 0x96).  hipcc emits two v_xor_b32 when k is a
+// scalar operand (the key schedule always is); inline asm keeps it to one VALU op.  The "s"
+// constraint makes a non-uniform k a compile error instead of a silent readfirstlane.
+__device__ __forceinline__ uint32_t xor3_sk(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "s"(k));
+    return d;
+}
+
+__device__ __forceinline__ uint32_t or3_v(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_or3_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 // Same rounds, constants and counter layout as rocRAND's philox4x32_10 engine: the block for
 // (seed, subsequence s, offset 4t) is philox10({t_lo, t_hi, s_lo, s_hi}, {seed_lo, seed_hi}).
+// The key (k0, k1) must be wave-uniform (it is the env / sampler seed everywhere).
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair
         const uint64_t p0 = (uint64_t)c.x * 0xD2511F53u;
         const uint64_t p1 = (uint64_t)c.z * 0xCD9E8D57u;
-        c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1,
-                       (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
+        c = make_uint4(xor3_sk((uint32_t)(p1 >> 32), c.y, k0), (uint32_t)p1,
+                       xor3_sk((uint32_t)(p0 >> 32), c.w, k1), (uint32_t)p0);
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
     return c;
 }
 
-enum : uint32_t { DOMAIN_STEP = 0u, DOMAIN_RESET = 2u, DOMAIN_SAMPLE = 3u };
+// Domain bits 30-31 of the subsequence word: step draws of the action-given / eps-greedy modes
+// (one block per step), random-policy draws (one block per two steps), explicit resets, sampler.
+enum : uint32_t { DOMAIN_STEP = 0u, DOMAIN_RANDOM = 1u, DOMAIN_RESET = 2u, DOMAIN_SAMPLE = 3u };
 
 __device__ __forceinline__ uint4 draw(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
                                       uint32_t domain, uint64_t t) {
@@ -252,6 +270,85 @@ __device__ __forceinline__ Board fresh_board(uint4 u, uint32_t p4_thresh) {
     set_cell(b, ca, u.w < p4_thresh ? 2u : 1u);
     set_cell(b, cb, (u.x << 2) < p4_thresh ? 2u : 1u);
     return b;
+}
+
+// ------------------------------------------------------------------ random policy, lean step
+// The random-policy step (np.random.randint(4) actions, src/dqn_lib.py:20-21) draws two words
+// (wa, wb) -- half of a DOMAIN_RANDOM block, see random_block.  Bits:
+//   action      wa >> 30
+//   spawn cell  the k-th empty cell, k = floor((wa << 2) * n / 2^32)   (wa bits 0..29)
+//   spawn value a 4 (exponent 2) iff wb < p4_thresh
+//   auto-reset  (terminal steps, which neither move nor spawn): first cell (wa >> 26) & 15,
+//               second the k2-th of the other 15 with k2 = floor((wa << 6) * 15 / 2^32), a 4
+//               iff (wb & 0xFFFF) < p4_16 resp. (wb >> 16) < p4_16, p4_16 = p4_thresh / 2^16
+//               rounded (0.5 -> 32768 exactly; 0.1 -> 6554 = 0.100006).
+__device__ __forceinline__ uint4 random_block(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
+                                              uint64_t pair) {
+    return draw(seed_lo, seed_hi, gid, DOMAIN_RANDOM, pair);
+}
+
+__device__ __forceinline__ uint32_t p4_thresh16(uint32_t p4_thresh) {
+    return (p4_thresh + 0x8000u) >> 16;
+}
+
+// No legal move (src/dqn_lib.py:17-18: max(available_moves) == 0) without the 4-direction mask:
+// a board with both an empty and a non-empty cell always has one (some tile borders a hole), so
+// it is terminal iff it is full with no equal neighbours, or empty.
+__device__ __forceinline__ bool is_done(const Board& b) {
+    const uint32_t z = z80(b.r0) | z80(b.r1) | z80(b.r2) | z80(b.r3);
+    const uint32_t H = z80(b.r0 ^ (b.r0 >> 8)) | z80(b.r1 ^ (b.r1 >> 8)) |
+                       z80(b.r2 ^ (b.r2 >> 8)) | z80(b.r3 ^ (b.r3 >> 8));
+    const uint32_t V = z80(b.r0 ^ b.r1) | z80(b.r1 ^ b.r2) | z80(b.r2 ^ b.r3);
+    // one compare: min(no-move witnesses, any tile) == 0
+    return min(z | (H & 0x00808080u) | V, b.r0 | b.r1 | b.r2 | b.r3) == 0u;
+}
+
+// spawn() without branches; on_mask = 0 (spawn exponent 0) leaves the board as it is.
+__device__ __forceinline__ void spawn_if(Board& b, uint32_t u_cell, uint32_t u_val,
+                                         uint32_t p4_thresh, uint32_t on_mask) {
+    const uint32_t z0 = z80(b.r0), z1 = z80(b.r1), z2 = z80(b.r2), z3 = z80(b.r3);
+    const uint32_t p1 = __popc(z0), p2 = p1 + __popc(z1), p3 = p2 + __popc(z2);
+    const uint32_t n = p3 + __popc(z3);
+    uint32_t k = __umulhi(u_cell, n);
+    const uint32_t row = (uint32_t)(k >= p1) + (uint32_t)(k >= p2) + (uint32_t)(k >= p3);
+    uint32_t z = row == 0u ? z0 : row == 1u ? z1 : row == 2u ? z2 : z3;
+    k -= row == 0u ? 0u : row == 1u ? p1 : row == 2u ? p2 : p3;
+    uint32_t byte = 0;
+    const uint32_t c01 = __popc(z & 0x8080u);
+    if (k >= c01) { k -= c01; z >>= 16; byte = 2; }
+    byte += (uint32_t)(k >= ((z >> 7) & 1u));
+    set_cell(b, row * 4u + byte, (u_val < p4_thresh ? 2u : 1u) & on_mask);
+}
+
+// One random-policy transition of board b with words (wa, wb): slide (a board the chosen move
+// leaves unchanged is its own slide, so an invalid or terminal move spawns nothing), spawn,
+// terminal test of the board BEFORE the move.  Returns the merge gain (0 unless it moved).
+__device__ __forceinline__ uint32_t random_step(Board& b, uint32_t wa, uint32_t wb,
+                                                uint32_t p4_thresh, bool& done) {
+    Board nb = b;
+    const uint32_t gain = apply_move(nb, wa >> 30);
+    // all-ones iff the move changed the board.  The OR is opaque to the compiler (inline asm):
+    // otherwise hipcc splits it into four v_cmp whose lane masks it merges with s_or_b64, and at
+    // one wave per SIMD every SALU op costs an issue turn.
+    const uint32_t diff = or3_v(nb.r0 ^ b.r0, nb.r1 ^ b.r1, (nb.r2 ^ b.r2) | (nb.r3 ^ b.r3));
+    const uint32_t moved = (uint32_t)((int32_t)(diff | (0u - diff)) >> 31);
+    done = is_done(b);
+    spawn_if(nb, wa << 2, wb, p4_thresh, moved);
+    b = nb;
+    return gain;
+}
+
+// Auto-reset board of a terminal random-policy step (bits: see above).  The two tiles are placed
+// with 64-bit shifts into the board's halves {r0, r1} / {r2, r3} (fewer selects than set_cell).
+__device__ __forceinline__ Board fresh_board_random(uint32_t wa, uint32_t wb, uint32_t p4_16) {
+    const uint32_t ca = (wa >> 26) & 15u;
+    const uint32_t k2 = __umulhi(wa << 6, 15u);
+    const uint32_t cb = k2 + (uint32_t)(k2 >= ca);
+    const uint64_t ta = (uint64_t)((wb & 0xFFFFu) < p4_16 ? 2u : 1u) << (8u * (ca & 7u));
+    const uint64_t tb = (uint64_t)((wb >> 16) < p4_16 ? 2u : 1u) << (8u * (cb & 7u));
+    const uint64_t lo = (ca < 8u ? ta : 0u) | (cb < 8u ? tb : 0u);
+    const uint64_t hi = (ca < 8u ? 0u : ta) | (cb < 8u ? 0u : tb);
+    return Board{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
 // ------------------------------------------------------------------ policy (src/dqn_lib.py:16-30)

@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NT) void k_conv_forward_pipe(ConvNetArgs A) {
 // the rows written are bitwise those of g2048_convnet_forward.
 struct GreedyArgs {
     ConvNetArgs net;        // rows = the env's boards, n = its size, q = [n][4]
-    const uint4* meta;      // {score, moves, steps_lo, steps_hi}: the draw's counter
+    const uint64_t* clock;  // [ceil(n/64)] step clocks: the draw's counter (board i: clock[i/64])
     const uint32_t* ep;     // [n][4]: ep[4i] = episodes (the schedule's e)
     uint64_t board_offset;  // global id of board 0
     uint32_t seed_lo, seed_hi;
@@ -287,15 +287,15 @@ __global__ __launch_bounds__(NT) void k_conv_forward_greedy(GreedyArgs G) {
     int qn = 0;  // queue length (uniform)
     for (int64_t w0 = c0; w0 < c1; w0 += GW) {
         const bool last = w0 + GW >= c1;
-        uint4 m[4];
+        uint64_t tt[4];
         uint32_t e[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int64_t i = w0 + k * NT + t;
-            m[k] = make_uint4(0u, 0u, 0u, 0u);
+            tt[k] = 0u;
             e[k] = 0u;
             if (i < c1) {
-                m[k] = G.meta[i];
+                tt[k] = G.clock[i >> 6];
                 if (G.eps_decay > 0.0) e[k] = G.ep[4 * i];
             }
         }
@@ -305,9 +305,8 @@ __global__ __launch_bounds__(NT) void k_conv_forward_greedy(GreedyArgs G) {
             const int64_t i = w0 + k * NT + t;
             bool g = false;
             if (i < c1) {
-                const uint64_t tt = (uint64_t)m[k].z | ((uint64_t)m[k].w << 32);
                 const uint4 u = g2048::draw(G.seed_lo, G.seed_hi, G.board_offset + (uint64_t)i,
-                                            g2048::DOMAIN_STEP, tt);
+                                            g2048::DOMAIN_STEP, tt[k]);
                 g = !g2048::explores(u.y, g2048::step_eps(G.eps_decay, G.eps_min, G.eps_dev,
                                                           G.eps, e[k]));
             }
@@ -540,9 +539,10 @@ extern "C" G2048_API int g2048_convnet_forward_greedy(const g2048_convnet_params
     if (!p->w1 || !p->b1 || !p->w2 || !p->b2 || !p->fc1_w || !p->fc1_b || !p->fc2_w || !p->fc2_b)
         return g2048_fail(G2048_EINVAL, "convnet_forward_greedy: NULL parameter pointer");
     uint8_t* board = nullptr;
-    uint32_t *meta = nullptr, *ep = nullptr;
+    uint32_t* ep = nullptr;
+    uint64_t* clock = nullptr;
     uint64_t seed = 0, offset = 0;
-    if (g2048_env_views(env, &board, &meta, &ep) != G2048_OK ||
+    if (g2048_env_views(env, &board, nullptr, &ep, &clock) != G2048_OK ||
         g2048_env_rng(env, &seed, &offset) != G2048_OK)
         return G2048_EINVAL;
     const int64_t n = g2048_env_size(env);
@@ -550,7 +550,7 @@ extern "C" G2048_API int g2048_convnet_forward_greedy(const g2048_convnet_params
     GreedyArgs G;
     G.net = ConvNetArgs{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b,
                         board, nullptr, n, q_out};
-    G.meta = reinterpret_cast<const uint4*>(meta);
+    G.clock = clock;
     G.ep = ep;
     G.board_offset = offset;
     G.seed_lo = (uint32_t)seed;

@@ -18,6 +18,7 @@ G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOMEM, G2048_EBADINPUT = 0, -1, -2, -
 P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
 ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
+ABI_VERSION = 2  # include/g2048.h G2048_ABI_VERSION
 
 # every symbol include/g2048.h declares, with (restype, argtypes)
 _vp, _i64, _u64, _i32, _u32, _int, _dbl = (C.c_void_p, C.c_int64, C.c_uint64, C.c_int32,
@@ -25,9 +26,9 @@ _vp, _i64, _u64, _i32, _u32, _int, _dbl = (C.c_void_p, C.c_int64, C.c_uint64, C.
 _pp = C.POINTER(C.c_void_p)
 SIGNATURES = {
     "g2048_env_create": (_int, [_pp, _i64, _u64, _u64, _int, _u32, _vp]),
-    "g2048_env_wrap": (_int, [_pp, _i64, _u64, _u64, _int, _u32, _vp, _vp, _vp, _int, _vp]),
+    "g2048_env_wrap": (_int, [_pp, _i64, _u64, _u64, _int, _u32, _vp, _vp, _vp, _vp, _int, _vp]),
     "g2048_env_destroy": (None, [_vp]),
-    "g2048_env_views": (_int, [_vp, _pp, _pp, _pp]),
+    "g2048_env_views": (_int, [_vp, _pp, _pp, _pp, _pp]),
     "g2048_env_size": (_i64, [_vp]),
     "g2048_env_reset": (_int, [_vp, _vp, _vp]),
     "g2048_env_step": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -110,7 +111,7 @@ def load() -> C.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.g2048_abi_version() != 1:
+        if lib.g2048_abi_version() != ABI_VERSION:
             raise ImportError("libg2048.so ABI version mismatch")
         _lib = lib
     return _lib

@@ -89,8 +89,9 @@ class VecEnv2048:
     """N independent 2048 boards on one GPU, stepped by the HIP kernels in csrc/g2048.hip.
 
     board  uint8 [N, 16]  log2 exponents (== Board2048.log_scale().state, src/board.py:224-231)
-    meta   int32 [N, 4]   {score (= merge_score()), moves (= len(_action_history)), steps_lo, hi}
+    meta   int32 [N, 2]   {score (= merge_score()), moves (= len(_action_history))}
     ep     int32 [N, 4]   {episodes finished, last score, last moves, last max exponent}
+    clock  int64 [ceil(N/64)]  steps taken by each 64-board group (all equal; the Philox counter)
     """
 
     def __init__(self, n_boards: int, seed: int = 0x2048, device="cuda", board_offset: int = 0,
@@ -109,14 +110,16 @@ class VecEnv2048:
         lib = N.load()
         kw = dict(device=self.device)
         self.board = torch.zeros((self.n, 16), dtype=torch.uint8, **kw)
-        self.meta = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
+        self.meta = torch.zeros((self.n, 2), dtype=torch.int32, **kw)
         self.ep = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
+        self.clock = torch.zeros(((self.n + 63) // 64,), dtype=torch.int64, **kw)
         self._h = C.c_void_p()
         self._destroy = lib.g2048_env_destroy
         with torch.cuda.device(self.device):
             N.check(lib.g2048_env_wrap(C.byref(self._h), self.n, self.seed, self.board_offset,
                                        self.device.index, self.flags, N.ptr(self.board),
-                                       N.ptr(self.meta), N.ptr(self.ep), int(reset),
+                                       N.ptr(self.meta), N.ptr(self.ep), N.ptr(self.clock),
+                                       int(reset),
                                        N.stream_of(self.device)), "g2048_env_wrap")
 
     def __del__(self):
@@ -301,7 +304,7 @@ class VecEnv2048:
 
     @property
     def steps(self):
-        return (self.meta[:, 2].to(torch.int64) & 0xFFFFFFFF) | (self.meta[:, 3].to(torch.int64) << 32)
+        return self.clock.repeat_interleave(64)[:self.n]
 
     def max_tile(self):
         return torch.where(self.board.amax(1) > 0, 1 << self.board.amax(1).to(torch.int64), 0)

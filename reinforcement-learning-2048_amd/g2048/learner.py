@@ -458,7 +458,7 @@ class Trainer:
                           "min_eps": self.min_eps},
               "env": {"n": env.n, "seed": env.seed, "board_offset": env.board_offset,
                       "flags": env.flags, "epoch": env.epoch, "board": cpu(env.board),
-                      "meta": cpu(env.meta), "ep": cpu(env.ep)},
+                      "meta": cpu(env.meta), "ep": cpu(env.ep), "clock": cpu(env.clock)},
               "replay": {"capacity": rb.capacity, "s": cpu(rb.s), "s2": cpu(rb.s2), "a": cpu(rb.a),
                          "r": cpu(rb.r), "d": cpu(rb.d), "count": cpu(rb.count)},
               "learner": self.learner.state_dict()}
@@ -481,6 +481,7 @@ class Trainer:
         env.board.copy_(e["board"])
         env.meta.copy_(e["meta"])
         env.ep.copy_(e["ep"])
+        env.clock.copy_(e["clock"])
         env.epoch = e["epoch"]
         for k in ("s", "s2", "a", "r", "d", "count"):
             getattr(rb, k).copy_(st["replay"][k])

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
     assert set(_declared()) == set(N.SIGNATURES)
-    assert lib.g2048_abi_version() == 1
+    assert lib.g2048_abi_version() == 2
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     exported = sorted(set(re.findall(r" T (g2048_\w+)", out)))
@@ -55,13 +55,11 @@ def test_header_compiles_as_c():
 
 
 def test_c_caller_compiles_and_links(tmp_path):
-    """examples/abi_demo.c (a plain-C client) builds against the header and links libg2048.so."""
-    import g2048._native as N
+    """examples/abi_demo.c (a plain-C client) builds against the header and links libg2048.so;
+    build() leaves the same binary in examples/ for tests/test_abi_gpu.py to run on the GPU."""
+    import __graft_entry__ as G
 
-    libdir = os.path.dirname(N.LIB_PATH)
-    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(ROOT, "examples", "abi_demo.c"), "-L", libdir, "-l:libg2048.so",
-                    "-Wl,-rpath," + libdir, "-o", str(tmp_path / "abi_demo")], check=True)
+    G.build_abi_demo(str(tmp_path / "abi_demo"))
     assert (tmp_path / "abi_demo").exists()
 
 

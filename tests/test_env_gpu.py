@@ -180,6 +180,8 @@ def test_random_steps_with_replay_vs_oracle(g2048, n, flags):
             assert np.array_equal(_np(lg), o["legal"]), step
     assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
     assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
+    assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
+    assert (ref.clock == 120).all()
     for name in ["s", "s2", "a", "r", "d"]:
         assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
     assert int(_np(rb.count)[0]) == int(ref_rb.count[0]) == 3 * n
@@ -261,21 +263,79 @@ def test_egreedy_nonfinite_golden_rows(g2048, golden_dir):
         assert np.array_equal(qs[live], g["qmax" + suf][live], equal_nan=True)
 
 
-def test_rollout_equals_single_steps(g2048):
-    n, seed, k = 2048, 4242, 37
-    e1 = g2048.VecEnv2048(n, seed=seed, device=DEV)
-    e2 = g2048.VecEnv2048(n, seed=seed, device=DEV)
-    r1, r2 = g2048.ReplayBuffer(64 * n, device=DEV), g2048.ReplayBuffer(64 * n, device=DEV)
+@pytest.mark.parametrize("n,p4", [(2048, 0.5), (2048 + 77, 0.1)])
+def test_rollout_equals_single_steps(g2048, n, p4):
+    """K random steps in one launch == K single steps: odd and even starting clocks (the pair
+    block is split across launches), odd and even K, a partial last workgroup, both p4 modes,
+    an episode log attached (terminal records + q-sum resets come from the rollout too), and a
+    ring that wraps inside the launch."""
+    seed = 4242
+    e1 = g2048.VecEnv2048(n, seed=seed, device=DEV, p4=p4)
+    e2 = g2048.VecEnv2048(n, seed=seed, device=DEV, p4=p4)
+    l1, l2 = e1.attach_episode_log(64), e2.attach_episode_log(64)
+    r1, r2 = g2048.ReplayBuffer(48 * n, device=DEV), g2048.ReplayBuffer(48 * n, device=DEV)
     rs = torch.zeros(n, dtype=torch.int64, device=DEV)
-    e1.rollout(k, replay=r1, reward_sum=rs)
     acc = torch.zeros(n, dtype=torch.int64, device=DEV)
-    for _ in range(k):
-        r, _, _ = e2.step(None, replay=r2)
-        acc += r
-    assert torch.equal(e1.board, e2.board) and torch.equal(e1.meta, e2.meta)
+    total = 0
+    for k in (3, 37, 64, 1, 0, 2):
+        e1.rollout(k, replay=r1, reward_sum=rs)
+        for _ in range(k):
+            r, _, _ = e2.step(None, replay=r2)
+            acc += r
+        total += k
+        assert torch.equal(e1.board, e2.board) and torch.equal(e1.meta, e2.meta), k
+        assert torch.equal(e1.clock, e2.clock), k
+    assert int(e1.clock.min()) == int(e1.clock.max()) == total
     assert torch.equal(e1.ep, e2.ep) and torch.equal(rs, acc)
     for name in ["s", "s2", "a", "r", "d", "count"]:
         assert torch.equal(getattr(r1, name), getattr(r2, name)), name
+    g1, g2 = l1.read(), l2.read()
+    assert g1["step"].numel() > 0
+    for f in g1:
+        assert torch.equal(g1[f], g2[f]), f
+    assert torch.equal(l1.qsum, l2.qsum)
+
+
+def test_rollout_vs_oracle(g2048):
+    """The rollout against the CPU oracle directly (random-policy draws: half a Philox block per
+    step), starting from an odd clock."""
+    n, seed = 1000, 77
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV, board_offset=3 * n)
+    rb = g2048.ReplayBuffer(40 * n, device=DEV)
+    ref = O.OracleEnv(n, seed=seed, board_offset=3 * n)
+    ref_rb = O.OracleReplay(40 * n)
+    env.step(None, replay=rb)
+    ref.step(O.MODE_RANDOM, replay=ref_rb)
+    env.rollout(50, replay=rb)
+    for _ in range(50):
+        ref.step(O.MODE_RANDOM, replay=ref_rb)
+    assert np.array_equal(_np(env.board), ref.board)
+    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
+    assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
+    for name in ["s", "s2", "a", "r", "d", "count"]:
+        assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
+
+
+def test_large_random_steps_vs_oracle(g2048):
+    """Past 2^20 boards the step runs 256-thread workgroups (k_step<.., 256>), without the
+    episode-counter prefetch above 2^18 boards: n = 2^20 + 77 (partial last block), random
+    mode, replay append, checked against the oracle."""
+    n, seed = (1 << 20) + 77, 5
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    rb = g2048.ReplayBuffer(3 * n, device=DEV)
+    ref = O.OracleEnv(n, seed=seed)
+    ref_rb = O.OracleReplay(3 * n)
+    for step in range(3):
+        r, d, _ = env.step(None, replay=rb)
+        o = ref.step(O.MODE_RANDOM, replay=ref_rb)
+        assert np.array_equal(_np(r), o["reward"]), step
+        assert np.array_equal(_np(d), o["done"]), step
+    assert np.array_equal(_np(env.board), ref.board)
+    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
+    for name in ["s", "s2", "a", "r", "d", "count"]:
+        assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
 
 
 def test_sample_encode_vs_oracle(g2048):
@@ -488,7 +548,7 @@ def test_fused_dense64_step_matches_forward_plus_step(g2048, mode):
         torch.cuda.synchronize()
         assert torch.equal(qf, q), t
         assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
-    for name in ("board", "meta", "ep"):
+    for name in ("board", "meta", "ep", "clock"):
         assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
     for name in ("s", "s2", "a", "r", "d", "count"):
         assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name
@@ -527,7 +587,7 @@ def test_fused_dense64_step_skips_explorers(g2048, mode):
         a1, r1, d1 = envs[1].step_egreedy(q, eps, replay=rbs[1], **kw)
         torch.cuda.synchronize()
         assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
-    for name in ("board", "meta", "ep"):
+    for name in ("board", "meta", "ep", "clock"):
         assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
     for name in ("s", "s2", "a", "r", "d", "count"):
         assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name

@@ -441,13 +441,14 @@ def _greedy_mask(env, eps):
     (counter = step t, global board id; key = seed) from the oracle, u.y / 2^32 >= eps_b."""
     from oracle import oracle as O
 
-    meta = env.meta.cpu().numpy().view(np.uint32)
+    clock = env.clock.cpu().numpy().view(np.uint64)
     seed = env.seed & ((1 << 64) - 1)
     key = [seed & 0xFFFFFFFF, seed >> 32]
     out = np.zeros(env.n, bool)
     for i in range(env.n):
         gid = env.board_offset + i
-        u = O.philox([meta[i, 2], meta[i, 3], gid & 0xFFFFFFFF, gid >> 32], key)
+        t = int(clock[i // 64])
+        u = O.philox([t & 0xFFFFFFFF, t >> 32, gid & 0xFFFFFFFF, gid >> 32], key)
         out[i] = not (float(u[1]) * (1.0 / 4294967296.0) < eps[i])
     return torch.from_numpy(out).to(DEV)
 

@@ -13,7 +13,7 @@ int g2048_fail(int code, const char* fmt, ...) {
 }
 #include "../reinforcement-learning-2048_amd/csrc/g2048_qnet.hip"
 // env accessors of libg2048.so that g2048_convnet_forward_greedy links against (unused here)
-extern "C" int g2048_env_views(g2048_env*, uint8_t**, uint32_t**, uint32_t**) { return 1; }
+extern "C" int g2048_env_views(g2048_env*, uint8_t**, uint32_t**, uint32_t**, uint64_t**) { return 1; }
 extern "C" int64_t g2048_env_size(const g2048_env*) { return 0; }
 extern "C" int g2048_env_rng(const g2048_env*, uint64_t*, uint64_t*) { return 1; }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
