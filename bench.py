@@ -1,13 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark of the 2048 hot path on MI355X (contract: see DESIGN.md "Measurement").
+"""Benchmark of the 2048 hot path on MI355X (contract: DESIGN.md section 6).
 
-Default workload = BASELINE.json configs[1]: 65 536 vectorised boards per GPU, env step only
-(uniform random actions drawn in-kernel from Philox), one g2048_env_step launch per step,
-replayed from hipGraphs of `--graph-steps` steps.  value = env steps/s over all ranks.
-Extra fields report the K-steps-per-launch rollout kernel and (with --train) DQN updates/s.
+Headline (BASELINE.json configs[1]): 65 536 vectorised boards per GPU, env step only, uniform
+random actions drawn in-kernel from Philox.  One bench "step" = one g2048_env_rollout launch that
+moves every board `--rollout-k` (64) times and appends each transition (s, a, r, s', done) to an
+HBM replay ring of N * K rows -- the fused play_one_step + deque.append of src/dqn_lib.py:91-107
+with the boards resident in VGPRs.  value = env steps/s over all ranks = N * K * world * steps /
+(max over ranks of the timed wall time).
 
-Multi-GPU: one process per GPU (torchrun), boards sharded by board_offset = rank * N, no
-collective on the env path (weak scaling); timing = max over ranks.
+Extra fields: the one-launch-per-step kernel (g2048_env_step, hipGraph-replayed) at the same N,
+DQN updates/s + full training-loop iterations at B = 8192 for the dense-64 / conv / dense-ref
+nets in fp32 (fused HIP kernels where they exist) and fp64 (the reference's precision), the CPU
+baselines (oracle env on every host core; the reference train_step in fp64 on torch CPU).
+
+Multi-GPU: one process per GPU (`--gpus N` starts them through torch.distributed.run when no
+torchrun environment is present), boards sharded by board_offset = rank * N, no collective on
+the env path (weak scaling), the learner's gradients all-reduced over RCCL.
 """
 from __future__ import annotations
 
@@ -27,45 +35,49 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "2048 env steps/sec + DQN updates/sec at 64k parallel boards, 1→8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# algorithmic bytes per env step of k_step (random mode, reward + done + legal outputs):
-# board 16 R + 16 W, meta 16 R + 16 W, reward 4 W, done 1 W, legal 1 W
-STEP_BYTES = 70
-# rollout kernel with replay append, per step: transition s 16 + s' 16 + a 1 + r 4 + d 1
+FP32_PEAK_TF = 157.3   # dense f32 (vector / MFMA) peak, MI355X_MICROARCH.md
+FP64_PEAK_TF = 78.6    # dense f64 peak
+# Algorithmic bytes per env step:
+#   rollout (the headline kernel): the replay append s 16 + s' 16 + a 1 + r 4 + d 1 = 38 B; the
+#   board / meta / episode counters are read and written once per launch (not per step)
 ROLLOUT_BYTES = 38
+#   one launch per step, random mode: board 16 R + 16 W + reward 4 + done 1 = 37 B;
+#   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
+STEP_BYTES = 37
+STEP_BYTES_BOOKKEEPING = 54
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "r01", "pmc_step.json")
-
-
-def pmc_traffic(kernel: str, boards: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (tools/gpu_pmc.sh:
-    separate FETCH_SIZE / WRITE_SIZE runs, FETCH_SIZE x2 gfx950 correction), or None."""
+def pmc_record(key: str):
+    """HBM bytes per launch (+ issue counters) of one kernel@shape from the committed rocprofv3
+    PMC passes (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE / SQ passes), or None."""
     try:
         with open(PMC_FILE) as f:
-            rec = json.load(f).get(f"{kernel}@{boards}")
+            return json.load(f).get(key)
     except (OSError, ValueError):
-        return None, None
-    if not rec:
-        return None, None
-    return rec["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, ROOT)
+        return None
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=2000)
-    p.add_argument("--warmup", type=int, default=200)
+    p.add_argument("--steps", type=int, default=200, help="timed rollout launches")
+    p.add_argument("--warmup", type=int, default=20, help="untimed rollout launches")
     p.add_argument("--boards", type=int, default=65536)
+    p.add_argument("--rollout-k", type=int, default=64, help="env steps per rollout launch")
+    p.add_argument("--step-steps", type=int, default=2000,
+                   help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
     p.add_argument("--seed", type=int, default=0x2048)
-    p.add_argument("--rollout-k", type=int, default=64, help="steps per rollout launch (0 = skip)")
-    p.add_argument("--train", default="dense64,conv",
-                   help="learner workloads to time (comma list of dense64,conv,dense; '' = none)")
+    p.add_argument("--train", default="dense64,conv,dense",
+                   help="learner nets to time (comma list of dense64,conv,dense; '' = none)")
+    p.add_argument("--train-dtypes", default="fp32,fp64")
     p.add_argument("--train-updates", type=int, default=200)
     p.add_argument("--batch", type=int, default=8192)
     p.add_argument("--replay", type=int, default=1 << 20)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-seconds", type=float, default=8.0)
     return p.parse_args()
 
 
@@ -78,6 +90,7 @@ def launch_ranks(args) -> int:
     through torch.distributed.run as a CHILD process -- nothing here has touched the GPU -- and
     return its exit code."""
     import socket
+    import subprocess
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -85,8 +98,6 @@ def launch_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port",
            str(port), os.path.abspath(__file__), *sys.argv[1:]]
-    import subprocess
-
     return subprocess.call(cmd)
 
 
@@ -97,8 +108,8 @@ def setup_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
+    torch.cuda.set_device(dev)
     if world > 1:
-        torch.cuda.set_device(dev)
         if BACKEND == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -130,6 +141,25 @@ def sum_over_ranks(x: float, world: int, dev) -> float:
     return float(t.item())
 
 
+def timed(world, dev, fn, reps: int):
+    """(max-over-ranks wall seconds, this rank's HIP-event seconds) of `reps` calls of fn,
+    bracketed by a barrier + synchronize on both sides; the events sit on the stream the
+    kernels are launched on (torch's current stream, which the g2048 wrappers use)."""
+    stream = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier(world, dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    barrier(world, dev)
+    wall = time.perf_counter() - t0
+    return max_over_ranks(wall, world, dev), e0.elapsed_time(e1) / 1e3
+
+
 def capture(fn, n_steps: int):
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
@@ -143,11 +173,36 @@ def capture(fn, n_steps: int):
     return g
 
 
-def bench_env(args, world, rank, dev):
+# ------------------------------------------------------------------ headline: the rollout kernel
+def bench_rollout(args, world, rank, dev):
+    """W untimed + `steps` timed k_rollout launches (K env steps of every board each, replay
+    append into an N*K-row ring)."""
     import g2048
 
-    n = args.boards
+    n, k = args.boards, args.rollout_k
     env = g2048.VecEnv2048(n, seed=args.seed, device=dev, board_offset=rank * n)
+    rb = g2048.ReplayBuffer(n * k, device=dev)
+
+    def launch():
+        env.rollout(k, replay=rb)
+
+    for _ in range(max(args.warmup, 1)):
+        launch()
+    torch.cuda.synchronize()
+    wall, ev = timed(world, dev, launch, args.steps)
+    env.check_errors()
+    assert int(rb.count) == n * k
+    return dict(wall=wall, ev_s=ev, n=n, k=k)
+
+
+# ------------------------------------------------------------------ one launch per step
+def bench_step(args, world, rank, dev):
+    """g2048_env_step (random actions, reward / done / legal outputs) replayed from hipGraphs of
+    --graph-steps launches; every captured graph is replayed once before the timed region."""
+    import g2048
+
+    n, steps = args.boards, args.step_steps
+    env = g2048.VecEnv2048(n, seed=args.seed + 1, device=dev, board_offset=rank * n)
     reward = torch.empty(n, dtype=torch.int32, device=dev)
     done = torch.empty(n, dtype=torch.uint8, device=dev)
     legal = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -155,97 +210,46 @@ def bench_env(args, world, rank, dev):
     def one_step():
         env.step(None, reward=reward, done=done, legal=legal)
 
-    G = max(1, min(args.graph_steps, args.steps))
-    graphs = [(capture(one_step, G), args.steps // G)]  # (capture executes one eager step)
-    if args.steps % G:
-        graphs.append((capture(one_step, args.steps % G), 1))
-    # warm-up: the W untimed steps run as graph replays too, so the timed region starts with the
-    # GPU already in its steady state (eager launches leave it idle between steps); every captured
-    # graph is replayed at least once whatever W is, so the timed region never holds the first
-    # replay of a fresh graph
-    for g, _ in graphs:
+    G = max(1, min(args.graph_steps, steps))
+    graphs = [(capture(one_step, G), steps // G)]
+    if steps % G:
+        graphs.append((capture(one_step, steps % G), 1))
+    for g, _ in graphs:  # warm: no timed replay is the first replay of its graph
         g.replay()
-    for _ in range(args.warmup // G):
+    for _ in range(3):
         graphs[0][0].replay()
-    for _ in range(args.warmup % G):
-        one_step()
     torch.cuda.synchronize()
 
-    stream = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world, dev)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for g, reps in graphs:
-        for _ in range(reps):
-            g.replay()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    barrier(world, dev)
-    wall = time.perf_counter() - t0
-    ev_s = e0.elapsed_time(e1) / 1e3
-    wall_max = max_over_ranks(wall, world, dev)
+    def run_all():
+        for g, reps in graphs:
+            for _ in range(reps):
+                g.replay()
 
-    # single-launch kernel duration (events bracketing one eager launch, median of 200)
-    durs = []
-    for _ in range(200):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        one_step()
-        b.record(stream)
-        b.synchronize()
-        durs.append(a.elapsed_time(b) / 1e3)
-    durs.sort()
-    single = durs[len(durs) // 2]
+    wall, ev = timed(world, dev, run_all, 1)
     env.check_errors()
-    return dict(wall=wall_max, ev_s=ev_s, single_launch_s=single, n=n, G=G)
-
-
-def launch_floor(n: int, dev, G: int = 100, reps: int = 20) -> float:
-    """Per-launch time of a graph-replayed device copy of the step's board + meta bytes (32 B in,
-    32 B out per board): the floor any one-launch-per-step kernel over n boards pays here."""
-    src = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    # the launch floor here: a graph-replayed device copy of the kernel's board + meta bytes
+    src = torch.zeros((n, 24), dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
-    g = capture(lambda: dst.copy_(src), G)
-    g.replay()
-    torch.cuda.synchronize()
-    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(reps):
-        g.replay()
-    b.record()
-    b.synchronize()
-    return a.elapsed_time(b) / 1e3 / (G * reps)
+    gf = capture(lambda: dst.copy_(src), 100)
+    gf.replay()
+    _, fl = timed(1, dev, gf.replay, 20)
+    per = ev / steps
+    return {"kernel": "k_step<MODE_RANDOM> (g2048_env_step, one launch per env step)",
+            "env_steps_per_s": sum_over_ranks(n * steps / wall, world, dev),
+            "launch_us_graph": per * 1e6,
+            "launch_floor_us": fl / 2000 * 1e6,
+            "bytes_per_step": STEP_BYTES,
+            "bytes_per_step_with_bookkeeping": STEP_BYTES_BOOKKEEPING,
+            "hbm_frac": STEP_BYTES * n / per / 1e9 / HBM_PEAK_GBS,
+            "note": "launch-bound at 64k boards (2.4 MB per launch): compare the launch floor"}
 
 
-def bench_rollout(args, world, rank, dev):
-    """K random steps per launch with fused replay append (replay pre-fill path)."""
-    import g2048
-
-    n, k = args.boards, args.rollout_k
-    env = g2048.VecEnv2048(n, seed=args.seed + 1, device=dev, board_offset=rank * n)
-    rb = g2048.ReplayBuffer(n * k, device=dev)
-    env.rollout(k, replay=rb)
-    torch.cuda.synchronize()
-    reps = 20
-    stream = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(reps):
-        env.rollout(k, replay=rb)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    s = e0.elapsed_time(e1) / 1e3 / reps
-    return dict(launch_s=s, steps_per_s=n * k / s, bytes_per_launch=n * k * ROLLOUT_BYTES)
-
-
-def bench_train(args, world, rank, dev, net):
+# ------------------------------------------------------------------ learner
+def bench_train(args, world, rank, dev, net, dtype):
     """BASELINE configs[2]/[3] (configs[4] at --gpus 8): N boards + Double-DQN, replay 1M,
-    B=8192, fp32, graph-captured update with RCCL gradient all-reduce when world > 1.
-    Times (a) learner updates alone and (b) the full loop iteration = Q forward of the boards
-    on the greedy branch + fused epsilon-greedy step/append + 1 update, early (eps ~ 1) and late
-    (eps = min_epsilon) in the schedule."""
+    B = 8192, gradient all-reduce over RCCL when world > 1.  (a) learner updates alone,
+    (b) the training-loop iteration = Q of the greedy-branch boards + fused eps-greedy step /
+    append + 1 update, early (eps ~ 1) and late (eps = min_epsilon) in the schedule."""
     import g2048
     from g2048.learner import DQNLearner, Trainer, flops_per_update
 
@@ -253,81 +257,52 @@ def bench_train(args, world, rank, dev, net):
     C = max(args.replay // n, 1) * n
     env = g2048.VecEnv2048(n, seed=args.seed + 7, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(C, device=dev)
-    L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=args.batch, target_sync_every=100)
+    tdt = torch.float32 if dtype == "fp32" else torch.float64
+    L = DQNLearner(rb, net=net, dtype=tdt, batch_size=args.batch, target_sync_every=100)
     T = Trainer(env, rb, L, updates_per_step=1, min_fill=0)
     T.prefill(C // n)  # replay pre-filled by random-policy rollout steps (one launch)
     for _ in range(5):
         T.step()
-    L.update()  # the learner's own graph (the Trainer may run a graphed loop): captured here
+    L.update()  # the learner's own graphs (the Trainer may run a graphed loop): captured here
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    K = args.train_updates
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world, dev)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for _ in range(K):
-        L.update()
-    e1.record(stream)
-    torch.cuda.synchronize()
-    barrier(world, dev)
-    upd_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
-    upd_ev = e0.elapsed_time(e1) / 1e3
+    K = args.train_updates if dtype == "fp32" else max(args.train_updates // 4, 10)
+    upd_wall, upd_ev = timed(world, dev, L.update, K)
     K2 = max(K // 2, 1)
-    barrier(world, dev)
-    t0 = time.perf_counter()
-    for _ in range(K2):
-        T.step()
-    torch.cuda.synchronize()
-    barrier(world, dev)
-    loop_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
-    # (b) ran at the start of the eps schedule (eps ~ 1: the conv forward runs on the few
-    # greedy-branch boards only, the dense step skips all-explore groups).  (c) the same loop
-    # late in training: every board past eps_decay_episodes, eps = min_epsilon (Q of ~all boards).
+    loop_wall, _ = timed(world, dev, T.step, K2)
     eps_early = float(T.current_epsilon().mean())
-    env.ep[:, 0] = int(T.eps_decay)
+    env.ep[:, 0] = int(T.eps_decay)  # every board past the decay: eps = min_epsilon
     T.step()
     torch.cuda.synchronize()
     eps_late = float(T.current_epsilon().mean())
-    barrier(world, dev)
-    t0 = time.perf_counter()
-    for _ in range(K2):
-        T.step()
-    torch.cuda.synchronize()
-    barrier(world, dev)
-    late_wall = max_over_ranks(time.perf_counter() - t0, world, dev)
+    late_wall, _ = timed(world, dev, T.step, K2)
     loss = float(L.last_loss)
     env.check_errors()
     fl = flops_per_update(net, args.batch)
+    peak = FP32_PEAK_TF if dtype == "fp32" else FP64_PEAK_TF
+    tf = fl / (upd_ev / K) / 1e12
     return {"updates_per_s": K / upd_wall, "update_ms": upd_ev / K * 1e3,
-            "learner_tflops": fl / (upd_ev / K) / 1e12,
+            "learner_tflops": tf, "flop_frac": tf / peak, "peak_tflops": peak,
+            "path": ("fused HIP kernels" if L.fused else "torch-ROCm GEMMs after the HIP "
+                     "gather+encode kernel"),
             "loop_iter_ms": loop_wall / K2 * 1e3,
             "loop_env_steps_per_s": sum_over_ranks(n * K2 / loop_wall, world, dev),
             "loop_updates_per_s": K2 / loop_wall, "loop_epsilon_mean": eps_early,
             "loop_late_iter_ms": late_wall / K2 * 1e3,
             "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
             "loop_late_epsilon_mean": eps_late,
-            "batch": args.batch, "replay": C, "dtype": "fp32", "loss": loss,
-            "params": L.n_params}
+            "batch": args.batch, "replay": C, "dtype": dtype, "loss": loss,
+            "params": L.n_params, "graphed_loop": T.graph}
 
 
-def cpu_baseline(args):
-    """The oracle (plain-C restatement of src/board.py + dqn_lib.play_one_step) on ONE host core,
-    bounded sample: 4096 boards stepped with random actions for ~args.cpu_seconds."""
-    from oracle import oracle as O
+# ------------------------------------------------------------------ CPU baselines
+def cpu_baselines(args):
+    """The oracle env on every host core + the reference train_step in fp64 on torch CPU
+    (oracle/cpu_baseline.py; its C library was built by __graft_entry__.build())."""
+    from oracle import cpu_baseline as CB
 
-    O.build()
-    n = 4096
-    env = O.OracleEnv(n, seed=args.seed)
-    env.step(O.MODE_RANDOM)
-    steps, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < args.cpu_seconds:
-        env.step(O.MODE_RANDOM)
-        steps += n
-    dt = time.perf_counter() - t0
-    return dict(value=steps / dt, unit="env steps/s", cores=1, kind="port",
-                sample=f"oracle/oracle2048.c random-policy steps, {n} boards x {steps // n} steps "
-                       f"({dt:.1f} s, 1 thread)")
+    env = CB.env_baseline(args.cpu_seconds)
+    env["learner"] = [CB.learner_baseline("conv", b, updates=2) for b in (5000, 8192)]
+    return env
 
 
 def main():
@@ -335,25 +310,20 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     world, rank, dev = setup_dist(args)
-    torch.cuda.set_device(dev)
-    # the extra fields run first: the headline env-step timing then starts on a GPU that has
-    # been busy for a while (a cold start measured 2.96 instead of 2.72 us per step)
-    ro = bench_rollout(args, world, rank, dev) if args.rollout_k > 0 else None
-    if ro:
-        ro_total = sum_over_ranks(ro["steps_per_s"], world, dev)
+    ro = bench_rollout(args, world, rank, dev)
+    n, k = ro["n"], ro["k"]
+    value = n * k * world * args.steps / ro["wall"]
+    launch_s = ro["ev_s"] / args.steps
+    achieved = ROLLOUT_BYTES * n * k / launch_s / 1e9
+    step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
     for net in [x for x in args.train.split(",") if x]:
-        train[net] = bench_train(args, world, rank, dev, net)
-    r = bench_env(args, world, rank, dev)
-    total_steps = sum_over_ranks(r["n"] * args.steps, world, dev)
-    value = total_steps / r["wall"]
-    per_step_s = r["ev_s"] / args.steps
-    achieved = STEP_BYTES * r["n"] / per_step_s / 1e9
+        for dt in [x for x in args.train_dtypes.split(",") if x]:
+            train[f"{net}.{dt}"] = bench_train(args, world, rank, dev, net, dt)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)
-    traffic, traffic_src = pmc_traffic("k_step", r["n"])
-    floor_s = launch_floor(r["n"], dev)
+        cpu = cpu_baselines(args)
+    rec = pmc_record(f"k_rollout@{n}x{k}")
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -362,34 +332,31 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": r["wall"] / args.steps * 1e3,
+            "ms_per_step": ro["wall"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (fresh boards from Philox spawns, uniform random actions)",
-            "config": {"workload": "BASELINE configs[1]: 64k vectorised boards, env-step-only "
-                                   "(no learner), random policy",
-                       "boards_per_gpu": r["n"], "global_boards": r["n"] * world,
-                       "parallelism": f"dp{world} (boards sharded, no collective)",
-                       "launch": f"1 g2048_env_step per step, hipGraph of {r['G']} steps"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": "k_step<MODE_RANDOM>",
-                         "bytes_per_launch": STEP_BYTES * r["n"],
-                         "launch_us_graph": per_step_s * 1e6,
-                         "launch_us_single_eager": r["single_launch_s"] * 1e6,
-                         # at 64k boards the step is bound by the launch floor, not by HBM:
-                         "launch_floor_us": floor_s * 1e6,
-                         "floor_frac": floor_s / per_step_s},
+            "config": {"workload": "BASELINE configs[1]: 64k vectorised boards per GPU, env step "
+                                   "only (no learner), random policy; one step = one rollout "
+                                   f"launch moving every board {k} times with replay append",
+                       "boards_per_gpu": n, "global_boards": n * world,
+                       "env_steps_per_launch": n * k, "replay_rows": n * k,
+                       "parallelism": f"dp{world} (boards sharded, no collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": rec["hbm_bytes_per_launch"] if rec else None,
+                         "traffic_source": os.path.relpath(PMC_FILE, ROOT) if rec else None,
+                         "kernel": "k_rollout (g2048_env_rollout, ring + buffer stores)",
+                         "bytes_per_step": ROLLOUT_BYTES,
+                         "bytes_per_launch": ROLLOUT_BYTES * n * k,
+                         "launch_us": launch_s * 1e6,
+                         "issue": rec.get("issue") if rec else None},
             "cpu_baseline": cpu,
         }
-        if ro:
-            line["rollout"] = {"kernel": "k_rollout (K steps/launch, replay append)",
-                               "k": args.rollout_k, "env_steps_per_s": ro_total,
-                               "launch_ms": ro["launch_s"] * 1e3,
-                               "replay_write_GBs": ro["bytes_per_launch"] / ro["launch_s"] / 1e9}
+        if step:
+            line["step_kernel"] = step
         if train:
             line["learner"] = train
         print(json.dumps(line), flush=True)

@@ -52,8 +52,18 @@ def reference_module(model: nn.Module) -> nn.Module:
         seq.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
         return seq
     if isinstance(model, nn.Sequential):
-        import copy
-        return copy.deepcopy(model).cpu()
+        # plain nn.Linear / nn.ReLU layers (the build's Linear subclass only changes the fp64
+        # backward): the reference notebooks unpickle torch's own classes
+        layers = []
+        for m in model:
+            if isinstance(m, nn.Linear):
+                lin = nn.Linear(m.in_features, m.out_features, bias=m.bias is not None)
+                layers.append(lin.to(m.weight.dtype))
+            else:
+                layers.append(type(m)())
+        seq = nn.Sequential(*layers)
+        seq.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+        return seq
     raise TypeError("model.pt export supports the conv net and nn.Sequential MLPs")
 
 

@@ -288,10 +288,9 @@ class Trainer:
         self.env, self.replay, self.learner = env, replay, learner
         # graph: replay one captured hipGraph per iteration (fused step + updates) once the
         # learner is updating; default on for the fused fp32 learners on one process
-        self.graph = (learner.fused and learner.graph and learner.world == 1) if graph is None \
-            else bool(graph)
-        if self.graph and not (learner.fused and learner.world == 1):
-            raise ValueError("the graphed loop needs a fused learner on one process")
+        self.graph = (learner.fused and learner.graph) if graph is None else bool(graph)
+        if self.graph and not learner.fused:
+            raise ValueError("the graphed loop needs a fused learner")
         self._loop_graph = None
         self.updates_per_step = int(updates_per_step)
         self.min_fill = int(min_fill if min_fill is not None else learner.B)
@@ -348,6 +347,8 @@ class Trainer:
         (boards, ring position, update counter) from device memory, so replay k equals eager
         iteration k bit for bit."""
         L = self.learner
+        if L.world > 1:
+            return self._graphed_iteration_dp()
         if self._loop_graph is None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -358,6 +359,27 @@ class Trainer:
             self._loop_graph = g
         self._loop_graph.replay()
         L.updates += self.updates_per_step
+
+    def _graphed_iteration_dp(self) -> None:
+        """Data-parallel form: graph A = the rollout step + the first update's gradient, the
+        flat-bucket all-reduce (RCCL) between replays, graph B = Adam (+ target sync); further
+        updates of the iteration run the learner's own two-graph update."""
+        L = self.learner
+        if self._loop_graph is None:
+            ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(ga):
+                self._rollout_step()
+                L._compute_grads()
+            with torch.cuda.graph(gb):
+                L._apply()
+            self._loop_graph = (ga, gb)
+        ga, gb = self._loop_graph
+        ga.replay()
+        L._allreduce()
+        gb.replay()
+        L.updates += 1
+        for _ in range(self.updates_per_step - 1):
+            L.update()
 
     def step(self) -> None:
         if self.track:

@@ -68,3 +68,72 @@ def test_two_ranks_stay_in_lockstep(tmp_path, net):
     assert res["finite"] and res["moved"]
     assert res["diff_loss"], "ranks should see different minibatches"
     assert res["same"], "replicas diverged"
+
+
+def _trainer_worker(rank, world, port, net, out_dir):
+    """The graphed data-parallel training loop (graph A = fused step + gradient, RCCL/gloo
+    all-reduce, graph B = Adam) against the eager loop: same boards, rings, weights, bitwise."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "reinforcement-learning-2048_amd")]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import g2048
+    from g2048.learner import DQNLearner, Trainer
+
+    n = 1024
+    res = []
+    for graph in (True, False):
+        env = g2048.VecEnv2048(n, seed=11, device=dev, board_offset=rank * n)
+        rb = g2048.ReplayBuffer(16 * n, device=dev)
+        L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=512, target_sync_every=3,
+                       seed=5, graph=graph)
+        T = Trainer(env, rb, L, updates_per_step=1, min_fill=0, graph=graph,
+                    eps_decay_episodes=20.0)
+        T.prefill(4)
+        for _ in range(7):
+            T.step()
+        torch.cuda.synchronize()
+        res.append(torch.cat([env.board.reshape(-1).float().cpu(), rb.s.reshape(-1).float().cpu(),
+                              torch.cat([p.detach().reshape(-1) for p in L.model.parameters()]).cpu(),
+                              torch.cat([p.detach().reshape(-1) for p in L.target.parameters()]).cpu()]))
+        assert T.graph == graph
+    same = torch.equal(res[0], res[1])
+    flags = [torch.zeros(1) for _ in range(world)]
+    dist.all_gather(flags, torch.tensor([1.0 if same else 0.0]))
+    if rank == 0:
+        torch.save({"same": all(float(f) == 1.0 for f in flags)}, os.path.join(out_dir, "res.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("net", ["conv", "dense64"])
+def test_graphed_dp_loop_equals_eager(tmp_path, net):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    mp.spawn(_trainer_worker, args=(2, _free_port(), net, str(tmp_path)), nprocs=2, join=True)
+    res = torch.load(os.path.join(tmp_path, "res.pt"), weights_only=True)
+    assert res["same"], "graphed DP loop differs from the eager DP loop"
+
+
+def test_bench_two_ranks():
+    """`bench.py --gpus 2` starts its own two ranks (gloo here: one GPU), shards the boards and
+    reports the whole-job line; the learner leg runs the DP update with the all-reduce."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, G2048_BENCH_BACKEND="gloo")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--steps", "20", "--warmup", "5", "--step-steps", "200",
+                          "--train", "dense64", "--train-dtypes", "fp32", "--train-updates", "20",
+                          "--no-cpu-baseline"], capture_output=True, text=True, env=env,
+                         timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert line["config"]["global_boards"] == 2 * 65536
+    assert line["value"] > 0 and line["step_kernel"]["env_steps_per_s"] > 0
+    assert line["learner"]["dense64.fp32"]["graphed_loop"] is True

@@ -1,9 +1,15 @@
 #!/bin/bash
-# GPU box: two separate PMC passes (FETCH_SIZE, WRITE_SIZE), kernel-trace only, no sys/runtime trace
+# GPU box: three separate PMC passes over tools/pmc_step.py (FETCH_SIZE; WRITE_SIZE; SQ issue
+# counters), kernel-trace only, no sys/runtime trace; summary -> gpurun_out/pmc.json
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_fetch -o fetch -- python tools/pmc_step.py > gpurun_out/pmc_fetch.log 2>&1 || { tail -30 gpurun_out/pmc_fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/pmc_write -o write -- python tools/pmc_step.py > gpurun_out/pmc_write.log 2>&1 || { tail -30 gpurun_out/pmc_write.log; exit 1; }
-find gpurun_out/pmc_fetch gpurun_out/pmc_write -name "*.csv" | head
-python tools/pmc_summary.py 'gpurun_out/pmc_fetch/**/*counter_collection.csv' 'gpurun_out/pmc_write/**/*counter_collection.csv' gpurun_out/pmc_step.json
+run_pass() {  # name, counters...
+    local name=$1; shift
+    timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
+        -d gpurun_out/pmc_$name -o $name -- python tools/pmc_step.py > gpurun_out/pmc_$name.log 2>&1 \
+        || { tail -30 gpurun_out/pmc_$name.log; return 1; }
+}
+run_pass fetch FETCH_SIZE && run_pass write WRITE_SIZE && \
+run_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA && \
+python tools/pmc_summary.py gpurun_out/pmc.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Workload for the PMC passes (FETCH_SIZE / WRITE_SIZE): eager g2048_env_step launches at
-64k boards (the bench config) and at 4M boards (past the 256 MiB Infinity Cache, where the
-counters see the real HBM stream), plus a k_rollout launch with replay append."""
+"""Workload for the rocprofv3 PMC passes (tools/gpu_pmc.sh): the bench's headline launch
+(k_rollout, 65 536 boards x K = 64 steps, replay ring of N*K rows), the one-launch-per-step
+kernel at 64k boards, and both at 4M boards (past the 256 MiB Infinity Cache, where the
+memory-side counters see the HBM stream: rollout K = 16)."""
 import os
 import sys
 
@@ -11,17 +12,20 @@ import torch  # noqa: E402
 
 import g2048  # noqa: E402
 
-for n in (65536, 1 << 22):
+# boards -> rollout K (tools/pmc_summary.py keys the results by this table)
+SHAPES = {65536: 64, 1 << 22: 16}
+
+for n, k in SHAPES.items():
     env = g2048.VecEnv2048(n, seed=3, device="cuda:0")
+    rb = g2048.ReplayBuffer(n * k, device="cuda:0")
+    for _ in range(8):
+        env.rollout(k, replay=rb)
+    torch.cuda.synchronize()
     r = torch.empty(n, dtype=torch.int32, device="cuda:0")
     d = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     lg = torch.empty(n, dtype=torch.uint8, device="cuda:0")
-    for _ in range(50):
+    for _ in range(20):
         env.step(None, reward=r, done=d, legal=lg)
-    torch.cuda.synchronize()
-    rb = g2048.ReplayBuffer(n * 8, device="cuda:0")
-    for _ in range(3):
-        env.rollout(8, replay=rb)
     torch.cuda.synchronize()
     del env, rb
     torch.cuda.empty_cache()

@@ -1,43 +1,77 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc passes into per-launch HBM bytes (profiles/<round>/pmc_step.json).
-gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reads 1/2 of the bytes of a
-wide (16 B/lane) coalesced stream -> x2; WRITE_SIZE is exact for 16-B stores.  Units: KB."""
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh) into profiles/<round>/pmc.json.
+
+HBM bytes per launch (MI355X_MICROARCH.md, HBM section, gfx950): FETCH_SIZE reads 1/2 of the
+bytes of a wide (16 B/lane) coalesced read stream -> x2; WRITE_SIZE is exact for 16-B stores.
+Units: KB.  Infinity-Cache hits are counted, so at 64k boards (the working set fits in the
+256 MiB cache) the numbers are memory-side traffic, not HBM-only; the 4M-board rows are past it.
+Issue counters (one SQ pass): per wave and env step, VALU / SALU instructions and the wave's
+cycles (quad-cycles, as SQ reports them); issue_util = (VALU + SALU active) / wave cycles.
+Usage: pmc_summary.py <out.json> <pass-dir> [<pass-dir> ...]"""
 import csv
 import glob
 import json
+import os
 import statistics
 import sys
 from collections import defaultdict
 
-
-def load(pattern, counter):
-    out = defaultdict(list)
-    for f in glob.glob(pattern, recursive=True):
-        for r in csv.DictReader(open(f)):
-            if r.get("Counter_Name") != counter:
-                continue
-            name = r["Kernel_Name"]
-            key = ("k_step" if "k_step" in name else "k_rollout" if "k_rollout" in name else None)
-            if key is None:
-                continue
-            out[(key, int(r["Grid_Size"]) if "Grid_Size" in r else int(r.get("Grid_Size_X", 0)))].append(
-                float(r["Counter_Value"]))
-    return out
+SHAPES = {65536: 64, 1 << 22: 16}  # tools/pmc_step.py: boards -> rollout K
 
 
-def main(fetch_glob, write_glob, out_path):
-    fe, wr = load(fetch_glob, "FETCH_SIZE"), load(write_glob, "WRITE_SIZE")
+def kernel_key(name: str, grid: int):
+    if "k_rollout" in name:
+        return f"k_rollout@{grid}x{SHAPES.get(grid, 0)}"
+    if "k_step" in name:
+        return f"k_step@{grid}"
+    return None
+
+
+def load(dirs):
+    vals = defaultdict(lambda: defaultdict(list))  # key -> counter -> [per dispatch]
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            per = defaultdict(float)  # (dispatch, counter) -> summed over dimensions
+            meta = {}
+            for r in csv.DictReader(open(f)):
+                grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+                key = kernel_key(r["Kernel_Name"], grid)
+                if key is None:
+                    continue
+                did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                per[(did, r["Counter_Name"])] += float(r["Counter_Value"])
+                meta[did] = key
+            for (did, cn), v in per.items():
+                vals[meta[did]][cn].append(v)
+    return vals
+
+
+def main(out_path, *dirs):
+    vals = load(dirs)
     res = {}
-    for key in sorted(set(fe) | set(wr)):
-        kern, grid = key
-        f = statistics.median(fe.get(key, [0.0]))
-        w = statistics.median(wr.get(key, [0.0]))
-        res[f"{kern}@{grid}"] = {"kernel": kern, "boards": grid, "dispatches": len(fe.get(key, [])),
-                                 "fetch_kb_raw": f, "write_kb": w,
-                                 "hbm_bytes_per_launch": (2 * f + w) * 1024}
+    for key in sorted(vals):
+        c = {cn: statistics.median(v) for cn, v in vals[key].items()}
+        rec = {"dispatches": max(len(v) for v in vals[key].values())}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            rec.update(fetch_kb_raw=c["FETCH_SIZE"], write_kb=c["WRITE_SIZE"],
+                       hbm_bytes_per_launch=(2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+        if "SQ_WAVES" in c and c["SQ_WAVES"] > 0:
+            steps = int(key.split("x")[1]) if key.startswith("k_rollout") else 1
+            per = lambda n: c.get(n, 0.0) / c["SQ_WAVES"] / steps  # noqa: E731
+            rec["issue"] = {
+                "valu_insts_per_wave_step": per("SQ_INSTS_VALU"),
+                "salu_insts_per_wave_step": per("SQ_INSTS_SALU"),
+                "valu_active_quads_per_wave_step": per("SQ_ACTIVE_INST_VALU"),
+                "salu_active_quads_per_wave_step": per("SQ_ACTIVE_INST_SCA"),
+                "wave_quads_per_wave_step": per("SQ_WAVE_CYCLES"),
+                "issue_util": (c.get("SQ_ACTIVE_INST_VALU", 0) + c.get("SQ_ACTIVE_INST_SCA", 0))
+                / max(c.get("SQ_WAVE_CYCLES", 1), 1),
+            }
+        res[key] = rec
+    os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(sys.argv[1], *sys.argv[2:])
