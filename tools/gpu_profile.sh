@@ -1,0 +1,14 @@
+#!/bin/bash
+# GPU box: the round's committed evidence under gpurun_out/prof/ -- the default bench line, the
+# rocprofv3 kernel-trace --stats summary of the same bench command, and the PMC passes.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/prof
+timeout -k 10 420 python bench.py > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err \
+    || { tail -20 gpurun_out/prof/bench.err; exit 1; }
+rm -rf /tmp/prof_bench
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_bench -o bench \
+    -- python bench.py --no-cpu-baseline > gpurun_out/prof/bench_rocprof.json 2> gpurun_out/prof/bench_rocprof.err \
+    || { tail -20 gpurun_out/prof/bench_rocprof.err; exit 1; }
+cp "$(find /tmp/prof_bench -name '*kernel_stats.csv' | head -1)" gpurun_out/prof/bench_kernel_stats.csv
+bash tools/gpu_pmc.sh && cp gpurun_out/pmc.json gpurun_out/prof/pmc.json
