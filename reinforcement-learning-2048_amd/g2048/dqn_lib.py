@@ -31,10 +31,47 @@ def board_as_flattened_tensor(env: VecEnv2048, device=None, dtype=torch.float64)
     return env.encode(dtype, conv=False)
 
 
+class BoardBatch:
+    """A batch of boards that are not an env's (sampled replay rows, the before / after boards
+    of a step): the same `board` (u8 [n, 16] exponents), `n`, `device` and `encode()` as
+    VecEnv2048, so every board_to_tensor_function -- the reference's two or a caller's own --
+    takes either."""
+
+    def __init__(self, board: torch.Tensor):
+        self.board = board
+        self.n = board.shape[0]
+        self.device = board.device
+
+    def encode(self, dtype=torch.float32, conv: bool = True):
+        x = self.board.to(dtype)
+        return x.view(self.n, 1, 4, 4) if conv else x
+
+
+_FUSED_ENCODERS = (board_as_4d_tensor, board_as_flattened_tensor)
+
+
 def reward_func_merge_score(board=None, next_board=None, action=None, done=None):
     """src/dqn_lib.py:87-88: next.merge_score() - board.merge_score().  The env kernel computes
     exactly this gain in-register; passing this function selects the fused path."""
     raise RuntimeError("reward_func_merge_score is computed inside the env step kernel")
+
+
+def _custom_rewards(reward_function, s, s2, action, done, replay_buffer, row0):
+    """A caller's reward_function(board, next_board, action, done) (src/dqn_lib.py:97,104) over
+    the whole batch -- BoardBatch views of the boards before / after the move (s' = s for
+    terminal and invalid moves, as the reference's peek_action), actions and done flags as
+    tensors -- written over the kernel's merge-score rewards in the ring rows just appended.
+    The ring stores rewards as int32 (the reference's merge-score rewards are ints)."""
+    r = reward_function(BoardBatch(s), BoardBatch(s2), action, done)
+    r = torch.as_tensor(r, device=s.device)
+    if r.shape != (s.shape[0],):
+        raise ValueError(f"reward_function must return one reward per board ({s.shape[0]})")
+    ri = r.to(torch.int32)
+    if r.is_floating_point() and not torch.equal(ri.to(r.dtype), r):
+        raise TypeError("the replay ring stores int32 rewards; reward_function returned "
+                        "non-integer values")
+    replay_buffer.r[row0:row0 + s.shape[0]].copy_(ri)
+    return ri
 
 
 # ------------------------------------------------------------------ acting (src/dqn_lib.py:16-30, 91-107)
@@ -66,15 +103,23 @@ def play_one_step(env: VecEnv2048, epsilon, model: torch.nn.Module, replay_buffe
     F5), move + spawn, merge-score reward, done flag, replay append.  Terminal boards record
     (s, a, 0, s, 1) and are re-dealt.  With epsilon >= 1 no Q-values are needed and `model`
     may be None (the random branch returns before the forward, :20-21).
+    A reward_function other than reward_func_merge_score is called as the reference calls it
+    (board, next_board, action, done), batched (see _custom_rewards); it needs the replay
+    buffer, where the transition's s' lives after the auto-reset.
     Returns (env, actions, rewards, dones, max_q_values)."""
-    if reward_function is not reward_func_merge_score:
-        raise NotImplementedError("only the reference reward (merge-score gain) is fused in the "
-                                  "env kernel; compute custom rewards from the replay rows")
+    custom = reward_function is not reward_func_merge_score
+    if custom and replay_buffer is None:
+        raise ValueError("a custom reward_function needs the replay buffer (it holds s')")
     if model is None or (not isinstance(epsilon, torch.Tensor) and float(epsilon) >= 1.0):
         q = torch.zeros((env.n, 4), dtype=torch.float32, device=env.device)
     else:
         q = q_values(env, model, board_to_tensor_function)
+    s = env.board.clone() if custom else None
+    row0 = int(env.clock[0]) % (replay_buffer.capacity // env.n) * env.n if custom else 0
     action, reward, done = env.step_egreedy(q, epsilon, replay=replay_buffer)
+    if custom:
+        reward = _custom_rewards(reward_function, s, replay_buffer.s2[row0:row0 + env.n],
+                                 action, done, replay_buffer, row0)
     return env, action, reward, done, q.amax(1)
 
 
@@ -94,13 +139,27 @@ def sample_experiences(batch_size: int, replay_buffer: ReplayBuffer, device=None
                        extract_sample_function: Callable = extract_samples_conv,
                        dtype=torch.float64, idx: torch.Tensor | None = None):
     """src/dqn_lib.py:67-84: B indices uniform with replacement over the filled rows
-    (np.random.randint(len, size=B) -> torch RNG on the device, graph-safe), then one fused
-    gather + log2-encode kernel.  Returns (states, actions i64, rewards, next_states, dones)."""
+    (np.random.randint(len, size=B) -> torch RNG on the device, graph-safe), then the gather +
+    encode.  With the reference's encoders (or None) the gather and the log2 encode are one
+    fused kernel; any other board_to_tensor_function is applied, as in the reference
+    (:71-80), to the sampled boards (BoardBatch views of the gathered rows) before
+    extract_sample_function.  Returns (states, actions i64, rewards, next_states, dones)."""
     if idx is None:
         idx = (torch.rand(batch_size, dtype=torch.float64, device=replay_buffer.device)
                * replay_buffer.count.to(torch.float64)).to(torch.int64)
-    s, a, r, s2, d, _ = replay_buffer.sample_encode(batch_size, dtype, idx=idx)
-    return extract_sample_function(s), a, r, extract_sample_function(s2), d
+    if board_to_tensor_function is None or board_to_tensor_function in _FUSED_ENCODERS:
+        s, a, r, s2, d, _ = replay_buffer.sample_encode(batch_size, dtype, idx=idx)
+        return extract_sample_function(s), a, r, extract_sample_function(s2), d
+    _, a, r, _, d, _ = replay_buffer.sample_encode(batch_size, dtype, idx=idx, want_s=False,
+                                                   want_s2=False)
+    dev = replay_buffer.device
+    s = board_to_tensor_function(BoardBatch(replay_buffer.s[idx]), dev, dtype)
+    s2 = board_to_tensor_function(BoardBatch(replay_buffer.s2[idx]), dev, dtype)
+
+    def layout(x):  # the reference layouts apply to 16 values per board; other encodings pass
+        return extract_sample_function(x.reshape(batch_size, 16)) if x[0].numel() == 16 else x
+
+    return layout(s), a, r, layout(s2), d
 
 
 def one_hot(tensor: torch.Tensor, no_outputs: int, device=None) -> torch.Tensor:
@@ -142,14 +201,22 @@ def targets_from_q(q_online_next, q_target_next, rewards, dones, discount_factor
     return rewards.to(next_q.dtype) + disc.to(next_q.dtype) * next_q
 
 
+def is_mse_sum(loss_fn) -> bool:
+    """None or nn.MSELoss(reduction='sum') -- the loss of the reference configs
+    (src/configs/double_dqn_conv.py:38), the one the fused HIP learner kernels implement."""
+    return loss_fn is None or (isinstance(loss_fn, torch.nn.MSELoss) and loss_fn.reduction == "sum")
+
+
 def dqn_loss(model, target_model, states, actions, rewards, next_states, dones, discount_factor,
-             use_double_dqn: bool = True):
-    """MSELoss(reduction='sum') of Q_online(s)[a] against the Bellman target (:146-158).
+             use_double_dqn: bool = True, loss_fn: Callable | None = None):
+    """loss_fn(Q_online(s)[a], y) against the Bellman target (:146-158); None = MSELoss(sum).
     The reference's one_hot-mask-and-sum picks the same element as gather (exact)."""
     y = bellman_targets(model, target_model, rewards, next_states, dones, discount_factor,
                         use_double_dqn)
     q = model(states).gather(1, actions[:, None].to(torch.int64))[:, 0]
-    return ((q - y) ** 2).sum(), q, y
+    if loss_fn is None:
+        return ((q - y) ** 2).sum(), q, y
+    return loss_fn(q, y), q, y
 
 
 def train_step(batch_size: int, discount_factor: float, model: torch.nn.Module,
@@ -160,8 +227,8 @@ def train_step(batch_size: int, discount_factor: float, model: torch.nn.Module,
                extract_samples_function: Callable = extract_samples_conv,
                reference_compat: bool = False, idx: torch.Tensor | None = None):
     """src/dqn_lib.py:119-164 on one minibatch sampled from the HBM replay ring.
-    loss_fn is accepted for signature parity; the loss is MSE(sum) as in the configs
-    (src/configs/double_dqn_conv.py:38).  reference_compat=True reproduces the reference's
+    loss_fn(q, y) as the reference calls it (:158); None = MSELoss(reduction='sum'), the configs'
+    loss (src/configs/double_dqn_conv.py:38).  reference_compat=True reproduces the reference's
     backward -> zero_grad -> step order, in which the optimizer never updates (F1)."""
     dtype = _model_dtype(model)
     states, actions, rewards, next_states, dones = sample_experiences(
@@ -169,14 +236,14 @@ def train_step(batch_size: int, discount_factor: float, model: torch.nn.Module,
         dtype=dtype, idx=idx)
     if reference_compat:
         loss, _, _ = dqn_loss(model, target_model, states, actions, rewards, next_states, dones,
-                              discount_factor, use_double_dqn)
+                              discount_factor, use_double_dqn, loss_fn)
         loss.backward()
         optimizer.zero_grad()
         optimizer.step()
         return loss
     optimizer.zero_grad()
     loss, _, _ = dqn_loss(model, target_model, states, actions, rewards, next_states, dones,
-                          discount_factor, use_double_dqn)
+                          discount_factor, use_double_dqn, loss_fn)
     loss.backward()
     optimizer.step()
     return loss

@@ -30,7 +30,7 @@ class DQNLearner:
                  batch_size: int = 8192, discount_factor: float = 0.8, lr: float = 1e-2,
                  use_double_dqn: bool = True, target_sync_every: int = 100, graph: bool = True,
                  seed: int = 0, model: torch.nn.Module | None = None,
-                 process_group=None, sampler=None):
+                 process_group=None, sampler=None, loss_fn=None):
         self.replay = replay
         self.device = replay.device
         self.dtype = dtype
@@ -43,6 +43,9 @@ class DQNLearner:
         # sampler(B, replay) -> int64 indices on the device; None = uniform with replacement over
         # the filled rows (src/dqn_lib.py:68), drawn by torch's graph-safe device RNG
         self.sampler = sampler
+        # loss_fn(q, y) of train_step (src/dqn_lib.py:158): None / MSELoss(sum) -- the configs'
+        # loss, which the fused kernels implement; any other loss runs the torch path
+        self.loss_fn = None if dqn_lib.is_mse_sum(loss_fn) else loss_fn
         self.world = world_size(process_group)
         if model is None:
             torch.manual_seed(seed)
@@ -62,7 +65,7 @@ class DQNLearner:
         self.graph = graph
         # fused HIP kernels (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip) for the fp32
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
-        self.kind = qnet.kind_of(self.model)
+        self.kind = qnet.kind_of(self.model) if self.loss_fn is None else None
         self.fused = self.kind is not None
         self._upd = None
         if self.fused:
@@ -114,7 +117,7 @@ class DQNLearner:
             s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
                                                         self._layout, dtype=self.dtype, idx=idx)
             loss, _, _ = dqn_lib.dqn_loss(self.model, self.target, s, a, r, s2, d, self.gamma,
-                                          self.use_double_dqn)
+                                          self.use_double_dqn, self.loss_fn)
         loss.backward()
         self.last_loss.copy_(loss.detach())
 

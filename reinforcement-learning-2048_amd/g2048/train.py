@@ -31,14 +31,14 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
                   updates_per_step: int = 1, min_fill: int | None = None, seed: int = 0,
                   device="cuda:0", track_boards: int = 1, episode_log_slots: int = 8,
                   graph: bool = True, board_offset: int = 0, process_group=None,
-                  loop_graph: bool | None = None) -> Trainer:
+                  loop_graph: bool | None = None, loss_fn=None) -> Trainer:
     cap = max(n_boards, (replay_buffer_length // n_boards) * n_boards)  # multiple of n
     env = VecEnv2048(n_boards, seed=0x2048 + seed, device=device, board_offset=board_offset)
     replay = ReplayBuffer(cap, device=device)
     learner = DQNLearner(replay, net=net, dtype=dtype, batch_size=batch_size,
                          discount_factor=discount_factor, lr=learning_rate,
                          use_double_dqn=use_double_dqn, target_sync_every=target_sync_every,
-                         graph=graph, seed=seed, process_group=process_group)
+                         graph=graph, seed=seed, process_group=process_group, loss_fn=loss_fn)
     return Trainer(env, replay, learner, updates_per_step=updates_per_step, min_fill=min_fill,
                    eps_decay_episodes=no_episodes_to_reach_epsilon, min_epsilon=min_epsilon,
                    episode_log_slots=episode_log_slots, track_boards=track_boards,
@@ -51,7 +51,8 @@ def hyperparameters(trainer: Trainer, no_episodes: int, snapshot_game_every_n_ep
     lr = L._adam.lr if L.fused else L.opt.param_groups[0]["lr"]
     return {"batch_size": L.B, "discount_factor": L.gamma, "model": str(L.model),
             "replay_buffer_length": trainer.replay.capacity, "learning_rate": lr,
-            "loss_fn": "MSELoss()", "optimizer": "Adam (fused)" if L.fused else str(L.opt),
+            "loss_fn": "MSELoss()" if L.loss_fn is None else str(L.loss_fn),
+            "optimizer": "Adam (fused)" if L.fused else str(L.opt),
             "no_episodes": no_episodes, "no_episodes_to_reach_epsilon": trainer.eps_decay,
             "min_epsilon": trainer.min_eps, "use_double_dqn": L.use_double_dqn,
             "snapshot_game_every_n_episodes": snapshot_game_every_n_episodes,

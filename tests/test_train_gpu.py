@@ -36,6 +36,7 @@ def _fingerprint(tr):
     torch.cuda.synchronize()
     L = tr.learner
     return {"board": tr.env.board.cpu().clone(), "meta": tr.env.meta.cpu().clone(),
+            "clock": tr.env.clock.cpu().clone(),
             "ep": tr.env.ep.cpu().clone(), "replay_s": tr.replay.s.cpu().clone(),
             "count": tr.replay.count.cpu().clone(), "log": tr.log.raw.cpu().clone(),
             "params": [p.detach().cpu().clone() for p in L.model.parameters()],
@@ -61,7 +62,7 @@ def test_resume_is_bit_exact(G, net, tmp_path):
     for _ in range(9):
         b.step()
     got = _fingerprint(b)
-    for k in ("board", "meta", "ep", "replay_s", "count", "log", "loss"):
+    for k in ("board", "meta", "clock", "ep", "replay_s", "count", "log", "loss"):
         assert torch.equal(got[k], want[k]), k
     for x, y in zip(got["params"] + got["target"], want["params"] + want["target"]):
         assert torch.equal(x, y)
