@@ -359,6 +359,32 @@ G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
                                    float* exp_avg_sq_dev, double lr, double beta1, double beta2,
                                    double eps, uint64_t sync_every, void* stream);
 
+/* ---- float64 (the reference's precision, src/configs/double_dqn_dense.py:15) -------------
+ * One whole Double-DQN update of the dense 16-64-4 net in float64, fused: per 64-row tile the
+ * sampler (idx_in, or the Philox draw of g2048_replay_sample_encode with epoch *step_dev),
+ * Q_target(s'), Q_online(s') -> y = r + double((1 - d) * gamma) * Q_target(s', a*) (gamma the
+ * float32 torch uses), Q_online(s) -> MSELoss(sum) -> gradient slab; then a fixed-order slab
+ * reduction that writes grad_out / loss_out and -- with exp_avg / exp_avg_sq -- applies torch's
+ * Adam in float64 to the ONLINE parameters in place (+ the target sync when t % sync_every ==
+ * 0).  Same step_dev protocol as g2048_dense64_update.  Parameters are device float64 tensors in
+ * torch's layouts (Linear [out][in]).  workspace: f64[g2048_dense64_update_f64_workspace(B)]. */
+typedef struct {
+    double *w1, *b1; /* Linear(16, 64) */
+    double *w2, *b2; /* Linear(64, 4)  */
+} g2048_dense64_params_f64;
+
+G2048_API int64_t g2048_dense64_update_f64_workspace(int64_t batch);
+G2048_API int g2048_dense64_update_f64(const g2048_dense64_params_f64* online,
+                                       const g2048_dense64_params_f64* target, g2048_replay* rb,
+                                       const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                       uint64_t* step_dev, float gamma, int double_dqn,
+                                       int64_t* idx_out_dev, double* y_out_dev,
+                                       double* workspace_dev, double* grad_out_dev,
+                                       double* loss_out_dev, double* exp_avg_dev,
+                                       double* exp_avg_sq_dev, double lr, double beta1,
+                                       double beta2, double eps, uint64_t sync_every,
+                                       void* stream);
+
 /* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
  * Best-first search from one board (exponents start[16], merge score start_score) until a
  * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion

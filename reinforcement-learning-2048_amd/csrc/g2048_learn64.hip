@@ -1,0 +1,401 @@
+// g2048_learn64.hip -- the Double-DQN update of the dense 16 -> 64 -> 4 Q-net in float64, the
+// reference's precision (src/configs/double_dqn_dense.py:15 `.double()`; BASELINE configs[2] at
+// width 64), fused: sampler + Q_target(s') + Q_online(s') -> y + Q_online(s) -> MSE(sum) ->
+// gradient in ONE launch per 64-row tile, then a fixed-order slab reduction with torch's Adam
+// (float64) and the target sync applied in place.  train_step: src/dqn_lib.py:119-164; the
+// target sync: :227-228.
+//
+// Tile = 64 minibatch rows per 256-thread workgroup, VALU float64 (on MI355X the f64 vector FMA
+// rate equals the f64 MFMA rate, and at 1 280 MAC per row the update is latency-bound, not
+// FLOP-bound).  Every output element has one owner thread and every sum runs in a fixed order,
+// so the update is run-to-run bitwise reproducible:
+//   h[s][j] = relu(b1[j] + W1[j] . x[s])        thread (j = t & 63, rows 16 (t >> 6) ..)
+//   Q[s][a] = b2[a] + W2[a] . h[s]              thread (s = t >> 2, a = t & 3)
+//   dW2[a][j], db2[a]: thread (a = t >> 6, j = t & 63) over the tile's rows of action a
+//   dh[s][j] = (h > 0) dq_s W2[a_s][j]          in place over h
+//   dW1[j][4q .. 4q+3] += sum_s dh[s][j] x[s][.]  thread (j = t & 63, q = t >> 6); db1[j]
+// Gradient accumulators persist in registers across a workgroup's tiles and are written once,
+// in torch's parameter order, to the workgroup's slab (+ its loss).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/g2048.h"
+#include "g2048_board.hpp"
+#include "g2048_common.hpp"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int S = 64;        // rows per tile
+constexpr int XS = 17;       // doubles per x row in LDS (odd: the row-strided reads spread)
+constexpr int HS = 65;       // doubles per h row
+constexpr int P_W1 = 0, P_B1 = 1024, P_W2 = 1088, P_B2 = 1344, P_N = 1348;
+constexpr int SLAB = P_N + 4;  // + the loss at P_N (doubles; rows 32-byte aligned)
+constexpr int MAX_SLABS = 256;
+
+struct Net64 {
+    double *w1, *b1, *w2, *b2;
+};
+
+struct alignas(16) Smem {
+    double x[S * XS];    // s' then s of the tile, as exponent doubles
+    double h[S * HS];    // relu(layer 1) -> dh
+    double w2[2][4 * 64];
+    double b1[2][64];
+    double b2[2][4];
+    double qa[S * 4];    // Q_target(s')
+    double qb[S * 4];    // Q_online(s') then Q_online(s)
+    double y[S];
+    double dq[S];
+    double loss[S];
+    int act[S];
+};
+
+__device__ __forceinline__ int64_t sample_row(int64_t b, unsigned long long ep,
+                                              unsigned long long count, uint32_t lo, uint32_t hi) {
+    // the draw of k_sample / the fp32 learners (domain 3): uniform over [0, count)
+    const uint4 u = g2048::philox10(
+        make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
+                   (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
+        lo, hi);
+    return (int64_t)__umul64hi(((unsigned long long)u.y << 32) | u.x, count);
+}
+
+__device__ __forceinline__ void put_row(double* xr, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        xr[4 * k + 0] = (double)(w[k] & 0xFFu);
+        xr[4 * k + 1] = (double)((w[k] >> 8) & 0xFFu);
+        xr[4 * k + 2] = (double)((w[k] >> 16) & 0xFFu);
+        xr[4 * k + 3] = (double)(w[k] >> 24);
+    }
+}
+
+// Q = relu(x W1^T + b1) W2^T + b2 for the tile in LDS (x rows visible) -> q[S][4]; h left in
+// LDS.  w1r: this thread's row W1[j][0..15] (registers).  Ends with a sync.
+__device__ __forceinline__ void forward(Smem& M, const double (&w1r)[16], int net, double* q) {
+    const int t = threadIdx.x, j = t & 63, rq = t >> 6;
+    const double bj = M.b1[net][j];
+#pragma unroll 4
+    for (int rr = 0; rr < 16; ++rr) {
+        const int s = rq * 16 + rr;
+        const double* xr = M.x + s * XS;
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc = fma(w1r[k], xr[k], acc);
+        const double pre = acc + bj;
+        M.h[s * HS + j] = pre > 0.0 ? pre : 0.0;
+    }
+    __syncthreads();
+    const int s = t >> 2, a = t & 3;
+    const double* hr = M.h + s * HS;
+    const double* w2 = M.w2[net] + a * 64;
+    double acc = 0.0;
+#pragma unroll 8
+    for (int jj = 0; jj < 64; ++jj) acc = fma(w2[jj], hr[jj], acc);
+    q[s * 4 + a] = acc + M.b2[net][a];
+    __syncthreads();
+}
+
+struct UpdArgs64 {
+    Net64 on, tg;
+    const uint4 *s, *s2;
+    const uint8_t *a, *d;
+    const int32_t* r;
+    const unsigned long long* count;
+    const unsigned long long* step;
+    const int64_t* idx_in;
+    int64_t batch;
+    uint32_t seed_lo, seed_hi;
+    float gamma;
+    int double_dqn;
+    int64_t* idx_out;
+    double* y_out;
+    double* slab;
+    unsigned long long* step_next;
+};
+
+__global__ __launch_bounds__(NT) void k_dense64_update_f64(UpdArgs64 A) {
+    __shared__ Smem M;
+    const int t = threadIdx.x, j = t & 63, qd = t >> 6;
+    const unsigned long long ep = A.idx_in ? 0ull : *A.step;
+    const unsigned long long count = A.idx_in ? 0ull : *A.count;
+    if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
+    // stage: W2, b1, b2 of both nets in LDS; this thread's W1 rows in registers
+    const Net64 nets[2] = {A.tg, A.on};  // net 0 = target, net 1 = online
+    double w1t[16], w1o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        w1t[k] = A.tg.w1[j * 16 + k];
+        w1o[k] = A.on.w1[j * 16 + k];
+    }
+    for (int i = t; i < 2 * 256; i += NT) M.w2[i >> 8][i & 255] = nets[i >> 8].w2[i & 255];
+    if (t < 128) M.b1[t >> 6][t & 63] = nets[t >> 6].b1[t & 63];
+    if (t < 8) M.b2[t >> 2][t & 3] = nets[t >> 2].b2[t & 3];
+    double w2o[4];  // W2_online[a][j] for dh
+#pragma unroll
+    for (int a = 0; a < 4; ++a) w2o[a] = A.on.w2[a * 64 + j];
+    // gradient accumulators (fixed order across the workgroup's tiles)
+    double g_w1[4] = {0.0, 0.0, 0.0, 0.0}, g_b1 = 0.0, g_w2 = 0.0, g_b2 = 0.0, g_loss = 0.0;
+    const int64_t ntiles = (A.batch + S - 1) / S;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b = tile * S + t;
+        uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+        double rj = 0.0;
+        float disc = 0.f;
+        bool ok = false;
+        __syncthreads();  // the previous tile is done with M
+        if (t < S) {
+            uint4 s2v = make_uint4(0u, 0u, 0u, 0u);
+            int aj = 0;
+            ok = b < A.batch;
+            if (ok) {
+                const int64_t row =
+                    A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+                A.idx_out[b] = row;
+                s2v = A.s2[row];
+                sv = A.s[row];
+                aj = A.a[row];
+                rj = (double)A.r[row];
+                // (1 - dones) * discount_factor: float32 in torch (src/dqn_lib.py:131)
+                disc = (float)(1 - (int)A.d[row]) * A.gamma;
+            }
+            put_row(M.x + t * XS, s2v);
+            M.act[t] = aj;
+        }
+        __syncthreads();
+        forward(M, w1t, 0, M.qa);  // Q_target(s')
+        forward(M, w1o, 1, M.qb);  // Q_online(s')
+        if (t < S) {
+            const double* qo = M.qb + t * 4;
+            const double* qt = M.qa + t * 4;
+            double next;
+            if (A.double_dqn) {
+                const uint32_t as = g2048::argmax4_torch(qo[0], qo[1], qo[2], qo[3]);
+                next = qt[as];
+            } else {
+                next = g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);
+            }
+            double y;
+            {
+#pragma clang fp contract(off)
+                y = rj + (double)disc * next;
+            }
+            M.y[t] = y;
+            if (ok) A.y_out[b] = y;
+            put_row(M.x + t * XS, sv);
+        }
+        __syncthreads();
+        forward(M, w1o, 1, M.qb);  // Q_online(s), h = its hidden layer
+        if (t < S) {
+            double dq = 0.0, l = 0.0;
+            if (ok) {
+#pragma clang fp contract(off)
+                const double e = M.qb[t * 4 + M.act[t]] - M.y[t];
+                dq = 2.0 * e;  // d sum (q - y)^2 / dq
+                l = e * e;
+            }
+            M.dq[t] = dq;
+            M.loss[t] = l;
+        }
+        __syncthreads();
+        // layer 2: dW2[a][j], db2[a] (thread (a = qd, j))
+        {
+            double acc = 0.0, accb = 0.0;
+            for (int s = 0; s < S; ++s) {
+                if (M.act[s] == qd) {
+                    acc = fma(M.dq[s], M.h[s * HS + j], acc);
+                    accb += M.dq[s];
+                }
+            }
+            g_w2 += acc;
+            if (j == 0) g_b2 += accb;
+        }
+        if (t == 0) {
+            double l = 0.0;
+            for (int s = 0; s < S; ++s) l += M.loss[s];
+            g_loss += l;
+        }
+        __syncthreads();  // h is overwritten with dh below
+#pragma unroll 4
+        for (int rr = 0; rr < 16; ++rr) {
+            const int s = qd * 16 + rr;
+            double& hv = M.h[s * HS + j];
+            const double w = M.act[s] == 0 ? w2o[0] : M.act[s] == 1 ? w2o[1]
+                           : M.act[s] == 2 ? w2o[2] : w2o[3];
+            hv = hv > 0.0 ? M.dq[s] * w : 0.0;
+        }
+        __syncthreads();
+        // layer 1: dW1[j][4 qd + i], db1[j]
+        {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0}, accb = 0.0;
+            for (int s = 0; s < S; ++s) {
+                const double dh = M.h[s * HS + j];
+                const double* xr = M.x + s * XS + 4 * qd;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc[i] = fma(dh, xr[i], acc[i]);
+                accb += dh;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) g_w1[i] += acc[i];
+            if (qd == 0) g_b1 += accb;
+        }
+    }
+    // slab in torch order: 0.weight [64][16], 0.bias [64], 2.weight [4][64], 2.bias [4], loss
+    double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sl[P_W1 + j * 16 + 4 * qd + i] = g_w1[i];
+    if (qd == 0) sl[P_B1 + j] = g_b1;
+    sl[P_W2 + qd * 64 + j] = g_w2;
+    if (j == 0) sl[P_B2 + qd] = g_b2;
+    if (t == 0) sl[P_N] = g_loss;
+}
+
+// torch.optim.Adam (single tensor, amsgrad off, no weight decay) on one float64 element, the
+// scalars as torch forms them in double: m.lerp_(g, 1 - b1); v.mul_(b2).addcmul_(g, g, 1 - b2);
+// denom = v.sqrt() / sqrt(1 - b2^t) + eps; p.addcdiv_(m, denom, -lr / (1 - b1^t)).
+__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
+                                         double g, double& m, double& v, double p) {
+#pragma clang fp contract(off)
+    const double step_size = lr / (1.0 - pow(b1, t));
+    const double bc2_sqrt = sqrt(1.0 - pow(b2, t));
+    m = m + (1.0 - b1) * (g - m);
+    v = v * b2 + (1.0 - b2) * g * g;
+    const double denom = sqrt(v) / bc2_sqrt + eps;
+    return p + (-step_size) * (m / denom);
+}
+
+constexpr int RW = 16;  // waves per reduction block
+static_assert(MAX_SLABS <= RW * 16, "reduction covers at most RW*16 slabs");
+
+struct RedArgs64 {
+    const double* slab;
+    int nslab;
+    double* grad;
+    double* loss;
+    const unsigned long long* step_next;
+    unsigned long long* step;
+    double* p[4];
+    double* tp[4];
+    unsigned long long sync_every;
+    double* m;
+    double* v;
+    double lr, b1, b2, eps;
+    int adam;
+};
+
+// block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... in order, then wave 0
+// combines the 16 partials in order and (adam) applies the update to the parameter in place.
+__global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
+    __shared__ double part[RW][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pos = blockIdx.x * 64 + lane;
+    double r = 0.0;
+    for (int g = wave; g < A.nslab; g += RW)
+        if (pos <= P_N) r += A.slab[(int64_t)g * SLAB + pos];
+    part[wave][lane] = r;
+    __syncthreads();
+    if (wave == 0 && pos <= P_N) {
+        double sum = part[0][lane];
+        for (int k = 1; k < RW; ++k) sum += part[k][lane];
+        if (pos == P_N) {
+            if (A.loss) *A.loss = sum;
+        } else {
+            if (A.grad) A.grad[pos] = sum;
+            if (A.adam) {
+                const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
+                const int base[4] = {P_W1, P_B1, P_W2, P_B2};
+                const unsigned long long t = *A.step_next;
+                double m = A.m[pos], v = A.v[pos];
+                const double np = adam64((double)t, A.lr, A.b1, A.b2, A.eps, sum, m, v,
+                                         A.p[k][pos - base[k]]);
+                A.m[pos] = m;
+                A.v[pos] = v;
+                A.p[k][pos - base[k]] = np;
+                if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
+            }
+        }
+    }
+    if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
+}
+
+}  // namespace
+
+extern "C" G2048_API int64_t g2048_dense64_update_f64_workspace(int64_t batch) {
+    // slabs (<= 256 workgroups) + the next-step word, in doubles
+    const int64_t tiles = (batch + S - 1) / S;
+    const int64_t grid = tiles < MAX_SLABS ? tiles : MAX_SLABS;
+    return grid * SLAB + 2;
+}
+
+extern "C" G2048_API int g2048_dense64_update_f64(
+    const g2048_dense64_params_f64* online, const g2048_dense64_params_f64* target,
+    g2048_replay* rb, const int64_t* idx_in, int64_t batch, uint64_t seed, uint64_t* step_dev,
+    float gamma, int double_dqn, int64_t* idx_out, double* y_out, double* workspace,
+    double* grad_out, double* loss_out, double* exp_avg, double* exp_avg_sq, double lr,
+    double beta1, double beta2, double eps, uint64_t sync_every, void* stream) {
+    if (!online || !target || !rb || batch <= 0 || !step_dev || !idx_out || !y_out || !workspace)
+        return g2048_fail(G2048_EINVAL, "dense64_update_f64: NULL argument or batch <= 0");
+    if (!online->w1 || !online->b1 || !online->w2 || !online->b2 || !target->w1 || !target->b1 ||
+        !target->w2 || !target->b2)
+        return g2048_fail(G2048_EINVAL, "dense64_update_f64: NULL parameter pointer");
+    const bool adam = exp_avg && exp_avg_sq;
+    if (!adam && !grad_out)
+        return g2048_fail(G2048_EINVAL,
+                          "dense64_update_f64: need exp_avg and exp_avg_sq (Adam) or grad_out");
+    uint8_t *s = nullptr, *s2 = nullptr, *a = nullptr, *d = nullptr;
+    int32_t* r = nullptr;
+    uint64_t* count = nullptr;
+    if (g2048_replay_views(rb, &s, &s2, &a, &r, &d, &count) != G2048_OK) return G2048_EINVAL;
+    const int64_t tiles = (batch + S - 1) / S;
+    const int grid = (int)(tiles < MAX_SLABS ? tiles : MAX_SLABS);
+    UpdArgs64 U;
+    U.on = Net64{online->w1, online->b1, online->w2, online->b2};
+    U.tg = Net64{target->w1, target->b1, target->w2, target->b2};
+    U.s = reinterpret_cast<const uint4*>(s);
+    U.s2 = reinterpret_cast<const uint4*>(s2);
+    U.a = a;
+    U.d = d;
+    U.r = r;
+    U.count = reinterpret_cast<const unsigned long long*>(count);
+    U.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    U.idx_in = idx_in;
+    U.batch = batch;
+    U.seed_lo = (uint32_t)seed;
+    U.seed_hi = (uint32_t)(seed >> 32);
+    U.gamma = gamma;
+    U.double_dqn = double_dqn;
+    U.idx_out = idx_out;
+    U.y_out = y_out;
+    U.slab = workspace;
+    U.step_next = reinterpret_cast<unsigned long long*>(workspace + (int64_t)grid * SLAB);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipLaunchKernelGGL(k_dense64_update_f64, dim3(grid), dim3(NT), 0, st, U);
+    RedArgs64 R;
+    R.slab = workspace;
+    R.nslab = grid;
+    R.grad = grad_out;
+    R.loss = loss_out;
+    R.step_next = U.step_next;
+    R.step = reinterpret_cast<unsigned long long*>(step_dev);
+    double* ps[4] = {online->w1, online->b1, online->w2, online->b2};
+    double* ts[4] = {target->w1, target->b1, target->w2, target->b2};
+    for (int k = 0; k < 4; ++k) {
+        R.p[k] = ps[k];
+        R.tp[k] = ts[k];
+    }
+    R.sync_every = adam ? sync_every : 0ull;
+    R.m = exp_avg;
+    R.v = exp_avg_sq;
+    R.lr = lr;
+    R.b1 = beta1;
+    R.b2 = beta2;
+    R.eps = eps;
+    R.adam = adam ? 1 : 0;
+    hipLaunchKernelGGL(k_dense64_reduce_f64, dim3((P_N + 1 + 63) / 64), dim3(64 * RW), 0, st, R);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "dense64_update_f64: %s", hipGetErrorString(e));
+}

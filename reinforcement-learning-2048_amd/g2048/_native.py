@@ -69,6 +69,10 @@ SIGNATURES = {
     "g2048_dense64_update_workspace": (_i64, [_i64]),
     "g2048_dense64_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
+    "g2048_dense64_update_f64_workspace": (_i64, [_i64]),
+    "g2048_dense64_update_f64": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
+                                        _u64, _vp]),
     "g2048_convnet_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
     "g2048_astar_search": (_int, [_vp, _i64, _int, _u64, _u64, _int, _i64, _i64, _vp, _vp, _vp,
@@ -88,7 +92,8 @@ class ConvNetParams(C.Structure):
 
 
 class Dense64Params(C.Structure):
-    """g2048_dense64_params: device pointers of the dense 16-64-4 Q-net's 4 fp32 tensors."""
+    """g2048_dense64_params / g2048_dense64_params_f64: device pointers of the dense 16-64-4
+    Q-net's 4 tensors (fp32 / fp64)."""
     _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2")]
 
 

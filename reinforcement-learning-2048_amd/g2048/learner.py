@@ -66,19 +66,26 @@ class DQNLearner:
         # fused HIP kernels (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip) for the fp32
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
         self.kind = qnet.kind_of(self.model) if self.loss_fn is None else None
+        # float64 (the reference's precision): the dense 16-64-4 net has a fused update too
+        # (g2048_dense64_update_f64); single process -- with world > 1 it runs the torch path
+        self.f64 = (self.kind is None and self.loss_fn is None and self.world == 1
+                    and qnet.kind64_of(self.model) == "dense64")
+        if self.f64:
+            self.kind = "dense64"
         self.fused = self.kind is not None
         self._upd = None
         if self.fused:
-            self._p_on = qnet.net_params(self.model)
-            self._p_tgt = qnet.net_params(self.target)
+            self._p_on = None if self.f64 else qnet.net_params(self.model)
+            self._p_tgt = None if self.f64 else qnet.net_params(self.target)
             # targets (sampler, both target-side forwards, Bellman), the graded half (forward +
             # MSE + backward) and a fixed-order slab reduction that writes the flat gradient
             # bucket or applies Adam (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip).  The
             # device update counter is the sampler epoch and Adam's t (bumped by the train launch).
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
-            self._y = torch.zeros(self.B, dtype=torch.float32, device=self.device)
-            self._adam = FusedAdam(params, lr=lr)
+            self._y = torch.zeros(self.B, dtype=torch.float64 if self.f64 else torch.float32,
+                                  device=self.device)
+            self._adam = qnet.Adam64(params, lr=lr) if self.f64 else FusedAdam(params, lr=lr)
             # the target sync (every target_sync_every updates) is done by the Adam launch on
             # the device update counter: no host decision between graph replays
             if self.target_sync_every:
@@ -87,7 +94,8 @@ class DQNLearner:
             # gradient reduction.  conv: targets (two half-grids, one net each), train forward,
             # train backward, reduce+Adam = 4 launches; dense64: sampler + targets + gradient in
             # ONE launch + reduce+Adam = 2 launches
-            upd = qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate
+            upd = (qnet.Dense64Update64 if self.f64 else
+                   qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate)
             self._upd = upd(self.model, self.target, self.B,
                             adam=self._adam if self.world == 1 else None)
             rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
@@ -208,7 +216,7 @@ class DQNLearner:
 
     @torch.no_grad()
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
-        if self.fused:
+        if self.fused and not self.f64:
             return qnet.forward(self.model, env.board, params=self._p_on)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
@@ -330,7 +338,7 @@ class Trainer:
     def _rollout_step(self) -> None:
         """Device work of play_one_step for all boards (stream-ordered, capturable)."""
         sched = (self.eps_decay, self.min_eps)
-        if self.learner.kind == "dense64":  # Q computed inside the step kernel (one launch)
+        if self.learner.kind == "dense64" and not self.learner.f64:  # Q inside the step kernel
             self.env.step_egreedy_dense64(self.learner._p_on, replay=self.replay,
                                           reward=self._reward, done=self._done,
                                           action=self._action, eps_schedule=sched)

@@ -43,12 +43,19 @@ def kind_of(model) -> str | None:
     return None
 
 
-def _tensors(model, order):
+def kind64_of(model) -> str | None:
+    """'dense64' when the fused float64 update exists for this model, else None."""
+    if next(model.parameters()).dtype != torch.float64:
+        return None
+    return "dense64" if is_dense64(model) else None
+
+
+def _tensors(model, order, dtype=torch.float32):
     sd = dict(model.named_parameters())
     ts = [sd[k] for k in order]
     for t in ts:
-        if t.dtype != torch.float32 or not t.is_cuda or not t.is_contiguous():
-            raise ValueError("fused Q-net kernels run fp32 contiguous CUDA parameters")
+        if t.dtype != dtype or not t.is_cuda or not t.is_contiguous():
+            raise ValueError(f"fused Q-net kernels run {dtype} contiguous CUDA parameters")
     return ts
 
 
@@ -201,6 +208,67 @@ class ConvUpdate:
             N.ptr(v), float(lr), float(b1), float(b2), float(eps),
             int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
             "g2048_convnet_update")
+
+
+class Adam64:
+    """Adam state of the fused float64 update (torch Adam semantics, applied inside the
+    gradient reduction): flat exp_avg / exp_avg_sq in the parameters' order; attach_target as
+    FusedAdam's."""
+
+    def __init__(self, params, lr: float = 1e-2, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.params = list(params)
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device
+        self.exp_avg = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.exp_avg_sq = torch.zeros(n, dtype=torch.float64, device=dev)
+        self.sync_every = 0
+
+    def attach_target(self, target_params, sync_every: int) -> None:
+        self._target = list(target_params)
+        self.sync_every = int(sync_every)
+
+    def reset_state(self):
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+
+
+class Dense64Update64:
+    """One whole Double-DQN update of a float64 dense 16-64-4 net (the reference's precision)
+    in two launches (g2048_dense64_update_f64): the same call and step_dev protocol as
+    Dense64Update, float64 throughout, Adam (Adam64) applied in the reduction."""
+
+    def __init__(self, model, target, batch: int, adam: Adam64 | None = None):
+        if kind64_of(model) != "dense64" or kind64_of(target) != "dense64":
+            raise TypeError("Dense64Update64 needs fp64 dense 16-64-4 online and target nets")
+        self.on = N.Dense64Params(*[t.data_ptr() for t in
+                                    _tensors(model, _DENSE_ORDER, torch.float64)])
+        self.tg = N.Dense64Params(*[t.data_ptr() for t in
+                                    _tensors(target, _DENSE_ORDER, torch.float64)])
+        self.batch = int(batch)
+        self.adam = adam
+        dev = next(model.parameters()).device
+        n = N.load().g2048_dense64_update_f64_workspace(self.batch)
+        self.workspace = torch.empty(n, dtype=torch.float64, device=dev)
+
+    def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
+                 idx_in=None, grad_out=None, loss_out=None):
+        if idx_out.numel() != self.batch or y_out.numel() != self.batch:
+            raise ValueError("idx_out / y_out must have `batch` elements")
+        if y_out.dtype != torch.float64:
+            raise TypeError("y_out must be float64")
+        if self.adam is None and grad_out is None:
+            raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        a = self.adam
+        m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
+        lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)
+        N.check(N.load().g2048_dense64_update_f64(
+            C.byref(self.on), C.byref(self.tg), replay.handle, N.ptr(idx_in), self.batch,
+            int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)), N.ptr(idx_out),
+            N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(m),
+            N.ptr(v), float(lr), float(b1), float(b2), float(eps),
+            int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
+            "g2048_dense64_update_f64")
 
 
 class Dense64Update:
