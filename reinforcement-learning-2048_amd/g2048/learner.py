@@ -351,6 +351,18 @@ class Trainer:
             self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward,
                                   done=self._done, action=self._action, eps_schedule=sched)
 
+    def _warm_forward(self) -> None:
+        """A rollout step whose Q comes from torch (the float64 learners) runs that forward once
+        outside the capture: hipBLASLt sets up a GEMM shape on its first call, which a stream
+        under capture does not permit.  Pure: nothing is stepped."""
+        L = self.learner
+        if L.f64:
+            side = torch.cuda.Stream(self.env.device)
+            side.wait_stream(torch.cuda.current_stream(self.env.device))
+            with torch.cuda.stream(side):
+                L.q_values(self.env)
+            torch.cuda.current_stream(self.env.device).wait_stream(side)
+
     def _graphed_iteration(self) -> None:
         """One iteration (step + updates_per_step updates, target syncs included: the fused
         Adam performs them on the device update counter) as ONE hipGraph replay.  Capture
@@ -361,6 +373,7 @@ class Trainer:
         if L.world > 1:
             return self._graphed_iteration_dp()
         if self._loop_graph is None:
+            self._warm_forward()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._rollout_step()
@@ -377,6 +390,7 @@ class Trainer:
         updates of the iteration run the learner's own two-graph update."""
         L = self.learner
         if self._loop_graph is None:
+            self._warm_forward()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self._rollout_step()
