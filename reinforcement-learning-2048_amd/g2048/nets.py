@@ -57,9 +57,9 @@ class _LinearSplitK(torch.autograd.Function):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:
-    """F.linear over the last dim; float64 (the reference's precision, run through torch) takes
-    the split-K weight gradient, float32 keeps F.linear (the fused HIP kernels own that path)."""
-    if x.dtype != torch.float64 or not torch.is_grad_enabled() or not w.requires_grad:
+    """F.linear over the last dim, with the split-K weight gradient whenever autograd will need
+    dW (the torch learner paths: float64, and float32 nets without a fused kernel)."""
+    if not torch.is_grad_enabled() or not w.requires_grad:
         return F.linear(x, w, b)
     shp = x.shape
     y = _LinearSplitK.apply(x.reshape(-1, shp[-1]), w, b)
@@ -67,8 +67,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Te
 
 
 class Linear(nn.Linear):
-    """nn.Linear (same parameters / state_dict) whose float64 backward uses the split-K weight
-    gradient of `linear`."""
+    """nn.Linear (same parameters / state_dict) whose backward uses the split-K weight gradient
+    of `linear`."""
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return linear(x, self.weight, self.bias)
