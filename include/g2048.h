@@ -385,6 +385,32 @@ G2048_API int g2048_dense64_update_f64(const g2048_dense64_params_f64* online,
                                        double beta2, double eps, uint64_t sync_every,
                                        void* stream);
 
+/* One whole Double-DQN update of the reference conv net (src/configs/double_dqn_conv.py:19-28)
+ * in float64, the reference's precision (`.double()`, :28): the arguments, step_dev protocol,
+ * sampler, Bellman target (gamma the float32 torch uses), MSELoss(sum), gradient order and
+ * Adam / target-sync semantics of g2048_dense64_update_f64, for Conv2d(1,64,2) -> ReLU ->
+ * Conv2d(64,64,2) -> ReLU -> Flatten -> Linear(256,64) -> ReLU -> Linear(64,4).  Five launches:
+ * operand packing, targets, two train launches, reduction + Adam.  grad_out: f64[33476] in
+ * torch parameter order.  workspace: f64[g2048_convnet_update_f64_workspace(B)]. */
+typedef struct {
+    double *w1, *b1;       /* Conv2d(1, 64, 2)  */
+    double *w2, *b2;       /* Conv2d(64, 64, 2) */
+    double *fc1_w, *fc1_b; /* Linear(256, 64)   */
+    double *fc2_w, *fc2_b; /* Linear(64, 4)     */
+} g2048_convnet_params_f64;
+
+G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch);
+G2048_API int g2048_convnet_update_f64(const g2048_convnet_params_f64* online,
+                                       const g2048_convnet_params_f64* target, g2048_replay* rb,
+                                       const int64_t* idx_in_dev, int64_t batch, uint64_t seed,
+                                       uint64_t* step_dev, float gamma, int double_dqn,
+                                       int64_t* idx_out_dev, double* y_out_dev,
+                                       double* workspace_dev, double* grad_out_dev,
+                                       double* loss_out_dev, double* exp_avg_dev,
+                                       double* exp_avg_sq_dev, double lr, double beta1,
+                                       double beta2, double eps, uint64_t sync_every,
+                                       void* stream);
+
 /* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
  * Best-first search from one board (exponents start[16], merge score start_score) until a
  * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion

@@ -1,0 +1,766 @@
+// g2048_conv64.hip -- the Double-DQN update of the reference conv Q-net in float64, the
+// reference's precision (src/configs/double_dqn_conv.py:19-28 `.double()`; BASELINE configs[3]):
+// train_step (src/dqn_lib.py:119-164) + the target sync (:227-228) as five launches:
+//   1. pack      the big weight matrices of both nets into f64-MFMA operand order (B fragments);
+//   2. targets   per 16-row tile: sampler, Q_online(s') and Q_target(s') -> y (Double or vanilla)
+//   3. train A   per tile: Q_online(s) -> MSE(sum) -> fc2 / fc1 gradients, dH2 -> dZ2 (workspace)
+//   4. train B   per tile: conv1 recomputed, conv2 / conv1 gradients from dZ2
+//   5. reduce    fixed-order sum of the per-workgroup gradient slabs + torch's Adam in float64
+//                (+ the target sync on the device update counter)
+// The GEMM-shaped layers (conv2 as im2col [rows = 16 boards x 4 positions] x [256 = tap x c] x
+// [64 o], fc1, and their backward products) run on v_mfma_f64_16x16x4_f64; conv1, fc2 and the
+// element-wise work on VALU.  Every sum has a fixed order, so an update is run-to-run bitwise
+// reproducible.  Layer order and shapes follow nets.Conv2048 / the reference nn.Sequential.
+//
+// f64 MFMA 16x16x4 fragments (gfx950, measured by tools/scratch/mfma64_probe.hip):
+//   A (16 x 4): lane l holds A[i = l % 16][k = l / 16]
+//   B (4 x 16): lane l holds B[k = l / 16][j = l % 16]
+//   D (16 x16): lane l, register r holds D[i = 4 r + l / 16][j = l % 16]
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/g2048.h"
+#include "g2048_board.hpp"
+#include "g2048_common.hpp"
+
+namespace {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int NT = 256;     // 4 waves
+constexpr int TB = 16;      // boards per tile
+constexpr int XS = 17;      // doubles per input row in LDS
+constexpr int DSB = 66;     // doubles per board row of a conv1 position plane (64 c + pad)
+constexpr int DPL = TB * DSB;  // doubles per position plane
+constexpr int HS = 258;     // doubles per board row of H2 / dZ2 (256 + pad)
+constexpr int H3S = 66;     // doubles per board row of H3 / dZ3
+constexpr int MAX_WG = 256;
+
+// flat parameter order (torch: model.parameters() of Conv2048 / the reference Sequential)
+constexpr int P_W1 = 0, P_B1 = 256, P_W2 = 320, P_B2 = 16704, P_F1 = 16768, P_FB1 = 33152,
+              P_F2 = 33216, P_FB2 = 33472, P_N = 33476;
+constexpr int SLAB = P_N + 4;  // + the loss at P_N
+constexpr int PACK = 16384;    // doubles per packed matrix
+
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+struct Net {
+    const double *w1, *b1, *w2, *b2, *f1, *fb1, *f2, *fb2;
+};
+
+// packed operands of one net: conv2 forward B (P2f), fc1 forward B (Pf1)
+struct Packed {
+    const double *p2f, *pf1;
+};
+
+struct alignas(16) Smem {
+    double x[TB * XS];      // input exponents of the tile (s' or s)
+    double d[9 * DPL];      // conv1 output (relu), [pos][board][c]
+    double h2[TB * HS];     // conv2 output (relu), flatten order o*4 + p; train B: dZ2
+    double h3[TB * H3S];    // fc1 output (relu); train A: dZ3
+    double w1[256], b1[64], b2[64], fb1[64], f2[256], fb2[4];  // the small parameters of a net
+    double q[TB * 4];
+    double q2[TB * 4];
+    double y[TB];
+    double r[TB];
+    double dq[TB];
+    double loss[TB];
+    float disc[TB];
+    int act[TB];
+};
+
+__device__ __forceinline__ void put_row(double* xr, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        xr[4 * k + 0] = (double)(w[k] & 0xFFu);
+        xr[4 * k + 1] = (double)((w[k] >> 8) & 0xFFu);
+        xr[4 * k + 2] = (double)((w[k] >> 16) & 0xFFu);
+        xr[4 * k + 3] = (double)(w[k] >> 24);
+    }
+}
+
+__device__ __forceinline__ void stage_small(Smem& M, const Net& n) {
+    const int t = threadIdx.x;
+    M.w1[t] = n.w1[t];
+    M.f2[t] = n.f2[t];
+    if (t < 64) {
+        M.b1[t] = n.b1[t];
+        M.b2[t] = n.b2[t];
+        M.fb1[t] = n.fb1[t];
+    }
+    if (t < 4) M.fb2[t] = n.fb2[t];
+}
+
+// conv1 + relu for the tile in M.x -> M.d[pos][b][c].  Thread (c = t & 63, boards 4g .. 4g+3).
+__device__ __forceinline__ void conv1(Smem& M) {
+    const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    const double w0 = M.w1[c * 4 + 0], w1 = M.w1[c * 4 + 1], w2 = M.w1[c * 4 + 2],
+                 w3 = M.w1[c * 4 + 3], bc = M.b1[c];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+        const int b = 4 * g + bb;
+        const double* xr = M.x + b * XS;
+#pragma unroll
+        for (int qy = 0; qy < 3; ++qy)
+#pragma unroll
+            for (int qx = 0; qx < 3; ++qx) {
+                const int i0 = qy * 4 + qx;
+                double a = bc;
+                a = fma(w0, xr[i0], a);
+                a = fma(w1, xr[i0 + 1], a);
+                a = fma(w2, xr[i0 + 4], a);
+                a = fma(w3, xr[i0 + 5], a);
+                M.d[(qy * 3 + qx) * DPL + b * DSB + c] = a > 0.0 ? a : 0.0;
+            }
+    }
+}
+
+// conv1 input position of output position p (0..3, 2x2) shifted by tap (0..3, 2x2): 3x3 index
+__device__ __forceinline__ int pos_of(int p, int tap) {
+    return ((p >> 1) + (tap >> 1)) * 3 + (p & 1) + (tap & 1);
+}
+
+// The forward of the tile in M.x through one net (small weights staged in M, big ones packed):
+// M.d, M.h2, M.h3 filled; Q -> q[TB][4].  Starts and ends with a barrier.
+__device__ void forward(Smem& M, const Packed& pk, double* q) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int lr = l & 15, lk = l >> 4;
+    __syncthreads();  // x and the small weights visible
+    conv1(M);
+    __syncthreads();
+    // conv2: wave w -> output channels 16w .. 16w+15; 4 row blocks = the 4 output positions
+    {
+        d4 acc[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) acc[p] = d4{0.0, 0.0, 0.0, 0.0};
+        const double* bp = pk.p2f + (size_t)w * 64 * 64 + l;
+        double bcur[8], bnxt[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bcur[u] = bp[u * 64];
+        for (int s0 = 0; s0 < 64; s0 += 8) {
+            if (s0 + 8 < 64) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) bnxt[u] = bp[(s0 + 8 + u) * 64];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int s = s0 + u, tap = s >> 4, c = 4 * (s & 15) + lk;
+#pragma unroll
+                for (int p = 0; p < 4; ++p)
+                    acc[p] = mfma(M.d[pos_of(p, tap) * DPL + lr * DSB + c], bcur[u], acc[p]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bcur[u] = bnxt[u];
+        }
+        const int o = 16 * w + lr;
+        const double bo = M.b2[o];
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double z = acc[p][r] + bo;
+                M.h2[(4 * r + lk) * HS + o * 4 + p] = z > 0.0 ? z : 0.0;
+            }
+    }
+    __syncthreads();
+    // fc1: wave w -> units 16w .. 16w+15, K = 256 in 4 interleaved chains
+    {
+        d4 acc[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+        const double* bp = pk.pf1 + (size_t)w * 64 * 64 + l;
+        double bcur[8], bnxt[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) bcur[u] = bp[u * 64];
+        for (int s0 = 0; s0 < 64; s0 += 8) {
+            if (s0 + 8 < 64) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) bnxt[u] = bp[(s0 + 8 + u) * 64];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int s = s0 + u;
+                acc[u & 3] = mfma(M.h2[lr * HS + 4 * s + lk], bcur[u], acc[u & 3]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) bcur[u] = bnxt[u];
+        }
+        const int j = 16 * w + lr;
+        const double bj = M.fb1[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const double z = ((acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r])) + bj;
+            M.h3[(4 * r + lk) * H3S + j] = z > 0.0 ? z : 0.0;
+        }
+    }
+    __syncthreads();
+    // fc2 (VALU): thread (b = t >> 2, a = t & 3) for t < 64, two chains
+    if (t < 64) {
+        const int b = t >> 2, a = t & 3;
+        const double* hr = M.h3 + b * H3S;
+        const double* wr = M.f2 + a * 64;
+        double e = 0.0, o = 0.0;
+#pragma unroll 8
+        for (int j = 0; j < 64; j += 2) {
+            e = fma(wr[j], hr[j], e);
+            o = fma(wr[j + 1], hr[j + 1], o);
+        }
+        q[b * 4 + a] = (e + o) + M.fb2[a];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ int64_t sample_row(int64_t b, unsigned long long ep,
+                                              unsigned long long count, uint32_t lo, uint32_t hi) {
+    // the draw of k_sample / the other fused learners (domain 3): uniform over [0, count)
+    const uint4 u = g2048::philox10(
+        make_uint4((uint32_t)b, (uint32_t)((uint64_t)b >> 32), (uint32_t)ep,
+                   (uint32_t)(ep >> 32) | (g2048::DOMAIN_SAMPLE << 30)),
+        lo, hi);
+    return (int64_t)__umul64hi(((unsigned long long)u.y << 32) | u.x, count);
+}
+
+struct Ring {
+    const uint4 *s, *s2;
+    const uint8_t *a, *d;
+    const int32_t* r;
+    const unsigned long long* count;
+};
+
+// ------------------------------------------------------------------ 1. pack
+struct PackArgs {
+    const double *w2_on, *f1_on, *w2_tg, *f1_tg;
+    double* out;  // [6][PACK]: p2f_on, pf1_on, p2f_tg, pf1_tg, pf1b_on, p2b_on
+};
+
+__global__ __launch_bounds__(NT) void k_pack(PackArgs A) {
+    const int e = blockIdx.x * NT + threadIdx.x;  // 0 .. 6 * PACK
+    const int m = e / PACK, i = e % PACK;
+    const int l = i & 63, lr = l & 15, lk = l >> 4;
+    double v;
+    if (m == 0 || m == 2) {  // conv2 forward: [w][s][l] = W2[16w + lr][4 (s & 15) + lk][s >> 4]
+        const int s = (i >> 6) & 63, w = i >> 12;
+        const double* w2 = m == 0 ? A.w2_on : A.w2_tg;
+        v = w2[(16 * w + lr) * 256 + (4 * (s & 15) + lk) * 4 + (s >> 4)];
+    } else if (m == 1 || m == 3) {  // fc1 forward: [w][s][l] = Wf1[16w + lr][4s + lk]
+        const int s = (i >> 6) & 63, w = i >> 12;
+        const double* f1 = m == 1 ? A.f1_on : A.f1_tg;
+        v = f1[(16 * w + lr) * 256 + 4 * s + lk];
+    } else if (m == 4) {  // fc1 backward: [w][cb][s][l] = Wf1[4s + lk][64w + 16cb + lr]
+        const int s = (i >> 6) & 15, cb = (i >> 10) & 3, w = i >> 12;
+        v = A.f1_on[(4 * s + lk) * 256 + 64 * w + 16 * cb + lr];
+    } else {  // conv2 backward: [w][tap][s][l] = W2[4s + lk][16w + lr][tap]
+        const int s = (i >> 6) & 15, tap = (i >> 10) & 3, w = i >> 12;
+        v = A.w2_on[(4 * s + lk) * 256 + (16 * w + lr) * 4 + tap];
+    }
+    A.out[e] = v;
+}
+
+// ------------------------------------------------------------------ 2. targets
+struct TgtArgs {
+    Net on, tg;
+    Packed pon, ptg;
+    Ring R;
+    const unsigned long long* step;
+    const int64_t* idx_in;
+    int64_t batch;
+    uint32_t seed_lo, seed_hi;
+    float gamma;
+    int double_dqn;
+    int64_t* idx_out;
+    double* y_out;
+    unsigned long long* step_next;
+};
+
+__global__ __launch_bounds__(NT) void k_conv64_targets(TgtArgs A) {
+    __shared__ Smem M;
+    const int t = threadIdx.x;
+    const unsigned long long ep = A.idx_in ? 0ull : *A.step;
+    const unsigned long long count = A.idx_in ? 0ull : *A.R.count;
+    if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
+    const int64_t ntiles = (A.batch + TB - 1) / TB;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b = tile * TB + t;
+        __syncthreads();  // the previous tile is done with M
+        if (t < TB) {
+            uint4 s2v = make_uint4(0u, 0u, 0u, 0u);
+            double rj = 0.0;
+            float disc = 0.f;
+            if (b < A.batch) {
+                const int64_t row =
+                    A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+                A.idx_out[b] = row;
+                s2v = A.R.s2[row];
+                rj = (double)A.R.r[row];
+                // (1 - dones) * discount_factor: float32 in torch (src/dqn_lib.py:131)
+                disc = (float)(1 - (int)A.R.d[row]) * A.gamma;
+            }
+            put_row(M.x + t * XS, s2v);
+            M.r[t] = rj;
+            M.disc[t] = disc;
+        }
+        if (A.double_dqn) {
+            stage_small(M, A.on);
+            forward(M, A.pon, M.q2);  // Q_online(s')
+        }
+        stage_small(M, A.tg);  // (forward ended with a barrier: the online weights are dead)
+        forward(M, A.ptg, M.q);  // Q_target(s')
+        if (t < TB && b < A.batch) {
+            const double* qt = M.q + t * 4;
+            double next;
+            if (A.double_dqn) {
+                const double* qo = M.q2 + t * 4;
+                next = qt[g2048::argmax4_torch(qo[0], qo[1], qo[2], qo[3])];
+            } else {
+                next = g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);
+            }
+            {
+#pragma clang fp contract(off)
+                A.y_out[b] = M.r[t] + (double)M.disc[t] * next;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ 3. train A
+struct TrainArgs {
+    Net on;
+    Packed pon;
+    const double* pf1b;  // fc1 backward operands
+    const double* p2b;   // conv2 backward operands
+    Ring R;
+    const int64_t* idx;
+    const double* y;
+    int64_t batch;
+    double* dz2;   // [ntiles * TB][256]
+    double* slab;  // [grid][SLAB]
+};
+
+__global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
+    __shared__ Smem M;
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int lr = l & 15, lk = l >> 4;
+    d4 gf1[16];  // dWf1 of wave w: rows j = 16w + 4r + lk, columns 16 cb + lr
+#pragma unroll
+    for (int c = 0; c < 16; ++c) gf1[c] = d4{0.0, 0.0, 0.0, 0.0};
+    double gf2 = 0.0, gfb2 = 0.0, gfb1 = 0.0, gloss = 0.0;
+    stage_small(M, A.on);
+    const int64_t ntiles = (A.batch + TB - 1) / TB;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b0 = tile * TB;
+        __syncthreads();
+        if (t < TB) {
+            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+            int aj = 0;
+            double yj = 0.0;
+            if (b0 + t < A.batch) {
+                const int64_t row = A.idx[b0 + t];
+                sv = A.R.s[row];
+                aj = A.R.a[row];
+                yj = A.y[b0 + t];
+            }
+            put_row(M.x + t * XS, sv);
+            M.act[t] = aj;
+            M.y[t] = yj;
+        }
+        forward(M, A.pon, M.q);  // Q_online(s); h2, h3 kept
+        if (t < TB) {
+            double dq = 0.0, ls = 0.0;
+            if (b0 + t < A.batch) {
+#pragma clang fp contract(off)
+                const double e = M.q[t * 4 + M.act[t]] - M.y[t];
+                dq = 2.0 * e;  // d sum (q - y)^2 / dq
+                ls = e * e;
+            }
+            M.dq[t] = dq;
+            M.loss[t] = ls;
+        }
+        __syncthreads();
+        // fc2: dWf2[a][j], dbf2[a] (thread a = w, j = l) over the tile's rows of action a
+        {
+            double acc = 0.0, accb = 0.0;
+            for (int s = 0; s < TB; ++s) {
+                if (M.act[s] == w) {
+                    acc = fma(M.dq[s], M.h3[s * H3S + l], acc);
+                    accb += M.dq[s];
+                }
+            }
+            gf2 += acc;
+            if (l == 0) gfb2 += accb;
+        }
+        if (t == 0) {
+            double ls = 0.0;
+            for (int s = 0; s < TB; ++s) ls += M.loss[s];
+            gloss += ls;
+        }
+        __syncthreads();  // h3 is overwritten with dZ3
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb) {
+            const int s = 4 * w + bb;
+            double& hv = M.h3[s * H3S + l];
+            hv = hv > 0.0 ? M.dq[s] * M.f2[M.act[s] * 64 + l] : 0.0;
+        }
+        __syncthreads();
+        if (t < 64) {
+            double acc = 0.0;
+            for (int s = 0; s < TB; ++s) acc += M.h3[s * H3S + t];
+            gfb1 += acc;
+        }
+        // dWf1 += dZ3^T H2: wave w -> rows j = 16w .., 16 column blocks, K = 16 boards
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const double a = M.h3[(4 * s + lk) * H3S + 16 * w + lr];
+#pragma unroll
+            for (int cb = 0; cb < 16; ++cb)
+                gf1[cb] = mfma(a, M.h2[(4 * s + lk) * HS + 16 * cb + lr], gf1[cb]);
+        }
+        // dH2 = dZ3 Wf1 (masked by relu'(H2)) -> dZ2: wave w -> columns 64w .. 64w+63
+        {
+            d4 acc[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
+            const double* bp = A.pf1b + (size_t)w * 4 * 16 * 64 + l;
+#pragma unroll 4
+            for (int s = 0; s < 16; ++s) {
+                const double a = M.h3[lr * H3S + 4 * s + lk];
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(a, bp[(cb * 16 + s) * 64], acc[cb]);
+            }
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int bq = 4 * r + lk, k = 64 * w + 16 * cb + lr;
+                    A.dz2[(b0 + bq) * 256 + k] = M.h2[bq * HS + k] > 0.0 ? acc[cb][r] : 0.0;
+                }
+        }
+    }
+    // slab: fc1.weight [64][256], fc1.bias, fc2.weight [4][64], fc2.bias, loss
+    double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#pragma unroll
+    for (int cb = 0; cb < 16; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sl[P_F1 + (16 * w + 4 * r + lk) * 256 + 16 * cb + lr] = gf1[cb][r];
+    if (t < 64) sl[P_FB1 + t] = gfb1;
+    sl[P_F2 + w * 64 + l] = gf2;
+    if (l == 0) sl[P_FB2 + w] = gfb2;
+    if (t == 0) sl[P_N] = gloss;
+}
+
+// ------------------------------------------------------------------ 4. train B
+__global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
+    __shared__ Smem M;
+    const int t = threadIdx.x, l = t & 63, w = t >> 6;
+    const int lr = l & 15, lk = l >> 4;
+    d4 gw2[16];  // dW2 of wave w: o = 16w + 4r + lk, c = 16 cbc + lr, tap; index tap * 4 + cbc
+#pragma unroll
+    for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
+    double gw1[4] = {0.0, 0.0, 0.0, 0.0}, gb1 = 0.0, gb2 = 0.0;
+    stage_small(M, A.on);
+    const int64_t ntiles = (A.batch + TB - 1) / TB;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t b0 = tile * TB;
+        __syncthreads();
+        if (t < TB) {
+            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+            if (b0 + t < A.batch) sv = A.R.s[A.idx[b0 + t]];
+            put_row(M.x + t * XS, sv);
+        }
+        // dZ2 of the tile -> M.h2 (rows of padded boards are zero)
+        for (int e = t; e < TB * 64; e += NT) {
+            const int bq = e >> 6, k4 = (e & 63) * 4;
+            const double* src = A.dz2 + (b0 + bq) * 256 + k4;
+            double* dst = M.h2 + bq * HS + k4;
+            dst[0] = src[0];
+            dst[1] = src[1];
+            dst[2] = src[2];
+            dst[3] = src[3];
+        }
+        __syncthreads();
+        conv1(M);
+        __syncthreads();
+        // db2[o] (thread o < 64)
+        if (t < 64) {
+            double acc = 0.0;
+            for (int s = 0; s < TB; ++s)
+#pragma unroll
+                for (int p = 0; p < 4; ++p) acc += M.h2[s * HS + t * 4 + p];
+            gb2 += acc;
+        }
+        // dW2 += dZ2^T im2col(D): wave w -> rows o = 16w .., K = 64 rows (p, b)
+#pragma unroll 2
+        for (int s = 0; s < 16; ++s) {
+            const int p = s >> 2, bq = 4 * (s & 3) + lk;
+            const double a = M.h2[bq * HS + (16 * w + lr) * 4 + p];
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap) {
+                const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
+#pragma unroll
+                for (int cbc = 0; cbc < 4; ++cbc)
+                    gw2[tap * 4 + cbc] = mfma(a, dr[16 * cbc], gw2[tap * 4 + cbc]);
+            }
+        }
+        // dD = col2im(dZ2 W2): wave w -> channels c = 16w .. 16w+15, one accumulator per
+        // conv1 position, K = 64 output channels
+        d4 dd[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) dd[q] = d4{0.0, 0.0, 0.0, 0.0};
+        const double* bp = A.p2b + (size_t)w * 4 * 16 * 64 + l;
+#pragma unroll 2
+        for (int s = 0; s < 16; ++s) {
+            double bt[4];
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap) bt[tap] = bp[(tap * 16 + s) * 64];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const double a = M.h2[lr * HS + (4 * s + lk) * 4 + p];
+#pragma unroll
+                for (int tap = 0; tap < 4; ++tap) {
+                    const int q = pos_of(p, tap);
+                    dd[q] = mfma(a, bt[tap], dd[q]);
+                }
+            }
+        }
+        // relu'(conv1) mask -> dZ1; dW1[c][tap] += dZ1 * x, db1[c] += dZ1
+        {
+            const int c = 16 * w + lr;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int bq = 4 * r + lk;
+                const double* xr = M.x + bq * XS;
+#pragma unroll
+                for (int q = 0; q < 9; ++q) {
+                    const double z = M.d[q * DPL + bq * DSB + c] > 0.0 ? dd[q][r] : 0.0;
+                    const int i0 = (q / 3) * 4 + (q % 3);
+                    gw1[0] = fma(z, xr[i0], gw1[0]);
+                    gw1[1] = fma(z, xr[i0 + 1], gw1[1]);
+                    gw1[2] = fma(z, xr[i0 + 4], gw1[2]);
+                    gw1[3] = fma(z, xr[i0 + 5], gw1[3]);
+                    gb1 += z;
+                }
+            }
+        }
+    }
+    // combine the 4 lane groups of a channel in a fixed order (through LDS), then the slab:
+    // conv1.weight [64][1][2][2], conv1.bias, conv2.weight [64][64][2][2], conv2.bias
+    double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+    __syncthreads();
+    double* red = M.d;  // [5][256] (x, d are dead)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[k * 256 + t] = gw1[k];
+    red[4 * 256 + t] = gb1;
+    __syncthreads();
+    if (t < 64) {
+        const int c = t, ww = c >> 4, cl = c & 15;
+        const int base = ww * 64 + cl;  // thread index of lane group 0 for channel c
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const double* v = red + k * 256 + base;
+            const double s = ((v[0] + v[16]) + v[32]) + v[48];
+            if (k < 4) sl[P_W1 + c * 4 + k] = s;
+            else sl[P_B1 + c] = s;
+        }
+        sl[P_B2 + c] = gb2;
+    }
+#pragma unroll
+    for (int tap = 0; tap < 4; ++tap)
+#pragma unroll
+        for (int cbc = 0; cbc < 4; ++cbc)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sl[P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cbc + lr) * 4 + tap] =
+                    gw2[tap * 4 + cbc][r];
+}
+
+// ------------------------------------------------------------------ 5. reduce + Adam
+// torch.optim.Adam (single tensor, amsgrad off, no weight decay) on one float64 element.
+__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
+                                         double g, double& m, double& v, double p) {
+#pragma clang fp contract(off)
+    const double step_size = lr / (1.0 - pow(b1, t));
+    const double bc2_sqrt = sqrt(1.0 - pow(b2, t));
+    m = m + (1.0 - b1) * (g - m);
+    v = v * b2 + (1.0 - b2) * g * g;
+    const double denom = sqrt(v) / bc2_sqrt + eps;
+    return p + (-step_size) * (m / denom);
+}
+
+constexpr int RW = 16;
+static_assert(MAX_WG <= RW * 16, "reduction covers at most RW*16 slabs");
+
+struct RedArgs {
+    const double* slab;
+    int nslab;
+    double* grad;
+    double* loss;
+    const unsigned long long* step_next;
+    unsigned long long* step;
+    double* p[8];
+    double* tp[8];
+    unsigned long long sync_every;
+    double *m, *v;
+    double lr, b1, b2, eps;
+    int adam;
+};
+
+__global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
+    __shared__ double part[RW][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int pos = blockIdx.x * 64 + lane;
+    double r = 0.0;
+    if (pos <= P_N)
+        for (int g = wave; g < A.nslab; g += RW) r += A.slab[(int64_t)g * SLAB + pos];
+    part[wave][lane] = r;
+    __syncthreads();
+    if (wave == 0 && pos <= P_N) {
+        double sum = part[0][lane];
+        for (int k = 1; k < RW; ++k) sum += part[k][lane];
+        if (pos == P_N) {
+            if (A.loss) *A.loss = sum;
+        } else {
+            if (A.grad) A.grad[pos] = sum;
+            if (A.adam) {
+                const int base[8] = {P_W1, P_B1, P_W2, P_B2, P_F1, P_FB1, P_F2, P_FB2};
+                int k = 7;
+                while (pos < base[k]) --k;
+                const unsigned long long tt = *A.step_next;
+                double m = A.m[pos], v = A.v[pos];
+                const double np =
+                    adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sum, m, v, A.p[k][pos - base[k]]);
+                A.m[pos] = m;
+                A.v[pos] = v;
+                A.p[k][pos - base[k]] = np;
+                if (A.sync_every && tt % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
+            }
+        }
+    }
+    if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
+}
+
+int grid_of(int64_t batch) {
+    const int64_t tiles = (batch + TB - 1) / TB;
+    return (int)(tiles < MAX_WG ? tiles : MAX_WG);
+}
+
+Net net_of(const g2048_convnet_params_f64* p) {
+    return Net{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b};
+}
+
+}  // namespace
+
+extern "C" G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch) {
+    if (batch <= 0) return 0;
+    const int64_t tiles = (batch + TB - 1) / TB;
+    // slabs | dZ2 rows | 6 packed matrices | the next-step word
+    return (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + 6 * PACK + 2;
+}
+
+extern "C" G2048_API int g2048_convnet_update_f64(
+    const g2048_convnet_params_f64* online, const g2048_convnet_params_f64* target,
+    g2048_replay* rb, const int64_t* idx_in, int64_t batch, uint64_t seed, uint64_t* step_dev,
+    float gamma, int double_dqn, int64_t* idx_out, double* y_out, double* workspace,
+    double* grad_out, double* loss_out, double* exp_avg, double* exp_avg_sq, double lr,
+    double beta1, double beta2, double eps, uint64_t sync_every, void* stream) {
+    if (!online || !target || !rb || batch <= 0 || !step_dev || !idx_out || !y_out || !workspace)
+        return g2048_fail(G2048_EINVAL, "convnet_update_f64: NULL argument or batch <= 0");
+    const g2048_convnet_params_f64* nets[2] = {online, target};
+    for (const auto* n : nets)
+        if (!n->w1 || !n->b1 || !n->w2 || !n->b2 || !n->fc1_w || !n->fc1_b || !n->fc2_w ||
+            !n->fc2_b)
+            return g2048_fail(G2048_EINVAL, "convnet_update_f64: NULL parameter pointer");
+    const bool adam = exp_avg && exp_avg_sq;
+    if (!adam && !grad_out)
+        return g2048_fail(G2048_EINVAL,
+                          "convnet_update_f64: need exp_avg and exp_avg_sq (Adam) or grad_out");
+    uint8_t *s = nullptr, *s2 = nullptr, *a = nullptr, *d = nullptr;
+    int32_t* r = nullptr;
+    uint64_t* count = nullptr;
+    if (g2048_replay_views(rb, &s, &s2, &a, &r, &d, &count) != G2048_OK) return G2048_EINVAL;
+    const int grid = grid_of(batch);
+    const int64_t tiles = (batch + TB - 1) / TB;
+    double* slab = workspace;
+    double* dz2 = slab + (int64_t)grid * SLAB;
+    double* pk = dz2 + tiles * TB * 256;
+    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(pk + 6 * PACK);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+
+    PackArgs P;
+    P.w2_on = online->w2;
+    P.f1_on = online->fc1_w;
+    P.w2_tg = target->w2;
+    P.f1_tg = target->fc1_w;
+    P.out = pk;
+    hipLaunchKernelGGL(k_pack, dim3(6 * PACK / NT), dim3(NT), 0, st, P);
+
+    Ring R;
+    R.s = reinterpret_cast<const uint4*>(s);
+    R.s2 = reinterpret_cast<const uint4*>(s2);
+    R.a = a;
+    R.d = d;
+    R.r = r;
+    R.count = reinterpret_cast<const unsigned long long*>(count);
+
+    TgtArgs T;
+    T.on = net_of(online);
+    T.tg = net_of(target);
+    T.pon = Packed{pk + 0 * PACK, pk + 1 * PACK};
+    T.ptg = Packed{pk + 2 * PACK, pk + 3 * PACK};
+    T.R = R;
+    T.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    T.idx_in = idx_in;
+    T.batch = batch;
+    T.seed_lo = (uint32_t)seed;
+    T.seed_hi = (uint32_t)(seed >> 32);
+    T.gamma = gamma;
+    T.double_dqn = double_dqn;
+    T.idx_out = idx_out;
+    T.y_out = y_out;
+    T.step_next = step_next;
+    hipLaunchKernelGGL(k_conv64_targets, dim3(grid), dim3(NT), 0, st, T);
+
+    TrainArgs A;
+    A.on = T.on;
+    A.pon = T.pon;
+    A.pf1b = pk + 4 * PACK;
+    A.p2b = pk + 5 * PACK;
+    A.R = R;
+    A.idx = idx_out;
+    A.y = y_out;
+    A.batch = batch;
+    A.dz2 = dz2;
+    A.slab = slab;
+    hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, st, A);
+    hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, st, A);
+
+    RedArgs D;
+    D.slab = slab;
+    D.nslab = grid;
+    D.grad = grad_out;
+    D.loss = loss_out;
+    D.step_next = step_next;
+    D.step = reinterpret_cast<unsigned long long*>(step_dev);
+    double* ps[8] = {online->w1, online->b1, online->w2, online->b2,
+                     online->fc1_w, online->fc1_b, online->fc2_w, online->fc2_b};
+    double* ts[8] = {target->w1, target->b1, target->w2, target->b2,
+                     target->fc1_w, target->fc1_b, target->fc2_w, target->fc2_b};
+    for (int k = 0; k < 8; ++k) {
+        D.p[k] = ps[k];
+        D.tp[k] = ts[k];
+    }
+    D.sync_every = adam ? sync_every : 0ull;
+    D.m = exp_avg;
+    D.v = exp_avg_sq;
+    D.lr = lr;
+    D.b1 = beta1;
+    D.b2 = beta2;
+    D.eps = eps;
+    D.adam = adam ? 1 : 0;
+    hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 63) / 64), dim3(64 * RW), 0, st, D);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "convnet_update_f64: %s", hipGetErrorString(e));
+}

@@ -73,6 +73,10 @@ SIGNATURES = {
     "g2048_dense64_update_f64": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
                                         _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
                                         _u64, _vp]),
+    "g2048_convnet_update_f64_workspace": (_i64, [_i64]),
+    "g2048_convnet_update_f64": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,
+                                        _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
+                                        _u64, _vp]),
     "g2048_convnet_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
     "g2048_astar_search": (_int, [_vp, _i64, _int, _u64, _u64, _int, _i64, _i64, _vp, _vp, _vp,
@@ -84,7 +88,8 @@ SIGNATURES = {
 
 
 class ConvNetParams(C.Structure):
-    """g2048_convnet_params: device pointers of the conv Q-net's 8 fp32 tensors."""
+    """g2048_convnet_params / g2048_convnet_params_f64: device pointers of the conv Q-net's 8
+    tensors (fp32 / fp64)."""
     _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2", "fc1_w", "fc1_b", "fc2_w",
                                           "fc2_b")]
 

@@ -66,12 +66,14 @@ class DQNLearner:
         # fused HIP kernels (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip) for the fp32
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
         self.kind = qnet.kind_of(self.model) if self.loss_fn is None else None
-        # float64 (the reference's precision): the dense 16-64-4 net has a fused update too
-        # (g2048_dense64_update_f64); single process -- with world > 1 it runs the torch path
+        # float64 (the reference's precision): the dense 16-64-4 and conv nets have fused
+        # updates too (g2048_dense64_update_f64, g2048_convnet_update_f64); single process --
+        # with world > 1 they run the torch path
+        k64 = qnet.kind64_of(self.model)
         self.f64 = (self.kind is None and self.loss_fn is None and self.world == 1
-                    and qnet.kind64_of(self.model) == "dense64")
+                    and k64 is not None)
         if self.f64:
-            self.kind = "dense64"
+            self.kind = k64
         self.fused = self.kind is not None
         self._upd = None
         if self.fused:
@@ -94,8 +96,10 @@ class DQNLearner:
             # gradient reduction.  conv: targets (two half-grids, one net each), train forward,
             # train backward, reduce+Adam = 4 launches; dense64: sampler + targets + gradient in
             # ONE launch + reduce+Adam = 2 launches
-            upd = (qnet.Dense64Update64 if self.f64 else
-                   qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate)
+            if self.f64:
+                upd = qnet.Dense64Update64 if self.kind == "dense64" else qnet.ConvUpdate64
+            else:
+                upd = qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate
             self._upd = upd(self.model, self.target, self.B,
                             adam=self._adam if self.world == 1 else None)
             rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
@@ -325,7 +329,7 @@ class Trainer:
         self._done = torch.empty(env.n, dtype=torch.uint8, device=env.device)
         # fused conv learner: Q of the greedy-branch boards only (rows of explorers unused)
         self._q = (torch.zeros((env.n, 4), dtype=torch.float32, device=env.device)
-                   if learner.fused and learner.kind == "conv" else None)
+                   if learner.fused and learner.kind == "conv" and not learner.f64 else None)
         self._numbers = {}  # (board, board_episode) -> Experiment episode number
 
     def prefill(self, steps: int) -> None:

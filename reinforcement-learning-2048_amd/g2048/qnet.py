@@ -44,9 +44,11 @@ def kind_of(model) -> str | None:
 
 
 def kind64_of(model) -> str | None:
-    """'dense64' when the fused float64 update exists for this model, else None."""
+    """'conv' / 'dense64' when a fused float64 update exists for this model, else None."""
     if next(model.parameters()).dtype != torch.float64:
         return None
+    if isinstance(model, Conv2048):
+        return "conv"
     return "dense64" if is_dense64(model) else None
 
 
@@ -269,6 +271,45 @@ class Dense64Update64:
             N.ptr(v), float(lr), float(b1), float(b2), float(eps),
             int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
             "g2048_dense64_update_f64")
+
+
+class ConvUpdate64:
+    """One whole Double-DQN update of a float64 conv net (the reference's precision) in five
+    launches (g2048_convnet_update_f64): operand packing, targets, two train launches and the
+    reduction with Adam (Adam64) applied in place; the same call and step_dev protocol as
+    Dense64Update64."""
+
+    def __init__(self, model, target, batch: int, adam: Adam64 | None = None):
+        if kind64_of(model) != "conv" or kind64_of(target) != "conv":
+            raise TypeError("ConvUpdate64 needs fp64 Conv2048 online and target nets")
+        self.on = N.ConvNetParams(*[t.data_ptr() for t in
+                                    _tensors(model, _CONV_ORDER, torch.float64)])
+        self.tg = N.ConvNetParams(*[t.data_ptr() for t in
+                                    _tensors(target, _CONV_ORDER, torch.float64)])
+        self.batch = int(batch)
+        self.adam = adam
+        dev = next(model.parameters()).device
+        n = N.load().g2048_convnet_update_f64_workspace(self.batch)
+        self.workspace = torch.empty(n, dtype=torch.float64, device=dev)
+
+    def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
+                 idx_in=None, grad_out=None, loss_out=None):
+        if idx_out.numel() != self.batch or y_out.numel() != self.batch:
+            raise ValueError("idx_out / y_out must have `batch` elements")
+        if y_out.dtype != torch.float64:
+            raise TypeError("y_out must be float64")
+        if self.adam is None and grad_out is None:
+            raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        a = self.adam
+        m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
+        lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)
+        N.check(N.load().g2048_convnet_update_f64(
+            C.byref(self.on), C.byref(self.tg), replay.handle, N.ptr(idx_in), self.batch,
+            int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)), N.ptr(idx_out),
+            N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out), N.ptr(loss_out), N.ptr(m),
+            N.ptr(v), float(lr), float(b1), float(b2), float(eps),
+            int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
+            "g2048_convnet_update_f64")
 
 
 class Dense64Update:
