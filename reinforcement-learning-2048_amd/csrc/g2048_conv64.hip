@@ -12,7 +12,7 @@
 // element-wise work on VALU.  Every sum has a fixed order, so an update is run-to-run bitwise
 // reproducible.  Layer order and shapes follow nets.Conv2048 / the reference nn.Sequential.
 //
-// f64 MFMA 16x16x4 fragments (gfx950, measured by tools/scratch/mfma64_probe.hip):
+// f64 MFMA 16x16x4 fragments (gfx950, measured by tools/mfma64_probe.hip):
 //   A (16 x 4): lane l holds A[i = l % 16][k = l / 16]
 //   B (4 x 16): lane l holds B[k = l / 16][j = l % 16]
 //   D (16 x16): lane l, register r holds D[i = 4 r + l / 16][j = l % 16]
