@@ -411,6 +411,20 @@ G2048_API int g2048_convnet_update_f64(const g2048_convnet_params_f64* online,
                                        double beta2, double eps, uint64_t sync_every,
                                        void* stream);
 
+/* The conv net's forward in float64 (the rollout's Q of a float64 learner): Q[b] (f64[n][4]) of
+ * rows[idx ? idx[b] : b]; and the greedy-branch-only form, with the selection and arguments of
+ * g2048_convnet_forward_greedy (rows of exploring boards are not written).  workspace: device
+ * f64[G2048_CONVNET_F64_FWD_WORKSPACE] (the packed weight operands, rewritten by every call). */
+#define G2048_CONVNET_F64_FWD_WORKSPACE 53248
+G2048_API int g2048_convnet_forward_f64(const g2048_convnet_params_f64* params,
+                                        const uint8_t* rows_dev, const int64_t* idx_dev, int64_t n,
+                                        double* q_out_dev, double* workspace_dev, void* stream);
+G2048_API int g2048_convnet_forward_greedy_f64(const g2048_convnet_params_f64* params,
+                                               g2048_env* env, const double* eps_dev, double eps,
+                                               double eps_decay_episodes, double eps_min,
+                                               double* q_out_dev, double* workspace_dev,
+                                               void* stream);
+
 /* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
  * Best-first search from one board (exponents start[16], merge score start_score) until a
  * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion

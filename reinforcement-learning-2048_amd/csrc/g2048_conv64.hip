@@ -41,7 +41,40 @@ constexpr int MAX_WG = 256;
 constexpr int P_W1 = 0, P_B1 = 256, P_W2 = 320, P_B2 = 16704, P_F1 = 16768, P_FB1 = 33152,
               P_F2 = 33216, P_FB2 = 33472, P_N = 33476;
 constexpr int SLAB = P_N + 4;  // + the loss at P_N
-constexpr int PACK = 16384;    // doubles per packed matrix
+constexpr int PACK = 16384;    // doubles per packed 64 x 256 matrix
+constexpr int PACKU = 9 * 4096;  // doubles of the packed Winograd conv2 weights U
+// packed operands (workspace): U and fc1 of the online net, U and fc1 of the target net, the
+// fc1 and conv2 backward operands of the online net
+constexpr int O_U_ON = 0, O_F1_ON = PACKU, O_U_TG = PACKU + PACK, O_F1_TG = 2 * PACKU + PACK,
+              O_F1B = 2 * PACKU + 2 * PACK, O_P2B = 2 * PACKU + 3 * PACK,
+              PACK_ALL = 2 * PACKU + 4 * PACK, PACK_FWD = PACKU + PACK;
+static_assert(PACK_ALL % 256 == 0 && PACK_FWD % 256 == 0, "pack grid");
+
+// Phase ticks (s_memtime deltas of thread 0 of workgroup 0, charged to the phase that ENDS at the
+// marker), compiled in only for kernel tuning (tools/prof_conv64.hip).
+#ifdef G2048_PHASE_PROF
+__device__ unsigned long long g_cphase[32];
+__device__ unsigned long long g_clast;
+#define CPHASE(k)                                                         \
+    do {                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                        \
+            const unsigned long long n_ = __builtin_amdgcn_s_memtime();   \
+            if ((k) >= 0) g_cphase[(k) < 0 ? 0 : (k)] += n_ - g_clast;    \
+            g_clast = n_;                                                 \
+        }                                                                 \
+    } while (0)
+#else
+#define CPHASE(k)
+#endif
+
+// The packed weights are the same for every tile, so loop-invariant code motion would hoist all
+// of a tile loop's B-fragment loads out of it (hundreds of registers, spills).  Passing the base
+// pointer through an empty asm per use makes it opaque and keeps each load in its k-step.
+template <typename T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -51,17 +84,21 @@ struct Net {
     const double *w1, *b1, *w2, *b2, *f1, *fb1, *f2, *fb2;
 };
 
-// packed operands of one net: conv2 forward B (P2f), fc1 forward B (Pf1)
+// packed operands of one net: conv2 forward B in the Winograd domain (U), fc1 forward B (Pf1)
 struct Packed {
-    const double *p2f, *pf1;
+    const double *u, *pf1;
+};
+
+struct SmallW {
+    double w1[256], b1[64], b2[64], fb1[64], f2[256], fb2[4];
 };
 
 struct alignas(16) Smem {
     double x[TB * XS];      // input exponents of the tile (s' or s)
-    double d[9 * DPL];      // conv1 output (relu), [pos][board][c]
+    double d[9 * DPL];      // [9][board][c]: forward: V = B^T d B (Winograd), train B: conv1 d
     double h2[TB * HS];     // conv2 output (relu), flatten order o*4 + p; train B: dZ2
     double h3[TB * H3S];    // fc1 output (relu); train A: dZ3
-    double w1[256], b1[64], b2[64], fb1[64], f2[256], fb2[4];  // the small parameters of a net
+    SmallW sw[2];           // the small parameters of up to two nets
     double q[TB * 4];
     double q2[TB * 4];
     double y[TB];
@@ -83,23 +120,23 @@ __device__ __forceinline__ void put_row(double* xr, uint4 v) {
     }
 }
 
-__device__ __forceinline__ void stage_small(Smem& M, const Net& n) {
+__device__ __forceinline__ void stage_small(SmallW& W, const Net& n) {
     const int t = threadIdx.x;
-    M.w1[t] = n.w1[t];
-    M.f2[t] = n.f2[t];
+    W.w1[t] = n.w1[t];
+    W.f2[t] = n.f2[t];
     if (t < 64) {
-        M.b1[t] = n.b1[t];
-        M.b2[t] = n.b2[t];
-        M.fb1[t] = n.fb1[t];
+        W.b1[t] = n.b1[t];
+        W.b2[t] = n.b2[t];
+        W.fb1[t] = n.fb1[t];
     }
-    if (t < 4) M.fb2[t] = n.fb2[t];
+    if (t < 4) W.fb2[t] = n.fb2[t];
 }
 
 // conv1 + relu for the tile in M.x -> M.d[pos][b][c].  Thread (c = t & 63, boards 4g .. 4g+3).
-__device__ __forceinline__ void conv1(Smem& M) {
+__device__ __forceinline__ void conv1(Smem& M, const SmallW& W) {
     const int t = threadIdx.x, c = t & 63, g = t >> 6;
-    const double w0 = M.w1[c * 4 + 0], w1 = M.w1[c * 4 + 1], w2 = M.w1[c * 4 + 2],
-                 w3 = M.w1[c * 4 + 3], bc = M.b1[c];
+    const double w0 = W.w1[c * 4 + 0], w1 = W.w1[c * 4 + 1], w2 = W.w1[c * 4 + 2],
+                 w3 = W.w1[c * 4 + 3], bc = W.b1[c];
 #pragma unroll
     for (int bb = 0; bb < 4; ++bb) {
         const int b = 4 * g + bb;
@@ -119,6 +156,46 @@ __device__ __forceinline__ void conv1(Smem& M) {
     }
 }
 
+// conv1 + relu + the Winograd input transform for the tile in M.x -> M.d = V[xi][b][c]:
+// V = B^T d B over the 3x3 map d of (b, c), B^T = [[1,-1,0],[0,1,0],[0,-1,1]].
+__device__ __forceinline__ void conv1_wino(Smem& M, const SmallW& W) {
+    const int t = threadIdx.x, c = t & 63, g = t >> 6;
+    const double w0 = W.w1[c * 4 + 0], w1 = W.w1[c * 4 + 1], w2 = W.w1[c * 4 + 2],
+                 w3 = W.w1[c * 4 + 3], bc = W.b1[c];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+        const int b = 4 * g + bb;
+        const double* xr = M.x + b * XS;
+        double d[9];
+#pragma unroll
+        for (int qy = 0; qy < 3; ++qy)
+#pragma unroll
+            for (int qx = 0; qx < 3; ++qx) {
+                const int i0 = qy * 4 + qx;
+                double a = bc;
+                a = fma(w0, xr[i0], a);
+                a = fma(w1, xr[i0 + 1], a);
+                a = fma(w2, xr[i0 + 4], a);
+                a = fma(w3, xr[i0 + 5], a);
+                d[qy * 3 + qx] = a > 0.0 ? a : 0.0;
+            }
+        double u[9];  // B^T d (along y)
+#pragma unroll
+        for (int x = 0; x < 3; ++x) {
+            u[x] = d[x] - d[3 + x];
+            u[3 + x] = d[3 + x];
+            u[6 + x] = d[6 + x] - d[3 + x];
+        }
+#pragma unroll
+        for (int y = 0; y < 3; ++y) {  // (B^T d) B (along x)
+            double* vr = M.d + b * DSB + c;
+            vr[(3 * y + 0) * DPL] = u[3 * y] - u[3 * y + 1];
+            vr[(3 * y + 1) * DPL] = u[3 * y + 1];
+            vr[(3 * y + 2) * DPL] = u[3 * y + 2] - u[3 * y + 1];
+        }
+    }
+}
+
 // conv1 input position of output position p (0..3, 2x2) shifted by tap (0..3, 2x2): 3x3 index
 __device__ __forceinline__ int pos_of(int p, int tap) {
     return ((p >> 1) + (tap >> 1)) * 3 + (p & 1) + (tap & 1);
@@ -126,71 +203,92 @@ __device__ __forceinline__ int pos_of(int p, int tap) {
 
 // The forward of the tile in M.x through one net (small weights staged in M, big ones packed):
 // M.d, M.h2, M.h3 filled; Q -> q[TB][4].  Starts and ends with a barrier.
-__device__ void forward(Smem& M, const Packed& pk, double* q) {
+__device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
     __syncthreads();  // x and the small weights visible
-    conv1(M);
+    conv1_wino(M, W);
     __syncthreads();
-    // conv2: wave w -> output channels 16w .. 16w+15; 4 row blocks = the 4 output positions
+    CPHASE(3);
+    // conv2 in the Winograd domain, F(2x2, 2x2): M_xi = V_xi U_xi ([16 b x 64 c] x [64 c x 64 o],
+    // nine independent GEMMs, 144 MFMAs per wave instead of the direct form's 256); wave w ->
+    // output channels 16w .. 16w+15.  Then Y = A^T M A (A^T = [[1,1,0],[0,1,1]]), lane-local.
     {
-        d4 acc[4];
+        d4 acc[9];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) acc[p] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = pk.p2f + (size_t)w * 64 * 64 + l;
-        double bcur[8], bnxt[8];
+        for (int x = 0; x < 9; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
+        const double* bp = opaque(pk.u) + (size_t)w * 9 * 16 * 64 + l;  // [w][xi][s][lane]
+        // B fragments two k-steps ahead in three rotating buffers
+        auto ld9 = [&](double(&b)[9], int s) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) bcur[u] = bp[u * 64];
-        for (int s0 = 0; s0 < 64; s0 += 8) {
-            if (s0 + 8 < 64) {
+            for (int x = 0; x < 9; ++x) b[x] = bp[(x * 16 + s) * 64];
+        };
+        auto mm9 = [&](const double(&b)[9], int s) {
+            const double* vr = M.d + lr * DSB + 4 * s + lk;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) bnxt[u] = bp[(s0 + 8 + u) * 64];
-            }
+            for (int x = 0; x < 9; ++x) acc[x] = mfma(vr[x * DPL], b[x], acc[x]);
+        };
+        // fully unrolled (a rolled loop keeps the accumulators in VGPRs and copies them to
+        // AGPRs and back every iteration); a scheduling barrier per step keeps each step's
+        // prefetch where it is written instead of letting the scheduler hoist every load
+        double bb[3][9];
+        ld9(bb[0], 0);
+        ld9(bb[1], 1);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int s = s0 + u, tap = s >> 4, c = 4 * (s & 15) + lk;
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    acc[p] = mfma(M.d[pos_of(p, tap) * DPL + lr * DSB + c], bcur[u], acc[p]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bcur[u] = bnxt[u];
+        for (int s = 0; s < 16; ++s) {
+            if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
+            mm9(bb[s % 3], s);
+            __builtin_amdgcn_sched_barrier(0);
         }
         const int o = 16 * w + lr;
-        const double bo = M.b2[o];
+        const double bo = W.b2[o];
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
+        for (int r = 0; r < 4; ++r) {
+            double n[6];  // A^T M along y: rows py = 0, 1 of 3 columns
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double z = acc[p][r] + bo;
-                M.h2[(4 * r + lk) * HS + o * 4 + p] = z > 0.0 ? z : 0.0;
+            for (int x = 0; x < 3; ++x) {
+                n[x] = acc[x][r] + acc[3 + x][r];
+                n[3 + x] = acc[3 + x][r] + acc[6 + x][r];
             }
+            double* hr = M.h2 + (4 * r + lk) * HS + o * 4;
+#pragma unroll
+            for (int py = 0; py < 2; ++py) {
+                const double z0 = (n[3 * py] + n[3 * py + 1]) + bo;
+                const double z1 = (n[3 * py + 1] + n[3 * py + 2]) + bo;
+                hr[2 * py] = z0 > 0.0 ? z0 : 0.0;
+                hr[2 * py + 1] = z1 > 0.0 ? z1 : 0.0;
+            }
+        }
     }
     __syncthreads();
+    CPHASE(4);
     // fc1: wave w -> units 16w .. 16w+15, K = 256 in 4 interleaved chains
     {
         d4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = pk.pf1 + (size_t)w * 64 * 64 + l;
-        double bcur[8], bnxt[8];
+        const double* bp = opaque(pk.pf1) + (size_t)w * 64 * 64 + l;
+        // B fragments two chunks of 8 k-steps ahead (rotating buffers, fully unrolled)
+        auto ld8 = [&](double(&b)[8], int k) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) bcur[u] = bp[u * 64];
-        for (int s0 = 0; s0 < 64; s0 += 8) {
-            if (s0 + 8 < 64) {
+            for (int u = 0; u < 8; ++u) b[u] = bp[(8 * k + u) * 64];
+        };
+        auto mm8 = [&](const double(&b)[8], int k) {
 #pragma unroll
-                for (int u = 0; u < 8; ++u) bnxt[u] = bp[(s0 + 8 + u) * 64];
-            }
+            for (int u = 0; u < 8; ++u)
+                acc[u & 3] = mfma(M.h2[lr * HS + 4 * (8 * k + u) + lk], b[u], acc[u & 3]);
+        };
+        double bb[3][8];
+        ld8(bb[0], 0);
+        ld8(bb[1], 1);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int s = s0 + u;
-                acc[u & 3] = mfma(M.h2[lr * HS + 4 * s + lk], bcur[u], acc[u & 3]);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) bcur[u] = bnxt[u];
+        for (int k = 0; k < 8; ++k) {
+            if (k + 2 < 8) ld8(bb[(k + 2) % 3], k + 2);
+            mm8(bb[k % 3], k);
+            __builtin_amdgcn_sched_barrier(0);
         }
         const int j = 16 * w + lr;
-        const double bj = M.fb1[j];
+        const double bj = W.fb1[j];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const double z = ((acc[0][r] + acc[1][r]) + (acc[2][r] + acc[3][r])) + bj;
@@ -198,20 +296,27 @@ __device__ void forward(Smem& M, const Packed& pk, double* q) {
         }
     }
     __syncthreads();
-    // fc2 (VALU): thread (b = t >> 2, a = t & 3) for t < 64, two chains
-    if (t < 64) {
-        const int b = t >> 2, a = t & 3;
-        const double* hr = M.h3 + b * H3S;
-        const double* wr = M.f2 + a * 64;
+    CPHASE(5);
+    // fc2 (VALU): thread (b = t >> 4, a = (t >> 2) & 3, part = t & 3) sums units 16 part ..
+    // 16 part + 15; the four parts are combined in a fixed order through lane shuffles
+    {
+        const int b = t >> 4, a = (t >> 2) & 3, part = t & 3;
+        const double* hr = M.h3 + b * H3S + 16 * part;
+        const double* wr = W.f2 + a * 64 + 16 * part;
         double e = 0.0, o = 0.0;
-#pragma unroll 8
-        for (int j = 0; j < 64; j += 2) {
+#pragma unroll
+        for (int j = 0; j < 16; j += 2) {
             e = fma(wr[j], hr[j], e);
             o = fma(wr[j + 1], hr[j + 1], o);
         }
-        q[b * 4 + a] = (e + o) + M.fb2[a];
+        const double v = e + o;
+        const double v1 = __shfl_xor(v, 1);  // the parts of lanes part ^ 1, ^ 2, ^ 3
+        const double v2 = __shfl_xor(v, 2);
+        const double v3 = __shfl_xor(v, 3);
+        if (part == 0) q[b * 4 + a] = ((v + v1) + (v2 + v3)) + W.fb2[a];
     }
     __syncthreads();
+    CPHASE(6);
 }
 
 __device__ __forceinline__ int64_t sample_row(int64_t b, unsigned long long ep,
@@ -232,30 +337,52 @@ struct Ring {
 };
 
 // ------------------------------------------------------------------ 1. pack
+// Operand order of the f64 MFMA B fragments (lane l of k-step s holds B[k = l / 16][j = l % 16]):
+//   U   [w][xi][s][l] = (G g G^T)[xi] of g = W2[o = 16w + lr][c = 4s + lk][.][.],
+//                       G = [[1,0],[1,1],[0,1]] (the Winograd kernel transform)
+//   Pf1 [w][s][l]     = Wf1[16w + lr][4s + lk]                       (fc1 forward)
+//   F1B [w][cb][s][l] = Wf1[4s + lk][64w + 16cb + lr]                (fc1 backward, dH2)
+//   P2B [w][tap][s][l] = W2[4s + lk][16w + lr][tap]                  (conv2 backward, dD)
 struct PackArgs {
     const double *w2_on, *f1_on, *w2_tg, *f1_tg;
-    double* out;  // [6][PACK]: p2f_on, pf1_on, p2f_tg, pf1_tg, pf1b_on, p2b_on
+    double* out;  // PACK_ALL doubles at the O_* offsets (PACK_FWD: the online U and Pf1 only)
 };
 
-__global__ __launch_bounds__(NT) void k_pack(PackArgs A) {
-    const int e = blockIdx.x * NT + threadIdx.x;  // 0 .. 6 * PACK
-    const int m = e / PACK, i = e % PACK;
+__device__ __forceinline__ double pack_u(const double* w2, int i) {
     const int l = i & 63, lr = l & 15, lk = l >> 4;
+    const int s = (i >> 6) & 15, xi = (i >> 10) % 9, w = (i >> 10) / 9;
+    const double* g = w2 + (16 * w + lr) * 256 + (4 * s + lk) * 4;  // g[ty * 2 + tx]
+    const int xy = xi / 3, xx = xi % 3;
+    double r[2];
+#pragma unroll
+    for (int tx = 0; tx < 2; ++tx)
+        r[tx] = xy == 0 ? g[tx] : xy == 1 ? g[tx] + g[2 + tx] : g[2 + tx];
+    return xx == 0 ? r[0] : xx == 1 ? r[0] + r[1] : r[1];
+}
+
+__device__ __forceinline__ double pack_f1(const double* f1, int i) {
+    const int l = i & 63, lr = l & 15, lk = l >> 4;
+    const int s = (i >> 6) & 63, w = i >> 12;
+    return f1[(16 * w + lr) * 256 + 4 * s + lk];
+}
+
+__global__ __launch_bounds__(NT) void k_pack(PackArgs A) {
+    const int e = blockIdx.x * NT + threadIdx.x;
     double v;
-    if (m == 0 || m == 2) {  // conv2 forward: [w][s][l] = W2[16w + lr][4 (s & 15) + lk][s >> 4]
-        const int s = (i >> 6) & 63, w = i >> 12;
-        const double* w2 = m == 0 ? A.w2_on : A.w2_tg;
-        v = w2[(16 * w + lr) * 256 + (4 * (s & 15) + lk) * 4 + (s >> 4)];
-    } else if (m == 1 || m == 3) {  // fc1 forward: [w][s][l] = Wf1[16w + lr][4s + lk]
-        const int s = (i >> 6) & 63, w = i >> 12;
-        const double* f1 = m == 1 ? A.f1_on : A.f1_tg;
-        v = f1[(16 * w + lr) * 256 + 4 * s + lk];
-    } else if (m == 4) {  // fc1 backward: [w][cb][s][l] = Wf1[4s + lk][64w + 16cb + lr]
-        const int s = (i >> 6) & 15, cb = (i >> 10) & 3, w = i >> 12;
-        v = A.f1_on[(4 * s + lk) * 256 + 64 * w + 16 * cb + lr];
-    } else {  // conv2 backward: [w][tap][s][l] = W2[4s + lk][16w + lr][tap]
-        const int s = (i >> 6) & 15, tap = (i >> 10) & 3, w = i >> 12;
-        v = A.w2_on[(4 * s + lk) * 256 + (16 * w + lr) * 4 + tap];
+    if (e < O_F1_ON) {
+        v = pack_u(A.w2_on, e);
+    } else if (e < O_U_TG) {
+        v = pack_f1(A.f1_on, e - O_F1_ON);
+    } else if (e < O_F1_TG) {
+        v = pack_u(A.w2_tg, e - O_U_TG);
+    } else if (e < O_F1B) {
+        v = pack_f1(A.f1_tg, e - O_F1_TG);
+    } else {
+        const int i = e < O_P2B ? e - O_F1B : e - O_P2B;
+        const int l = i & 63, lr = l & 15, lk = l >> 4;
+        const int s = (i >> 6) & 15, q = (i >> 10) & 3, w = i >> 12;
+        v = e < O_P2B ? A.f1_on[(4 * s + lk) * 256 + 64 * w + 16 * q + lr]
+                      : A.w2_on[(4 * s + lk) * 256 + (16 * w + lr) * 4 + q];
     }
     A.out[e] = v;
 }
@@ -282,33 +409,45 @@ __global__ __launch_bounds__(NT) void k_conv64_targets(TgtArgs A) {
     const unsigned long long ep = A.idx_in ? 0ull : *A.step;
     const unsigned long long count = A.idx_in ? 0ull : *A.R.count;
     if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
+    CPHASE(-1);
+    stage_small(M.sw[0], A.on);
+    stage_small(M.sw[1], A.tg);
     const int64_t ntiles = (A.batch + TB - 1) / TB;
+    // the sampled row of board t of a tile: index, s', r, (1 - d) * gamma (float32 in torch,
+    // src/dqn_lib.py:131); the next tile's row is fetched while the current one runs
+    uint4 s2v = make_uint4(0u, 0u, 0u, 0u);
+    double rj = 0.0;
+    float disc = 0.f;
+    auto fetch = [&](int64_t tile) {
+        s2v = make_uint4(0u, 0u, 0u, 0u);
+        rj = 0.0;
+        disc = 0.f;
+        const int64_t b = tile * TB + t;
+        if (t < TB && tile < ntiles && b < A.batch) {
+            const int64_t row =
+                A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
+            A.idx_out[b] = row;
+            s2v = A.R.s2[row];
+            rj = (double)A.R.r[row];
+            disc = (float)(1 - (int)A.R.d[row]) * A.gamma;
+        }
+    };
+    fetch(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b = tile * TB + t;
         __syncthreads();  // the previous tile is done with M
         if (t < TB) {
-            uint4 s2v = make_uint4(0u, 0u, 0u, 0u);
-            double rj = 0.0;
-            float disc = 0.f;
-            if (b < A.batch) {
-                const int64_t row =
-                    A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
-                A.idx_out[b] = row;
-                s2v = A.R.s2[row];
-                rj = (double)A.R.r[row];
-                // (1 - dones) * discount_factor: float32 in torch (src/dqn_lib.py:131)
-                disc = (float)(1 - (int)A.R.d[row]) * A.gamma;
-            }
             put_row(M.x + t * XS, s2v);
             M.r[t] = rj;
             M.disc[t] = disc;
         }
-        if (A.double_dqn) {
-            stage_small(M, A.on);
-            forward(M, A.pon, M.q2);  // Q_online(s')
-        }
-        stage_small(M, A.tg);  // (forward ended with a barrier: the online weights are dead)
-        forward(M, A.ptg, M.q);  // Q_target(s')
+        fetch(tile + gridDim.x);
+        CPHASE(1);
+        // Q_online(s') (Double DQN) then Q_target(s'): one call site, so forward is inlined once
+#pragma unroll 1
+        for (int net = A.double_dqn ? 0 : 1; net < 2; ++net)
+            forward(M, M.sw[net], net ? A.ptg : A.pon, net ? M.q : M.q2);
+        CPHASE(2);
         if (t < TB && b < A.batch) {
             const double* qt = M.q + t * 4;
             double next;
@@ -323,6 +462,7 @@ __global__ __launch_bounds__(NT) void k_conv64_targets(TgtArgs A) {
                 A.y_out[b] = M.r[t] + (double)M.disc[t] * next;
             }
         }
+        CPHASE(7);
     }
 }
 
@@ -348,26 +488,38 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) gf1[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gf2 = 0.0, gfb2 = 0.0, gfb1 = 0.0, gloss = 0.0;
-    stage_small(M, A.on);
+    CPHASE(-1);
+    stage_small(M.sw[0], A.on);
+    const SmallW& W = M.sw[0];
     const int64_t ntiles = (A.batch + TB - 1) / TB;
+    // board t of a tile: s, a, y; the next tile's are fetched while the current one runs
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    int aj = 0;
+    double yj = 0.0;
+    auto fetch = [&](int64_t tile) {
+        sv = make_uint4(0u, 0u, 0u, 0u);
+        aj = 0;
+        yj = 0.0;
+        const int64_t b = tile * TB + t;
+        if (t < TB && tile < ntiles && b < A.batch) {
+            const int64_t row = A.idx[b];
+            sv = A.R.s[row];
+            aj = A.R.a[row];
+            yj = A.y[b];
+        }
+    };
+    fetch(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * TB;
         __syncthreads();
         if (t < TB) {
-            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-            int aj = 0;
-            double yj = 0.0;
-            if (b0 + t < A.batch) {
-                const int64_t row = A.idx[b0 + t];
-                sv = A.R.s[row];
-                aj = A.R.a[row];
-                yj = A.y[b0 + t];
-            }
             put_row(M.x + t * XS, sv);
             M.act[t] = aj;
             M.y[t] = yj;
         }
-        forward(M, A.pon, M.q);  // Q_online(s); h2, h3 kept
+        fetch(tile + gridDim.x);
+        CPHASE(8);
+        forward(M, W, A.pon, M.q);  // Q_online(s); h2, h3 kept
         if (t < TB) {
             double dq = 0.0, ls = 0.0;
             if (b0 + t < A.batch) {
@@ -398,11 +550,12 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
             gloss += ls;
         }
         __syncthreads();  // h3 is overwritten with dZ3
+        CPHASE(9);
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb) {
             const int s = 4 * w + bb;
             double& hv = M.h3[s * H3S + l];
-            hv = hv > 0.0 ? M.dq[s] * M.f2[M.act[s] * 64 + l] : 0.0;
+            hv = hv > 0.0 ? M.dq[s] * W.f2[M.act[s] * 64 + l] : 0.0;
         }
         __syncthreads();
         if (t < 64) {
@@ -410,6 +563,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
             for (int s = 0; s < TB; ++s) acc += M.h3[s * H3S + t];
             gfb1 += acc;
         }
+        CPHASE(10);
         // dWf1 += dZ3^T H2: wave w -> rows j = 16w .., 16 column blocks, K = 16 boards
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -418,17 +572,31 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
             for (int cb = 0; cb < 16; ++cb)
                 gf1[cb] = mfma(a, M.h2[(4 * s + lk) * HS + 16 * cb + lr], gf1[cb]);
         }
+        CPHASE(11);
         // dH2 = dZ3 Wf1 (masked by relu'(H2)) -> dZ2: wave w -> columns 64w .. 64w+63
         {
             d4 acc[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-            const double* bp = A.pf1b + (size_t)w * 4 * 16 * 64 + l;
-#pragma unroll 4
-            for (int s = 0; s < 16; ++s) {
+            const double* bp = opaque(A.pf1b) + (size_t)w * 4 * 16 * 64 + l;
+            // B fragments two k-steps ahead (rotating buffers, fully unrolled)
+            auto ld4 = [&](double(&b)[4], int s) {
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) b[cb] = bp[(cb * 16 + s) * 64];
+            };
+            auto mm4 = [&](const double(&b)[4], int s) {
                 const double a = M.h3[lr * H3S + 4 * s + lk];
 #pragma unroll
-                for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(a, bp[(cb * 16 + s) * 64], acc[cb]);
+                for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(a, b[cb], acc[cb]);
+            };
+            double bb[3][4];
+            ld4(bb[0], 0);
+            ld4(bb[1], 1);
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                if (s + 2 < 16) ld4(bb[(s + 2) % 3], s + 2);
+                mm4(bb[s % 3], s);
+                __builtin_amdgcn_sched_barrier(0);
             }
 #pragma unroll
             for (int cb = 0; cb < 4; ++cb)
@@ -438,6 +606,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
                     A.dz2[(b0 + bq) * 256 + k] = M.h2[bq * HS + k] > 0.0 ? acc[cb][r] : 0.0;
                 }
         }
+        CPHASE(12);
     }
     // slab: fc1.weight [64][256], fc1.bias, fc2.weight [4][64], fc2.bias, loss
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
@@ -449,6 +618,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
     sl[P_F2 + w * 64 + l] = gf2;
     if (l == 0) sl[P_FB2 + w] = gfb2;
     if (t == 0) sl[P_N] = gloss;
+    CPHASE(13);
 }
 
 // ------------------------------------------------------------------ 4. train B
@@ -460,29 +630,37 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gw1[4] = {0.0, 0.0, 0.0, 0.0}, gb1 = 0.0, gb2 = 0.0;
-    stage_small(M, A.on);
+    CPHASE(-1);
+    stage_small(M.sw[0], A.on);
     const int64_t ntiles = (A.batch + TB - 1) / TB;
+    // the tile's boards and its dZ2 rows (16 x 256 doubles, 16-byte loads); the next tile's are
+    // fetched while the current one runs
+    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    double2 zv[8];
+    auto fetch = [&](int64_t tile) {
+        sv = make_uint4(0u, 0u, 0u, 0u);
+        const int64_t b = tile * TB + t;
+        if (t < TB && tile < ntiles && b < A.batch) sv = A.R.s[A.idx[b]];
+        if (tile < ntiles) {
+            const double2* src = reinterpret_cast<const double2*>(A.dz2 + tile * TB * 256);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) zv[k] = src[t + NT * k];
+        }
+    };
+    fetch(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t b0 = tile * TB;
         __syncthreads();
-        if (t < TB) {
-            uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-            if (b0 + t < A.batch) sv = A.R.s[A.idx[b0 + t]];
-            put_row(M.x + t * XS, sv);
+        if (t < TB) put_row(M.x + t * XS, sv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {  // element pair e = t + NT k: row e / 128, column 2 (e % 128)
+            const int e = t + NT * k;
+            *reinterpret_cast<double2*>(M.h2 + (e >> 7) * HS + 2 * (e & 127)) = zv[k];
         }
-        // dZ2 of the tile -> M.h2 (rows of padded boards are zero)
-        for (int e = t; e < TB * 64; e += NT) {
-            const int bq = e >> 6, k4 = (e & 63) * 4;
-            const double* src = A.dz2 + (b0 + bq) * 256 + k4;
-            double* dst = M.h2 + bq * HS + k4;
-            dst[0] = src[0];
-            dst[1] = src[1];
-            dst[2] = src[2];
-            dst[3] = src[3];
-        }
+        fetch(tile + gridDim.x);
+        CPHASE(14);
+        conv1(M, M.sw[0]);
         __syncthreads();
-        conv1(M);
-        __syncthreads();
+        CPHASE(15);
         // db2[o] (thread o < 64)
         if (t < 64) {
             double acc = 0.0;
@@ -504,27 +682,37 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
                     gw2[tap * 4 + cbc] = mfma(a, dr[16 * cbc], gw2[tap * 4 + cbc]);
             }
         }
+        CPHASE(16);
         // dD = col2im(dZ2 W2): wave w -> channels c = 16w .. 16w+15, one accumulator per
         // conv1 position, K = 64 output channels
         d4 dd[9];
 #pragma unroll
         for (int q = 0; q < 9; ++q) dd[q] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = A.p2b + (size_t)w * 4 * 16 * 64 + l;
-#pragma unroll 2
-        for (int s = 0; s < 16; ++s) {
-            double bt[4];
+        const double* bp = opaque(A.p2b) + (size_t)w * 4 * 16 * 64 + l;
+        // B fragments two k-steps ahead (fully unrolled, rotating buffers)
+        double bt[3][4];
 #pragma unroll
-            for (int tap = 0; tap < 4; ++tap) bt[tap] = bp[(tap * 16 + s) * 64];
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int tap = 0; tap < 4; ++tap) bt[s][tap] = bp[(tap * 16 + s) * 64];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            if (s + 2 < 16) {
+#pragma unroll
+                for (int tap = 0; tap < 4; ++tap) bt[(s + 2) % 3][tap] = bp[(tap * 16 + s + 2) * 64];
+            }
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
                 const double a = M.h2[lr * HS + (4 * s + lk) * 4 + p];
 #pragma unroll
                 for (int tap = 0; tap < 4; ++tap) {
                     const int q = pos_of(p, tap);
-                    dd[q] = mfma(a, bt[tap], dd[q]);
+                    dd[q] = mfma(a, bt[s % 3][tap], dd[q]);
                 }
             }
+            __builtin_amdgcn_sched_barrier(0);
         }
+        CPHASE(17);
         // relu'(conv1) mask -> dZ1; dW1[c][tap] += dZ1 * x, db1[c] += dZ1
         {
             const int c = 16 * w + lr;
@@ -544,6 +732,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
                 }
             }
         }
+        CPHASE(18);
     }
     // combine the 4 lane groups of a channel in a fixed order (through LDS), then the slab:
     // conv1.weight [64][1][2][2], conv1.bias, conv2.weight [64][64][2][2], conv2.bias
@@ -574,6 +763,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             for (int r = 0; r < 4; ++r)
                 sl[P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cbc + lr) * 4 + tap] =
                     gw2[tap * 4 + cbc][r];
+    CPHASE(19);
 }
 
 // ------------------------------------------------------------------ 5. reduce + Adam
@@ -641,6 +831,81 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
     if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
 }
 
+// ------------------------------------------------------------------ rollout forward
+// Q (float64) of boards rows[idx[b]] / rows[b] -- or, with a step clock, only of the env's boards
+// whose next eps-greedy step takes the greedy branch, the only branch where
+// epsilon_greedy_policy evaluates the model (src/dqn_lib.py:20-24; the selection of
+// g2048_convnet_forward_greedy).  Workgroup w owns the boards [w*chunk, (w+1)*chunk): per window
+// of NT boards the selected ones are queued (ballot + prefix) and run in 16-board tiles through
+// forward(); fewer than 16 left over carry into the next window.  Q of a board does not depend
+// on its tile mates.
+struct Fwd64Args {
+    Net on;
+    Packed pk;
+    const uint4* rows;
+    const int64_t* idx;
+    int64_t n;
+    double* q;
+    const uint64_t* clock;  // null: every board
+    const uint32_t* ep;
+    uint64_t board_offset;
+    uint32_t seed_lo, seed_hi;
+    const double* eps_dev;
+    double eps, eps_decay, eps_min;
+    int64_t chunk;
+};
+
+__global__ __launch_bounds__(NT) void k_conv64_forward(Fwd64Args A) {
+    __shared__ Smem M;
+    __shared__ int32_t queue[NT + TB];
+    __shared__ int32_t wcnt[4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    stage_small(M.sw[0], A.on);
+    const int64_t c0 = (int64_t)blockIdx.x * A.chunk;
+    const int64_t c1 = c0 + A.chunk < A.n ? c0 + A.chunk : A.n;
+    int qn = 0;
+    for (int64_t w0 = c0; w0 < c1; w0 += NT) {
+        const bool last = w0 + NT >= c1;
+        const int64_t i = w0 + t;
+        bool g = i < c1;
+        if (g && A.clock) {
+            const uint4 u = g2048::draw(A.seed_lo, A.seed_hi, A.board_offset + (uint64_t)i,
+                                        g2048::DOMAIN_STEP, A.clock[i >> 6]);
+            const uint32_t e = A.eps_decay > 0.0 ? A.ep[4 * i] : 0u;
+            g = !g2048::explores(u.y, g2048::step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, e));
+        }
+        const uint64_t bal = __ballot(g);
+        if (lane == 0) wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int base = qn;
+        for (int ww = 0; ww < wv; ++ww) base += wcnt[ww];
+        if (g) queue[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(i - c0);
+        qn += (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+        __syncthreads();
+        const int nt = last ? (qn + TB - 1) / TB : qn / TB;
+        for (int j = 0; j < nt; ++j) {
+            const int nb = qn - j * TB < TB ? qn - j * TB : TB;
+            if (t < TB) {
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (t < nb) {
+                    const int64_t b = c0 + queue[j * TB + t];
+                    v = A.rows[A.idx ? A.idx[b] : b];
+                }
+                put_row(M.x + t * XS, v);
+            }
+            forward(M, M.sw[0], A.pk, M.q);
+            if (t < nb * 4) A.q[(c0 + queue[j * TB + (t >> 2)]) * 4 + (t & 3)] = M.q[t];
+        }
+        // carry the remainder (< TB boards) to the front of the queue
+        const int rem = qn - nt * TB;
+        __syncthreads();
+        const int32_t keep = t < rem ? queue[nt * TB + t] : 0;
+        __syncthreads();
+        if (t < rem) queue[t] = keep;
+        qn = rem;
+    }
+}
+
 int grid_of(int64_t batch) {
     const int64_t tiles = (batch + TB - 1) / TB;
     return (int)(tiles < MAX_WG ? tiles : MAX_WG);
@@ -652,11 +917,73 @@ Net net_of(const g2048_convnet_params_f64* p) {
 
 }  // namespace
 
+static int fwd64_launch(const g2048_convnet_params_f64* p, Fwd64Args& F, double* workspace,
+                        void* stream, const char* what) {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    PackArgs P{p->w2, p->fc1_w, p->w2, p->fc1_w, workspace};
+    hipLaunchKernelGGL(k_pack, dim3(PACK_FWD / NT), dim3(NT), 0, st, P);  // online U, Pf1 only
+    F.on = net_of(p);
+    F.pk = Packed{workspace + O_U_ON, workspace + O_F1_ON};
+    const int grid = grid_of(F.n);
+    F.chunk = (F.n + grid - 1) / grid;
+    hipLaunchKernelGGL(k_conv64_forward, dim3(grid), dim3(NT), 0, st, F);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+static bool params_ok(const g2048_convnet_params_f64* n) {
+    return n && n->w1 && n->b1 && n->w2 && n->b2 && n->fc1_w && n->fc1_b && n->fc2_w && n->fc2_b;
+}
+
+extern "C" G2048_API int g2048_convnet_forward_f64(const g2048_convnet_params_f64* p,
+                                                   const uint8_t* rows, const int64_t* idx,
+                                                   int64_t n, double* q_out, double* workspace,
+                                                   void* stream) {
+    if (!params_ok(p) || !rows || !q_out || !workspace || n < 0)
+        return g2048_fail(G2048_EINVAL, "convnet_forward_f64: NULL argument or n < 0");
+    if (n == 0) return G2048_OK;
+    Fwd64Args F{};
+    F.rows = reinterpret_cast<const uint4*>(rows);
+    F.idx = idx;
+    F.n = n;
+    F.q = q_out;
+    return fwd64_launch(p, F, workspace, stream, "convnet_forward_f64");
+}
+
+extern "C" G2048_API int g2048_convnet_forward_greedy_f64(
+    const g2048_convnet_params_f64* p, g2048_env* env, const double* eps_dev, double eps,
+    double eps_decay_episodes, double eps_min, double* q_out, double* workspace, void* stream) {
+    if (!params_ok(p) || !env || !q_out || !workspace)
+        return g2048_fail(G2048_EINVAL, "convnet_forward_greedy_f64: NULL argument");
+    uint8_t* board = nullptr;
+    uint32_t* ep = nullptr;
+    uint64_t* clock = nullptr;
+    uint64_t seed = 0, offset = 0;
+    if (g2048_env_views(env, &board, nullptr, &ep, &clock) != G2048_OK ||
+        g2048_env_rng(env, &seed, &offset) != G2048_OK)
+        return G2048_EINVAL;
+    Fwd64Args F{};
+    F.rows = reinterpret_cast<const uint4*>(board);
+    F.n = g2048_env_size(env);
+    if (F.n <= 0) return g2048_fail(G2048_EINVAL, "convnet_forward_greedy_f64: empty env");
+    F.q = q_out;
+    F.clock = clock;
+    F.ep = ep;
+    F.board_offset = offset;
+    F.seed_lo = (uint32_t)seed;
+    F.seed_hi = (uint32_t)(seed >> 32);
+    F.eps_dev = eps_dev;
+    F.eps = eps;
+    F.eps_decay = eps_decay_episodes > 0.0 ? eps_decay_episodes : 0.0;
+    F.eps_min = eps_min;
+    return fwd64_launch(p, F, workspace, stream, "convnet_forward_greedy_f64");
+}
+
 extern "C" G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch) {
     if (batch <= 0) return 0;
     const int64_t tiles = (batch + TB - 1) / TB;
     // slabs | dZ2 rows | 6 packed matrices | the next-step word
-    return (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + 6 * PACK + 2;
+    return (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + PACK_ALL + 2;
 }
 
 extern "C" G2048_API int g2048_convnet_update_f64(
@@ -667,11 +994,8 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     double beta1, double beta2, double eps, uint64_t sync_every, void* stream) {
     if (!online || !target || !rb || batch <= 0 || !step_dev || !idx_out || !y_out || !workspace)
         return g2048_fail(G2048_EINVAL, "convnet_update_f64: NULL argument or batch <= 0");
-    const g2048_convnet_params_f64* nets[2] = {online, target};
-    for (const auto* n : nets)
-        if (!n->w1 || !n->b1 || !n->w2 || !n->b2 || !n->fc1_w || !n->fc1_b || !n->fc2_w ||
-            !n->fc2_b)
-            return g2048_fail(G2048_EINVAL, "convnet_update_f64: NULL parameter pointer");
+    if (!params_ok(online) || !params_ok(target))
+        return g2048_fail(G2048_EINVAL, "convnet_update_f64: NULL parameter pointer");
     const bool adam = exp_avg && exp_avg_sq;
     if (!adam && !grad_out)
         return g2048_fail(G2048_EINVAL,
@@ -685,7 +1009,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     double* slab = workspace;
     double* dz2 = slab + (int64_t)grid * SLAB;
     double* pk = dz2 + tiles * TB * 256;
-    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(pk + 6 * PACK);
+    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(pk + PACK_ALL);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
     PackArgs P;
@@ -694,7 +1018,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     P.w2_tg = target->w2;
     P.f1_tg = target->fc1_w;
     P.out = pk;
-    hipLaunchKernelGGL(k_pack, dim3(6 * PACK / NT), dim3(NT), 0, st, P);
+    hipLaunchKernelGGL(k_pack, dim3(PACK_ALL / NT), dim3(NT), 0, st, P);
 
     Ring R;
     R.s = reinterpret_cast<const uint4*>(s);
@@ -707,8 +1031,8 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     TgtArgs T;
     T.on = net_of(online);
     T.tg = net_of(target);
-    T.pon = Packed{pk + 0 * PACK, pk + 1 * PACK};
-    T.ptg = Packed{pk + 2 * PACK, pk + 3 * PACK};
+    T.pon = Packed{pk + O_U_ON, pk + O_F1_ON};
+    T.ptg = Packed{pk + O_U_TG, pk + O_F1_TG};
     T.R = R;
     T.step = reinterpret_cast<const unsigned long long*>(step_dev);
     T.idx_in = idx_in;
@@ -725,8 +1049,8 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     TrainArgs A;
     A.on = T.on;
     A.pon = T.pon;
-    A.pf1b = pk + 4 * PACK;
-    A.p2b = pk + 5 * PACK;
+    A.pf1b = pk + O_F1B;
+    A.p2b = pk + O_P2B;
     A.R = R;
     A.idx = idx_out;
     A.y = y_out;

@@ -76,6 +76,8 @@ class DQNLearner:
             self.kind = k64
         self.fused = self.kind is not None
         self._upd = None
+        # float64 conv: the rollout's Q through the fused forward as well
+        self._fwd64 = qnet.ConvForward64(self.model) if self.f64 and self.kind == "conv" else None
         if self.fused:
             self._p_on = None if self.f64 else qnet.net_params(self.model)
             self._p_tgt = None if self.f64 else qnet.net_params(self.target)
@@ -222,6 +224,8 @@ class DQNLearner:
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
         if self.fused and not self.f64:
             return qnet.forward(self.model, env.board, params=self._p_on)
+        if self._fwd64 is not None:
+            return self._fwd64(env.board)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 
@@ -328,8 +332,10 @@ class Trainer:
         self._reward = torch.empty(env.n, dtype=torch.int32, device=env.device)
         self._done = torch.empty(env.n, dtype=torch.uint8, device=env.device)
         # fused conv learner: Q of the greedy-branch boards only (rows of explorers unused)
-        self._q = (torch.zeros((env.n, 4), dtype=torch.float32, device=env.device)
-                   if learner.fused and learner.kind == "conv" and not learner.f64 else None)
+        self._q = None
+        if learner.fused and learner.kind == "conv":
+            self._q = torch.zeros((env.n, 4), dtype=torch.float64 if learner.f64 else torch.float32,
+                                  device=env.device)
         self._numbers = {}  # (board, board_episode) -> Experiment episode number
 
     def prefill(self, steps: int) -> None:
@@ -347,7 +353,9 @@ class Trainer:
                                           reward=self._reward, done=self._done,
                                           action=self._action, eps_schedule=sched)
         else:
-            if self._q is not None:  # the model runs on the greedy branch only (src/dqn_lib.py:20-24)
+            if self._q is not None and self.learner._fwd64 is not None:  # greedy branch only
+                q = self.learner._fwd64.greedy(self.env, eps_schedule=sched, out=self._q)
+            elif self._q is not None:  # the model runs on the greedy branch only (src/dqn_lib.py:20-24)
                 q = qnet.forward_greedy(self.learner.model, self.env, eps_schedule=sched,
                                         out=self._q, params=self.learner._p_on)
             else:
@@ -360,7 +368,7 @@ class Trainer:
         outside the capture: hipBLASLt sets up a GEMM shape on its first call, which a stream
         under capture does not permit.  Pure: nothing is stepped."""
         L = self.learner
-        if L.f64:
+        if L.f64 and L._fwd64 is None:
             side = torch.cuda.Stream(self.env.device)
             side.wait_stream(torch.cuda.current_stream(self.env.device))
             with torch.cuda.stream(side):

@@ -121,6 +121,50 @@ def forward_greedy(model, env, epsilon=0.0, eps_schedule=None, out: torch.Tensor
     return out
 
 
+CONV64_FWD_WORKSPACE = 53248  # G2048_CONVNET_F64_FWD_WORKSPACE
+
+
+class ConvForward64:
+    """The float64 conv net's forward (g2048_convnet_forward_f64 / _greedy_f64): Q f64 [n, 4]
+    of board rows, or only of the env boards whose next eps-greedy step is greedy (the rows
+    epsilon_greedy_policy evaluates the model on, src/dqn_lib.py:20-24).  Holds the packed-operand
+    workspace; the parameter pointers are read at construction (the tensors keep their storage)."""
+
+    def __init__(self, model):
+        if kind64_of(model) != "conv":
+            raise TypeError("ConvForward64 needs an fp64 Conv2048")
+        self.p = N.ConvNetParams(*[t.data_ptr() for t in
+                                   _tensors(model, _CONV_ORDER, torch.float64)])
+        self.ws = torch.empty(CONV64_FWD_WORKSPACE, dtype=torch.float64,
+                              device=next(model.parameters()).device)
+
+    def __call__(self, rows: torch.Tensor, idx: torch.Tensor | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+        if rows.dtype != torch.uint8 or rows.dim() != 2 or rows.shape[1] != 16 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous uint8 [*, 16] board tensor")
+        if idx is not None and (idx.dtype != torch.int64 or not idx.is_contiguous()):
+            raise ValueError("idx must be contiguous int64")
+        n = rows.shape[0] if idx is None else idx.numel()
+        if out is None:
+            out = torch.empty((n, 4), dtype=torch.float64, device=rows.device)
+        N.check(N.load().g2048_convnet_forward_f64(C.byref(self.p), N.ptr(rows), N.ptr(idx), n,
+                                                   N.ptr(out), N.ptr(self.ws),
+                                                   N.stream_of(rows.device)),
+                "g2048_convnet_forward_f64")
+        return out
+
+    def greedy(self, env, epsilon=0.0, eps_schedule=None, out: torch.Tensor | None = None):
+        if out is None:
+            out = torch.empty((env.n, 4), dtype=torch.float64, device=env.device)
+        if out.shape != (env.n, 4) or out.dtype != torch.float64 or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous float64 [{env.n}, 4] tensor")
+        eps_ptr, eps_val, dec, mn = env.eps_args(epsilon, eps_schedule)
+        N.check(N.load().g2048_convnet_forward_greedy_f64(
+            C.byref(self.p), env.handle, eps_ptr, eps_val, dec, mn, N.ptr(out), N.ptr(self.ws),
+            N.stream_of(env.device)), "g2048_convnet_forward_greedy_f64")
+        return out
+
+
 class TrainGrad:
     """Graded half of train_step for a fused net: writes the loss and the gradient of
     sum_b (Q(s_b)[a_b] - y_b)^2 into a flat fp32 buffer laid out like

@@ -503,3 +503,85 @@ def test_conv_forward_greedy_rejects_dense(G):
     env = G.VecEnv2048(64, device=DEV)
     with pytest.raises(ValueError):
         qnet.forward_greedy(make_net("dense64", torch.float32, DEV), env, 0.5)
+
+
+@pytest.mark.parametrize("n", [1, 777, 65536])
+def test_conv_forward_f64_matches_torch(G, n):
+    """g2048_convnet_forward_f64 (f64 MFMA) against the float64 torch net (the reference's
+    Sequential arithmetic, src/configs/double_dqn_conv.py:19-28) on the same boards, directly and
+    through an index vector: 1e-12 relative (the sums run in another order)."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    env = G.VecEnv2048(n, device=DEV, seed=40 + n)
+    env.rollout(30)
+    m = det_init(make_net("conv", torch.float64, DEV), 0.4)
+    F = qnet.ConvForward64(m)
+    q = F(env.board)
+    with torch.no_grad():
+        ref = m(env.encode(torch.float64, conv=True)).reshape(n, 4)
+    torch.testing.assert_close(q, ref, rtol=1e-12, atol=1e-12 * float(ref.abs().max()))
+    idx = torch.randint(0, n, (333,), device=DEV)
+    torch.testing.assert_close(F(env.board, idx), q[idx], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("n,form", [(4096, 0.5), (300001, "schedule")])
+def test_conv_forward_greedy_f64_rows(G, n, form):
+    """g2048_convnet_forward_greedy_f64 writes Q only for the boards whose next step is greedy --
+    bitwise the full f64 forward's rows -- and stepping on it equals stepping on the full Q."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    envs = []
+    ep0 = torch.randint(0, 8, (n,), generator=torch.Generator().manual_seed(n), dtype=torch.int32)
+    for _ in range(2):
+        e = G.VecEnv2048(n, device=DEV, seed=11 + n, board_offset=5 * n)
+        e.rollout(25)
+        e.ep[:, 0] = ep0.to(DEV)
+        envs.append(e)
+    if form == "schedule":
+        kw = dict(eps_schedule=(6.0, 0.1))
+        eps = np.maximum((6.0 - ep0.numpy().astype(np.float64)) / 6.0, 0.1)
+    else:
+        kw = dict(epsilon=form)
+        eps = np.full(n, float(form))
+    m = det_init(make_net("conv", torch.float64, DEV), 0.3)
+    F = qnet.ConvForward64(m)
+    full = F(envs[0].board)
+    out = torch.full((n, 4), float("nan"), dtype=torch.float64, device=DEV)
+    F.greedy(envs[0], out=out, **kw)
+    g = _greedy_mask(envs[0], eps)
+    assert 0 < int(g.sum()) < n
+    assert torch.equal(out[g], full[g])
+    assert bool(out[~g].isnan().all())
+    eps_arg = kw.get("epsilon", 0.0)
+    sched = kw.get("eps_schedule")
+    a0, r0, d0 = envs[0].step_egreedy(out, eps_arg, eps_schedule=sched)
+    a1, r1, d1 = envs[1].step_egreedy(full, eps_arg, eps_schedule=sched)
+    assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1)
+    assert torch.equal(envs[0].board, envs[1].board)
+
+
+def test_f64_conv_trainer_graphed_equals_eager(G):
+    """The float64 conv training loop (fused greedy forward + eps-greedy step + fused f64 update)
+    replayed from one hipGraph per iteration equals the eager loop bitwise."""
+    from g2048.learner import DQNLearner, Trainer
+
+    outs = []
+    for graph in (True, False):
+        n = 2048
+        env = G.VecEnv2048(n, device=DEV, seed=77)
+        rb = G.ReplayBuffer(8 * n, device=DEV)
+        L = DQNLearner(rb, net="conv", dtype=torch.float64, batch_size=512, seed=4,
+                       target_sync_every=3)
+        T = Trainer(env, rb, L, updates_per_step=1, min_fill=0, eps_decay_episodes=3,
+                    graph=graph)
+        T.prefill(2)
+        for _ in range(12):
+            T.step()
+        torch.cuda.synchronize()
+        outs.append((env.board.clone(), float(L.last_loss),
+                     torch.cat([p.detach().reshape(-1) for p in L.model.parameters()])))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
+    assert torch.equal(outs[0][2], outs[1][2])
