@@ -44,10 +44,10 @@ constexpr int SLAB = P_N + 4;  // + the loss at P_N
 constexpr int PACK = 16384;    // doubles per packed 64 x 256 matrix
 constexpr int PACKU = 9 * 4096;  // doubles of the packed Winograd conv2 weights U
 // packed operands (workspace): U and fc1 of the online net, U and fc1 of the target net, the
-// fc1 and conv2 backward operands of the online net
+// fc1 and (Winograd) conv2 backward operands of the online net
 constexpr int O_U_ON = 0, O_F1_ON = PACKU, O_U_TG = PACKU + PACK, O_F1_TG = 2 * PACKU + PACK,
-              O_F1B = 2 * PACKU + 2 * PACK, O_P2B = 2 * PACKU + 3 * PACK,
-              PACK_ALL = 2 * PACKU + 4 * PACK, PACK_FWD = PACKU + PACK;
+              O_F1B = 2 * PACKU + 2 * PACK, O_UB = 2 * PACKU + 3 * PACK,
+              PACK_ALL = 3 * PACKU + 3 * PACK, PACK_FWD = PACKU + PACK;
 static_assert(PACK_ALL % 256 == 0 && PACK_FWD % 256 == 0, "pack grid");
 
 // Phase ticks (s_memtime deltas of thread 0 of workgroup 0, charged to the phase that ENDS at the
@@ -70,10 +70,13 @@ __device__ unsigned long long g_clast;
 // The packed weights are the same for every tile, so loop-invariant code motion would hoist all
 // of a tile loop's B-fragment loads out of it (hundreds of registers, spills).  Passing the base
 // pointer through an empty asm per use makes it opaque and keeps each load in its k-step.
-template <typename T>
-__device__ __forceinline__ const T* opaque(const T* p) {
-    asm volatile("" : "+s"(p));
-    return p;
+// The pointer stays in the global address space: a generic pointer would turn the loads into
+// flat loads, which also count on lgkmcnt, so every LDS wait would wait for the prefetches too.
+typedef __attribute__((address_space(1))) const double gdouble;
+__device__ __forceinline__ const gdouble* opaque(const double* p) {
+    const gdouble* g = (const gdouble*)p;
+    asm volatile("" : "+s"(g));
+    return g;
 }
 
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
@@ -132,68 +135,55 @@ __device__ __forceinline__ void stage_small(SmallW& W, const Net& n) {
     if (t < 4) W.fb2[t] = n.fb2[t];
 }
 
-// conv1 + relu for the tile in M.x -> M.d[pos][b][c].  Thread (c = t & 63, boards 4g .. 4g+3).
-__device__ __forceinline__ void conv1(Smem& M, const SmallW& W) {
-    const int t = threadIdx.x, c = t & 63, g = t >> 6;
-    const double w0 = W.w1[c * 4 + 0], w1 = W.w1[c * 4 + 1], w2 = W.w1[c * 4 + 2],
-                 w3 = W.w1[c * 4 + 3], bc = W.b1[c];
+// conv1 + relu for the tile in M.x on MFMA: per conv1 output position q (3x3) one 16x16x4 MFMA
+// per wave, A[b][tap] = x[b][q + tap], B[tap][c] = W1[c][tap] (wave w -> channels 16w ..).  The
+// lane then holds d[q] of (b = 4r + l/16, c = 16w + l%16) for all nine q and writes either
+//   WINO: V = B^T d B (Winograd input transform, B^T = [[1,-1,0],[0,1,0],[0,-1,1]]) -> M.d[xi]
+//   else: d itself -> M.d[q]                      (train B: the direct form and relu mask)
+// The forward and train B run this same function, so their d (and relu mask) agree bitwise.
+template <bool WINO>
+__device__ __forceinline__ uint64_t conv1_mfma(const double* xs, double* dst, const SmallW& W) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
+    const int c = 16 * w + lr;
+    const double wb = W.w1[c * 4 + lk];  // B[tap = lk][c]
+    const int toff = (lk >> 1) * 4 + (lk & 1);
+    const double* xr = xs + lr * XS + toff;
+    d4 dq[9];
 #pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-        const int b = 4 * g + bb;
-        const double* xr = M.x + b * XS;
+    for (int q = 0; q < 9; ++q)
+        dq[q] = mfma(xr[(q / 3) * 4 + (q % 3)], wb, d4{0.0, 0.0, 0.0, 0.0});
+    const double bc = W.b1[c];
+    uint64_t mask = 0;  // bit 9r + q: d > 0 (relu') of (b = 4r + lk, c, q)
 #pragma unroll
-        for (int qy = 0; qy < 3; ++qy)
-#pragma unroll
-            for (int qx = 0; qx < 3; ++qx) {
-                const int i0 = qy * 4 + qx;
-                double a = bc;
-                a = fma(w0, xr[i0], a);
-                a = fma(w1, xr[i0 + 1], a);
-                a = fma(w2, xr[i0 + 4], a);
-                a = fma(w3, xr[i0 + 5], a);
-                M.d[(qy * 3 + qx) * DPL + b * DSB + c] = a > 0.0 ? a : 0.0;
-            }
-    }
-}
-
-// conv1 + relu + the Winograd input transform for the tile in M.x -> M.d = V[xi][b][c]:
-// V = B^T d B over the 3x3 map d of (b, c), B^T = [[1,-1,0],[0,1,0],[0,-1,1]].
-__device__ __forceinline__ void conv1_wino(Smem& M, const SmallW& W) {
-    const int t = threadIdx.x, c = t & 63, g = t >> 6;
-    const double w0 = W.w1[c * 4 + 0], w1 = W.w1[c * 4 + 1], w2 = W.w1[c * 4 + 2],
-                 w3 = W.w1[c * 4 + 3], bc = W.b1[c];
-#pragma unroll
-    for (int bb = 0; bb < 4; ++bb) {
-        const int b = 4 * g + bb;
-        const double* xr = M.x + b * XS;
+    for (int r = 0; r < 4; ++r) {
         double d[9];
 #pragma unroll
-        for (int qy = 0; qy < 3; ++qy)
-#pragma unroll
-            for (int qx = 0; qx < 3; ++qx) {
-                const int i0 = qy * 4 + qx;
-                double a = bc;
-                a = fma(w0, xr[i0], a);
-                a = fma(w1, xr[i0 + 1], a);
-                a = fma(w2, xr[i0 + 4], a);
-                a = fma(w3, xr[i0 + 5], a);
-                d[qy * 3 + qx] = a > 0.0 ? a : 0.0;
-            }
-        double u[9];  // B^T d (along y)
-#pragma unroll
-        for (int x = 0; x < 3; ++x) {
-            u[x] = d[x] - d[3 + x];
-            u[3 + x] = d[3 + x];
-            u[6 + x] = d[6 + x] - d[3 + x];
+        for (int q = 0; q < 9; ++q) {
+            const double a = dq[q][r] + bc;
+            d[q] = a > 0.0 ? a : 0.0;
+            mask |= (uint64_t)(a > 0.0) << (9 * r + q);
         }
+        double* out = dst + (4 * r + lk) * DSB + c;
+        if constexpr (WINO) {
+            double u[9];  // B^T d (along y)
 #pragma unroll
-        for (int y = 0; y < 3; ++y) {  // (B^T d) B (along x)
-            double* vr = M.d + b * DSB + c;
-            vr[(3 * y + 0) * DPL] = u[3 * y] - u[3 * y + 1];
-            vr[(3 * y + 1) * DPL] = u[3 * y + 1];
-            vr[(3 * y + 2) * DPL] = u[3 * y + 2] - u[3 * y + 1];
+            for (int x = 0; x < 3; ++x) {
+                u[x] = d[x] - d[3 + x];
+                u[3 + x] = d[3 + x];
+                u[6 + x] = d[6 + x] - d[3 + x];
+            }
+#pragma unroll
+            for (int y = 0; y < 3; ++y) {  // (B^T d) B (along x)
+                out[(3 * y + 0) * DPL] = u[3 * y] - u[3 * y + 1];
+                out[(3 * y + 1) * DPL] = u[3 * y + 1];
+                out[(3 * y + 2) * DPL] = u[3 * y + 2] - u[3 * y + 1];
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 9; ++q) out[q * DPL] = d[q];
         }
     }
+    return mask;
 }
 
 // conv1 input position of output position p (0..3, 2x2) shifted by tap (0..3, 2x2): 3x3 index
@@ -207,7 +197,7 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
     __syncthreads();  // x and the small weights visible
-    conv1_wino(M, W);
+    conv1_mfma<true>(M.x, M.d, W);
     __syncthreads();
     CPHASE(3);
     // conv2 in the Winograd domain, F(2x2, 2x2): M_xi = V_xi U_xi ([16 b x 64 c] x [64 c x 64 o],
@@ -217,27 +207,30 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
         d4 acc[9];
 #pragma unroll
         for (int x = 0; x < 9; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = opaque(pk.u) + (size_t)w * 9 * 16 * 64 + l;  // [w][xi][s][lane]
+        const gdouble* bp = opaque(pk.u) + (size_t)w * 9 * 16 * 64 + l;  // [w][xi][s][lane]
         // B fragments two k-steps ahead in three rotating buffers
         auto ld9 = [&](double(&b)[9], int s) {
 #pragma unroll
             for (int x = 0; x < 9; ++x) b[x] = bp[(x * 16 + s) * 64];
         };
-        auto mm9 = [&](const double(&b)[9], int s) {
+        auto la9 = [&](double(&a)[9], int s) {
             const double* vr = M.d + lr * DSB + 4 * s + lk;
 #pragma unroll
-            for (int x = 0; x < 9; ++x) acc[x] = mfma(vr[x * DPL], b[x], acc[x]);
+            for (int x = 0; x < 9; ++x) a[x] = vr[x * DPL];
         };
         // fully unrolled (a rolled loop keeps the accumulators in VGPRs and copies them to
         // AGPRs and back every iteration); a scheduling barrier per step keeps each step's
-        // prefetch where it is written instead of letting the scheduler hoist every load
-        double bb[3][9];
+        // prefetches (A one step, B two steps ahead) where they are written
+        double bb[3][9], aa[2][9];
         ld9(bb[0], 0);
         ld9(bb[1], 1);
+        la9(aa[0], 0);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
+            if (s + 1 < 16) la9(aa[(s + 1) & 1], s + 1);
             if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
-            mm9(bb[s % 3], s);
+#pragma unroll
+            for (int x = 0; x < 9; ++x) acc[x] = mfma(aa[s & 1][x], bb[s % 3][x], acc[x]);
             __builtin_amdgcn_sched_barrier(0);
         }
         const int o = 16 * w + lr;
@@ -267,24 +260,26 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
         d4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = opaque(pk.pf1) + (size_t)w * 64 * 64 + l;
+        const gdouble* bp = opaque(pk.pf1) + (size_t)w * 64 * 64 + l;
         // B fragments two chunks of 8 k-steps ahead (rotating buffers, fully unrolled)
         auto ld8 = [&](double(&b)[8], int k) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) b[u] = bp[(8 * k + u) * 64];
         };
-        auto mm8 = [&](const double(&b)[8], int k) {
+        auto la8 = [&](double(&a)[8], int k) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                acc[u & 3] = mfma(M.h2[lr * HS + 4 * (8 * k + u) + lk], b[u], acc[u & 3]);
+            for (int u = 0; u < 8; ++u) a[u] = M.h2[lr * HS + 4 * (8 * k + u) + lk];
         };
-        double bb[3][8];
+        double bb[3][8], aa[2][8];
         ld8(bb[0], 0);
         ld8(bb[1], 1);
+        la8(aa[0], 0);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
+            if (k + 1 < 8) la8(aa[(k + 1) & 1], k + 1);
             if (k + 2 < 8) ld8(bb[(k + 2) % 3], k + 2);
-            mm8(bb[k % 3], k);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u & 3] = mfma(aa[k & 1][u], bb[k % 3][u], acc[u & 3]);
             __builtin_amdgcn_sched_barrier(0);
         }
         const int j = 16 * w + lr;
@@ -342,16 +337,20 @@ struct Ring {
 //                       G = [[1,0],[1,1],[0,1]] (the Winograd kernel transform)
 //   Pf1 [w][s][l]     = Wf1[16w + lr][4s + lk]                       (fc1 forward)
 //   F1B [w][cb][s][l] = Wf1[4s + lk][64w + 16cb + lr]                (fc1 backward, dH2)
-//   P2B [w][tap][s][l] = W2[4s + lk][16w + lr][tap]                  (conv2 backward, dD)
+//   UB  [w][xi][s][l] = (G g G^T)[xi] of g = W2[o = 4s + lk][c = 16w + lr] (conv2 backward, dV)
 struct PackArgs {
     const double *w2_on, *f1_on, *w2_tg, *f1_tg;
     double* out;  // PACK_ALL doubles at the O_* offsets (PACK_FWD: the online U and Pf1 only)
 };
 
+// (G g G^T)[xi] of g = W2[o][c][.][.] for lane l of k-step s of wave w:
+//   forward  (U):  o = 16w + lr, c = 4s + lk     backward (UB): c = 16w + lr, o = 4s + lk
+template <bool BWD>
 __device__ __forceinline__ double pack_u(const double* w2, int i) {
     const int l = i & 63, lr = l & 15, lk = l >> 4;
     const int s = (i >> 6) & 15, xi = (i >> 10) % 9, w = (i >> 10) / 9;
-    const double* g = w2 + (16 * w + lr) * 256 + (4 * s + lk) * 4;  // g[ty * 2 + tx]
+    const int o = BWD ? 4 * s + lk : 16 * w + lr, c = BWD ? 16 * w + lr : 4 * s + lk;
+    const double* g = w2 + o * 256 + c * 4;  // g[ty * 2 + tx]
     const int xy = xi / 3, xx = xi % 3;
     double r[2];
 #pragma unroll
@@ -370,19 +369,20 @@ __global__ __launch_bounds__(NT) void k_pack(PackArgs A) {
     const int e = blockIdx.x * NT + threadIdx.x;
     double v;
     if (e < O_F1_ON) {
-        v = pack_u(A.w2_on, e);
+        v = pack_u<false>(A.w2_on, e);
     } else if (e < O_U_TG) {
         v = pack_f1(A.f1_on, e - O_F1_ON);
     } else if (e < O_F1_TG) {
-        v = pack_u(A.w2_tg, e - O_U_TG);
+        v = pack_u<false>(A.w2_tg, e - O_U_TG);
     } else if (e < O_F1B) {
         v = pack_f1(A.f1_tg, e - O_F1_TG);
-    } else {
-        const int i = e < O_P2B ? e - O_F1B : e - O_P2B;
+    } else if (e < O_UB) {
+        const int i = e - O_F1B;
         const int l = i & 63, lr = l & 15, lk = l >> 4;
         const int s = (i >> 6) & 15, q = (i >> 10) & 3, w = i >> 12;
-        v = e < O_P2B ? A.f1_on[(4 * s + lk) * 256 + 64 * w + 16 * q + lr]
-                      : A.w2_on[(4 * s + lk) * 256 + (16 * w + lr) * 4 + q];
+        v = A.f1_on[(4 * s + lk) * 256 + 64 * w + 16 * q + lr];
+    } else {
+        v = pack_u<true>(A.w2_on, e - O_UB);
     }
     A.out[e] = v;
 }
@@ -471,7 +471,7 @@ struct TrainArgs {
     Net on;
     Packed pon;
     const double* pf1b;  // fc1 backward operands
-    const double* p2b;   // conv2 backward operands
+    const double* p2b;   // conv2 backward operands (Winograd: UB)
     Ring R;
     const int64_t* idx;
     const double* y;
@@ -578,7 +578,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
             d4 acc[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-            const double* bp = opaque(A.pf1b) + (size_t)w * 4 * 16 * 64 + l;
+            const gdouble* bp = opaque(A.pf1b) + (size_t)w * 4 * 16 * 64 + l;
             // B fragments two k-steps ahead (rotating buffers, fully unrolled)
             auto ld4 = [&](double(&b)[4], int s) {
 #pragma unroll
@@ -622,107 +622,132 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
 }
 
 // ------------------------------------------------------------------ 4. train B
+// conv2 / conv1 gradients.  The input gradient runs in the Winograd domain (the backward of the
+// forward's F(2x2, 2x2)); the weight gradient stays direct, accumulated across the workgroup's
+// tiles in MFMA accumulators (a Winograd dU would need its nine transforms per tile on VALU):
+//   dM_xi = (A dY A^T)_xi       A = [[1,0],[1,1],[0,1]], dY = dZ2 of (b, o) -- its corners
+//                               xi = 0, 2, 6, 8 are dY itself                     (lane-local)
+//   dW2  += dY^T im2col(d)      [64 o x 64 (p, b)] x [64 x 256 (tap, c)]: 256 MFMAs per wave
+//   dV_xi = dM_xi U_xi^T        [16 b x 64 o] x [64 o x 64 c]: 9 x 16 MFMAs per wave
+//   dd    = B dV B^T            B = [[1,0,0],[-1,1,-1],[0,0,1]], then relu'(d) -> dZ1
+// 409 MFMAs per wave and tile instead of the all-direct form's 521.
+struct alignas(16) SmemB {
+    double x[TB * XS];
+    double d[9 * DPL];   // conv1 output d[q][b][c] of the tile (direct form)
+    double dm[9 * DPL];  // dM_xi[b][o]
+    SmallW sw;
+};
+
 __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
-    __shared__ Smem M;
+    __shared__ SmemB M;
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
-    d4 gw2[16];  // dW2 of wave w: o = 16w + 4r + lk, c = 16 cbc + lr, tap; index tap * 4 + cbc
+    d4 gw2[16];  // dW2 of wave w: o = 16w + 4r + lk, c = 16 cb + lr, tap; index tap * 4 + cb
 #pragma unroll
     for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gw1[4] = {0.0, 0.0, 0.0, 0.0}, gb1 = 0.0, gb2 = 0.0;
     CPHASE(-1);
-    stage_small(M.sw[0], A.on);
+    stage_small(M.sw, A.on);
     const int64_t ntiles = (A.batch + TB - 1) / TB;
-    // the tile's boards and its dZ2 rows (16 x 256 doubles, 16-byte loads); the next tile's are
-    // fetched while the current one runs
+    // the tile's boards (the next tile's fetched while the current one runs)
     uint4 sv = make_uint4(0u, 0u, 0u, 0u);
-    double2 zv[8];
     auto fetch = [&](int64_t tile) {
         sv = make_uint4(0u, 0u, 0u, 0u);
         const int64_t b = tile * TB + t;
         if (t < TB && tile < ntiles && b < A.batch) sv = A.R.s[A.idx[b]];
-        if (tile < ntiles) {
-            const double2* src = reinterpret_cast<const double2*>(A.dz2 + tile * TB * 256);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) zv[k] = src[t + NT * k];
-        }
     };
     fetch(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         __syncthreads();
         if (t < TB) put_row(M.x + t * XS, sv);
+        {  // dM = A dY A^T of the thread's four (b = (t >> 6) + 4k, o = t & 63) pairs; db2
+            const int o = t & 63;
+            double2 zv[4][2];  // dZ2 of the pairs: four doubles (p) each
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {  // element pair e = t + NT k: row e / 128, column 2 (e % 128)
-            const int e = t + NT * k;
-            *reinterpret_cast<double2*>(M.h2 + (e >> 7) * HS + 2 * (e & 127)) = zv[k];
+            for (int k = 0; k < 4; ++k) {
+                const double2* src = reinterpret_cast<const double2*>(
+                    A.dz2 + (tile * TB + (t >> 6) + 4 * k) * 256 + o * 4);
+                zv[k][0] = src[0];
+                zv[k][1] = src[1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const double y00 = zv[k][0].x, y01 = zv[k][0].y, y10 = zv[k][1].x, y11 = zv[k][1].y;
+                gb2 += ((y00 + y01) + y10) + y11;
+                const double m[9] = {y00, y00 + y01, y01, y00 + y10, ((y00 + y01) + y10) + y11,
+                                     y01 + y11, y10, y10 + y11, y11};
+                double* dst = M.dm + ((t >> 6) + 4 * k) * DSB + o;
+#pragma unroll
+                for (int x = 0; x < 9; ++x) dst[x * DPL] = m[x];
+            }
         }
         fetch(tile + gridDim.x);
         CPHASE(14);
-        conv1(M, M.sw[0]);
+        const uint64_t mask = conv1_mfma<false>(M.x, M.d, M.sw);
         __syncthreads();
         CPHASE(15);
-        // db2[o] (thread o < 64)
-        if (t < 64) {
-            double acc = 0.0;
-            for (int s = 0; s < TB; ++s)
-#pragma unroll
-                for (int p = 0; p < 4; ++p) acc += M.h2[s * HS + t * 4 + p];
-            gb2 += acc;
-        }
-        // dW2 += dZ2^T im2col(D): wave w -> rows o = 16w .., K = 64 rows (p, b)
+        // dW2 += dY^T im2col(d): wave w -> rows o = 16w .., K = 64 rows (p, b) in 16 k-steps;
+        // dY[b][o][p] is dM at the corner xi = 0, 2, 6, 8 of p = 0, 1, 2, 3
 #pragma unroll 2
         for (int s = 0; s < 16; ++s) {
             const int p = s >> 2, bq = 4 * (s & 3) + lk;
-            const double a = M.h2[bq * HS + (16 * w + lr) * 4 + p];
+            const int xc = (p >> 1) * 6 + (p & 1) * 2;
+            const double a = M.dm[xc * DPL + bq * DSB + 16 * w + lr];
 #pragma unroll
             for (int tap = 0; tap < 4; ++tap) {
                 const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
 #pragma unroll
-                for (int cbc = 0; cbc < 4; ++cbc)
-                    gw2[tap * 4 + cbc] = mfma(a, dr[16 * cbc], gw2[tap * 4 + cbc]);
+                for (int cb = 0; cb < 4; ++cb)
+                    gw2[tap * 4 + cb] = mfma(a, dr[16 * cb], gw2[tap * 4 + cb]);
             }
         }
         CPHASE(16);
-        // dD = col2im(dZ2 W2): wave w -> channels c = 16w .. 16w+15, one accumulator per
-        // conv1 position, K = 64 output channels
-        d4 dd[9];
+        // dV_xi: wave w -> channels c = 16w .., K = 64 o in 16 k-steps, nine chains; B two
+        // steps ahead
+        d4 dv[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) dd[q] = d4{0.0, 0.0, 0.0, 0.0};
-        const double* bp = opaque(A.p2b) + (size_t)w * 4 * 16 * 64 + l;
-        // B fragments two k-steps ahead (fully unrolled, rotating buffers)
-        double bt[3][4];
+        for (int x = 0; x < 9; ++x) dv[x] = d4{0.0, 0.0, 0.0, 0.0};
+        {
+            const gdouble* ub = opaque(A.p2b) + (size_t)w * 9 * 16 * 64 + l;  // UB [w][xi][s][l]
+            auto ld9 = [&](double(&b)[9], int s) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+                for (int x = 0; x < 9; ++x) b[x] = ub[(x * 16 + s) * 64];
+            };
+            double bb[3][9];
+            ld9(bb[0], 0);
+            ld9(bb[1], 1);
 #pragma unroll
-            for (int tap = 0; tap < 4; ++tap) bt[s][tap] = bp[(tap * 16 + s) * 64];
+            for (int s = 0; s < 16; ++s) {
+                if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
+                const double* ar = M.dm + lr * DSB + 4 * s + lk;
 #pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            if (s + 2 < 16) {
-#pragma unroll
-                for (int tap = 0; tap < 4; ++tap) bt[(s + 2) % 3][tap] = bp[(tap * 16 + s + 2) * 64];
+                for (int x = 0; x < 9; ++x) dv[x] = mfma(ar[x * DPL], bb[s % 3][x], dv[x]);
+                __builtin_amdgcn_sched_barrier(0);
             }
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const double a = M.h2[lr * HS + (4 * s + lk) * 4 + p];
-#pragma unroll
-                for (int tap = 0; tap < 4; ++tap) {
-                    const int q = pos_of(p, tap);
-                    dd[q] = mfma(a, bt[s % 3][tap], dd[q]);
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
         }
         CPHASE(17);
-        // relu'(conv1) mask -> dZ1; dW1[c][tap] += dZ1 * x, db1[c] += dZ1
+        // dd = B dV B^T, relu'(conv1) -> dZ1; dW1[c][tap] += dZ1 * x, db1[c] += dZ1
         {
-            const int c = 16 * w + lr;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int bq = 4 * r + lk;
-                const double* xr = M.x + bq * XS;
+                double u[9];  // B dV (along y)
+#pragma unroll
+                for (int x = 0; x < 3; ++x) {
+                    u[x] = dv[x][r];
+                    u[3 + x] = (dv[3 + x][r] - dv[x][r]) - dv[6 + x][r];
+                    u[6 + x] = dv[6 + x][r];
+                }
+                double dz[9];
+#pragma unroll
+                for (int y = 0; y < 3; ++y) {  // (B dV) B^T (along x)
+                    dz[3 * y] = u[3 * y];
+                    dz[3 * y + 1] = (u[3 * y + 1] - u[3 * y]) - u[3 * y + 2];
+                    dz[3 * y + 2] = u[3 * y + 2];
+                }
+                const double* xr = M.x + (4 * r + lk) * XS;
 #pragma unroll
                 for (int q = 0; q < 9; ++q) {
-                    const double z = M.d[q * DPL + bq * DSB + c] > 0.0 ? dd[q][r] : 0.0;
+                    const double z = (mask >> (9 * r + q)) & 1ull ? dz[q] : 0.0;
                     const int i0 = (q / 3) * 4 + (q % 3);
                     gw1[0] = fma(z, xr[i0], gw1[0]);
                     gw1[1] = fma(z, xr[i0 + 1], gw1[1]);
@@ -734,14 +759,16 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         }
         CPHASE(18);
     }
-    // combine the 4 lane groups of a channel in a fixed order (through LDS), then the slab:
-    // conv1.weight [64][1][2][2], conv1.bias, conv2.weight [64][64][2][2], conv2.bias
+    // combine in a fixed order through LDS: the 4 lane groups of a conv1 channel (dW1, db1) and
+    // the 4 threads of a conv2 channel (db2); then the slab: conv1.weight [64][1][2][2],
+    // conv1.bias, conv2.weight [64][64][2][2], conv2.bias
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
     __syncthreads();
-    double* red = M.d;  // [5][256] (x, d are dead)
+    double* red = M.d;  // [6][256] (x, d are dead)
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[k * 256 + t] = gw1[k];
     red[4 * 256 + t] = gb1;
+    red[5 * 256 + t] = gb2;
     __syncthreads();
     if (t < 64) {
         const int c = t, ww = c >> 4, cl = c & 15;
@@ -749,20 +776,21 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             const double* v = red + k * 256 + base;
-            const double s = ((v[0] + v[16]) + v[32]) + v[48];
-            if (k < 4) sl[P_W1 + c * 4 + k] = s;
-            else sl[P_B1 + c] = s;
+            const double sm = ((v[0] + v[16]) + v[32]) + v[48];
+            if (k < 4) sl[P_W1 + c * 4 + k] = sm;
+            else sl[P_B1 + c] = sm;
         }
-        sl[P_B2 + c] = gb2;
+        const double* v2 = red + 5 * 256 + c;  // threads c, c + 64, c + 128, c + 192
+        sl[P_B2 + c] = ((v2[0] + v2[64]) + v2[128]) + v2[192];
     }
 #pragma unroll
     for (int tap = 0; tap < 4; ++tap)
 #pragma unroll
-        for (int cbc = 0; cbc < 4; ++cbc)
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                sl[P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cbc + lr) * 4 + tap] =
-                    gw2[tap * 4 + cbc][r];
+                sl[P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4 + tap] =
+                    gw2[tap * 4 + cb][r];
     CPHASE(19);
 }
 
@@ -1050,7 +1078,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     A.on = T.on;
     A.pon = T.pon;
     A.pf1b = pk + O_F1B;
-    A.p2b = pk + O_P2B;
+    A.p2b = pk + O_UB;
     A.R = R;
     A.idx = idx_out;
     A.y = y_out;

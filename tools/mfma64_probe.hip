@@ -67,6 +67,24 @@ __global__ __launch_bounds__(256) void kmfma8(double* out, int iters) {
     for (int k = 0; k < 8; ++k) s += c[k][k & 3];
     out[blockIdx.x * 256 + l] = s;
 }
+// 8 chains, every MFMA with its own A and B registers (no reuse), operands fixed in registers
+__global__ __launch_bounds__(256) void kmfma_distinct(double* out, int iters) {
+    const int l = threadIdx.x;
+    double a[8], b[8];
+    for (int k = 0; k < 8; ++k) {
+        a[k] = 1.0 + (l + k) * 1e-9;
+        b[k] = 1.0 - (l * k) * 1e-9;
+    }
+    d4 c[8];
+    for (int k = 0; k < 8; ++k) c[k] = d4{0, 0, 0, 0};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[k], b[k], c[k], 0, 0, 0);
+    }
+    double s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k][k & 3];
+    out[blockIdx.x * 256 + l] = s;
+}
 __global__ __launch_bounds__(256) void kfma(double* out, int iters) {
     const int l = threadIdx.x;
     double a = 1.0 + l * 1e-9, b = 1.0 - l * 1e-9;
@@ -102,6 +120,15 @@ int main2() {
         (void)hipEventElapsedTime(&ms, e0, e1);
         const double fl2 = 1024.0 * 256 * it * 8 * 2.0;
         printf("v_fma_f64 8 chains: %.3f ms  %.1f TF\n", ms, fl2 / ms / 1e9);
+        {
+            (void)hipEventRecord(e0);
+            kmfma_distinct<<<1024, 256>>>(d, it / 2);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double fl3 = 1024.0 * 4 * (it / 2) * 8 * 2048.0;
+            printf("mfma f64 8 chains, distinct A/B per MFMA: %.3f ms  %.1f TF\n", ms, fl3 / ms / 1e9);
+        }
         for (int blocks = 1024; blocks <= 2048; blocks *= 2) {
             (void)hipEventRecord(e0);
             kmfma8<<<blocks, 256>>>(d, it / 2);

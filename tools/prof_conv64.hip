@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
     A.on = T.on;
     A.pon = T.pon;
     A.pf1b = pk + O_F1B;
-    A.p2b = pk + O_P2B;
+    A.p2b = pk + O_UB;
     A.R = R;
     A.idx = idx;
     A.y = y;
