@@ -808,7 +808,7 @@ __device__ __forceinline__ double adam64(double t, double lr, double b1, double 
 }
 
 constexpr int RW = 16;
-static_assert(MAX_WG <= RW * 16, "reduction covers at most RW*16 slabs");
+static_assert(MAX_WG % RW == 0 && SLAB % 2 == 0, "reduction: MAX_WG / RW slabs per wave, pairs");
 
 struct RedArgs {
     const double* slab;
@@ -825,34 +825,58 @@ struct RedArgs {
     int adam;
 };
 
+// Block = 128 positions (two per lane, 16-byte loads) x RW waves: wave w sums slabs w, w + RW,
+// ... with all of its loads in flight at once, then wave 0 adds the RW partials in wave order
+// and applies Adam.  (The summation order is fixed: bitwise run to run.)
 __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
-    __shared__ double part[RW][64];
+    __shared__ double2 part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pos = blockIdx.x * 64 + lane;
-    double r = 0.0;
-    if (pos <= P_N)
-        for (int g = wave; g < A.nslab; g += RW) r += A.slab[(int64_t)g * SLAB + pos];
+    const int pos = blockIdx.x * 128 + 2 * lane;  // positions pos, pos + 1 (SLAB is even)
+    double2 r = make_double2(0.0, 0.0);
+    if (pos <= P_N) {
+        double2 v[MAX_WG / RW];
+#pragma unroll
+        for (int k = 0; k < MAX_WG / RW; ++k) {
+            const int g = wave + RW * k;
+            v[k] = g < A.nslab ? *reinterpret_cast<const double2*>(A.slab + (int64_t)g * SLAB + pos)
+                               : make_double2(0.0, 0.0);
+        }
+#pragma unroll
+        for (int k = 0; k < MAX_WG / RW; ++k) {
+            r.x += v[k].x;
+            r.y += v[k].y;
+        }
+    }
     part[wave][lane] = r;
     __syncthreads();
-    if (wave == 0 && pos <= P_N) {
-        double sum = part[0][lane];
-        for (int k = 1; k < RW; ++k) sum += part[k][lane];
-        if (pos == P_N) {
-            if (A.loss) *A.loss = sum;
-        } else {
-            if (A.grad) A.grad[pos] = sum;
+    if (wave == 0) {
+        double2 sum = part[0][lane];
+        for (int k = 1; k < RW; ++k) {
+            sum.x += part[k][lane].x;
+            sum.y += part[k][lane].y;
+        }
+        const double sums[2] = {sum.x, sum.y};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ps = pos + h;
+            if (ps > P_N) continue;
+            if (ps == P_N) {
+                if (A.loss) *A.loss = sums[h];
+                continue;
+            }
+            if (A.grad) A.grad[ps] = sums[h];
             if (A.adam) {
                 const int base[8] = {P_W1, P_B1, P_W2, P_B2, P_F1, P_FB1, P_F2, P_FB2};
                 int k = 7;
-                while (pos < base[k]) --k;
+                while (ps < base[k]) --k;
                 const unsigned long long tt = *A.step_next;
-                double m = A.m[pos], v = A.v[pos];
-                const double np =
-                    adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sum, m, v, A.p[k][pos - base[k]]);
-                A.m[pos] = m;
-                A.v[pos] = v;
-                A.p[k][pos - base[k]] = np;
-                if (A.sync_every && tt % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
+                double m = A.m[ps], v = A.v[ps];
+                const double np = adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v,
+                                         A.p[k][ps - base[k]]);
+                A.m[ps] = m;
+                A.v[ps] = v;
+                A.p[k][ps - base[k]] = np;
+                if (A.sync_every && tt % A.sync_every == 0ull) A.tp[k][ps - base[k]] = np;
             }
         }
     }
@@ -1111,7 +1135,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     D.b2 = beta2;
     D.eps = eps;
     D.adam = adam ? 1 : 0;
-    hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 63) / 64), dim3(64 * RW), 0, st, D);
+    hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 127) / 128), dim3(64 * RW), 0, st, D);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "convnet_update_f64: %s", hipGetErrorString(e));

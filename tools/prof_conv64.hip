@@ -125,7 +125,7 @@ int main(int argc, char** argv) {
             case 2: hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, nullptr, A); break;
             case 3: hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, nullptr, A); break;
             default:
-                hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 63) / 64), dim3(64 * RW), 0,
+                hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 127) / 128), dim3(64 * RW), 0,
                                    nullptr, D);
         }
     };
