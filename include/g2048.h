@@ -425,6 +425,16 @@ G2048_API int g2048_convnet_forward_greedy_f64(const g2048_convnet_params_f64* p
                                                double* q_out_dev, double* workspace_dev,
                                                void* stream);
 
+/* g2048_adam_step_sync in float64: the Adam update of the float64 fused reductions (torch's Adam
+ * with its scalars in double) over n_tensors (<= 16) float64 parameter tensors, for a
+ * data-parallel float64 learner (gradient -> all-reduce -> this step). */
+G2048_API int g2048_adam_step_sync_f64(double* const* params_dev, const int64_t* numels,
+                                       int n_tensors, const double* grad_dev, double* exp_avg_dev,
+                                       double* exp_avg_sq_dev, const uint64_t* step_dev, double lr,
+                                       double beta1, double beta2, double eps,
+                                       double* const* target_params_dev, uint64_t sync_every,
+                                       void* stream);
+
 /* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
  * Best-first search from one board (exponents start[16], merge score start_score) until a
  * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion

@@ -47,6 +47,38 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][i - A.off[k]] = np;
 }
 
+// The float64 form (the reference's precision): g2048::adam64, the update the float64 fused
+// reductions apply, so a data-parallel float64 learner (gradient -> all-reduce -> this step)
+// moves the weights exactly as the single-process one on the same gradient.
+struct AdamArgs64 {
+    double* p[kMaxTensors];
+    double* tp[kMaxTensors];
+    unsigned long long sync_every;
+    int64_t off[kMaxTensors + 1];
+    int nt;
+    const double* g;
+    double* m;
+    double* v;
+    const unsigned long long* step;
+    double lr, b1, b2, eps;
+};
+
+__global__ __launch_bounds__(256) void k_adam64(AdamArgs64 A) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= A.off[A.nt]) return;
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < kMaxTensors; ++j) k += (j < A.nt && i >= A.off[j]) ? 1 : 0;
+    double* p = A.p[k] + (i - A.off[k]);
+    const unsigned long long t = *A.step;
+    double m = A.m[i], v = A.v[i];
+    const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, A.g[i], m, v, *p);
+    A.m[i] = m;
+    A.v[i] = v;
+    *p = np;
+    if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][i - A.off[k]] = np;
+}
+
 }  // namespace
 
 static int adam_launch(float* const* params, const int64_t* numels, int n_tensors,
@@ -100,4 +132,43 @@ extern "C" G2048_API int g2048_adam_step_sync(float* const* params, const int64_
                                               void* stream) {
     return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
                        beta2, eps, target_params, sync_every, stream);
+}
+
+extern "C" G2048_API int g2048_adam_step_sync_f64(double* const* params, const int64_t* numels,
+                                                  int n_tensors, const double* grad,
+                                                  double* exp_avg, double* exp_avg_sq,
+                                                  const uint64_t* step_dev, double lr,
+                                                  double beta1, double beta2, double eps,
+                                                  double* const* target_params,
+                                                  uint64_t sync_every, void* stream) {
+    if (!params || !numels || n_tensors <= 0 || n_tensors > kMaxTensors || !grad || !exp_avg ||
+        !exp_avg_sq || !step_dev)
+        return g2048_fail(G2048_EINVAL, "adam_step_f64: bad arguments (n_tensors <= %d)",
+                          kMaxTensors);
+    if (sync_every && !target_params)
+        return g2048_fail(G2048_EINVAL, "adam_step_f64: sync_every > 0 needs target_params");
+    AdamArgs64 A;
+    A.nt = n_tensors;
+    A.off[0] = 0;
+    for (int j = 0; j < kMaxTensors; ++j) {
+        A.p[j] = j < n_tensors ? params[j] : nullptr;
+        A.tp[j] = (sync_every && j < n_tensors) ? target_params[j] : nullptr;
+        if (j < n_tensors) A.off[j + 1] = A.off[j] + numels[j];
+    }
+    for (int j = n_tensors + 1; j <= kMaxTensors; ++j) A.off[j] = A.off[n_tensors];
+    A.sync_every = sync_every;
+    A.g = grad;
+    A.m = exp_avg;
+    A.v = exp_avg_sq;
+    A.step = reinterpret_cast<const unsigned long long*>(step_dev);
+    A.lr = lr;
+    A.b1 = beta1;
+    A.b2 = beta2;
+    A.eps = eps;
+    const int64_t n = A.off[n_tensors];
+    hipLaunchKernelGGL(k_adam64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), A);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "adam_step_f64: %s", hipGetErrorString(e));
 }

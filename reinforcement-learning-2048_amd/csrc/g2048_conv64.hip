@@ -794,19 +794,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     CPHASE(19);
 }
 
-// ------------------------------------------------------------------ 5. reduce + Adam
-// torch.optim.Adam (single tensor, amsgrad off, no weight decay) on one float64 element.
-__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
-                                         double g, double& m, double& v, double p) {
-#pragma clang fp contract(off)
-    const double step_size = lr / (1.0 - pow(b1, t));
-    const double bc2_sqrt = sqrt(1.0 - pow(b2, t));
-    m = m + (1.0 - b1) * (g - m);
-    v = v * b2 + (1.0 - b2) * g * g;
-    const double denom = sqrt(v) / bc2_sqrt + eps;
-    return p + (-step_size) * (m / denom);
-}
-
 constexpr int RW = 16;
 static_assert(MAX_WG % RW == 0 && SLAB % 2 == 0, "reduction: MAX_WG / RW slabs per wave, pairs");
 
@@ -871,7 +858,7 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
                 while (ps < base[k]) --k;
                 const unsigned long long tt = *A.step_next;
                 double m = A.m[ps], v = A.v[ps];
-                const double np = adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v,
+                const double np = g2048::adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v,
                                          A.p[k][ps - base[k]]);
                 A.m[ps] = m;
                 A.v[ps] = v;

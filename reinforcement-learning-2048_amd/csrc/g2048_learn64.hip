@@ -253,20 +253,6 @@ __global__ __launch_bounds__(NT) void k_dense64_update_f64(UpdArgs64 A) {
     if (t == 0) sl[P_N] = g_loss;
 }
 
-// torch.optim.Adam (single tensor, amsgrad off, no weight decay) on one float64 element, the
-// scalars as torch forms them in double: m.lerp_(g, 1 - b1); v.mul_(b2).addcmul_(g, g, 1 - b2);
-// denom = v.sqrt() / sqrt(1 - b2^t) + eps; p.addcdiv_(m, denom, -lr / (1 - b1^t)).
-__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
-                                         double g, double& m, double& v, double p) {
-#pragma clang fp contract(off)
-    const double step_size = lr / (1.0 - pow(b1, t));
-    const double bc2_sqrt = sqrt(1.0 - pow(b2, t));
-    m = m + (1.0 - b1) * (g - m);
-    v = v * b2 + (1.0 - b2) * g * g;
-    const double denom = sqrt(v) / bc2_sqrt + eps;
-    return p + (-step_size) * (m / denom);
-}
-
 constexpr int RW = 16;  // waves per reduction block
 static_assert(MAX_SLABS <= RW * 16, "reduction covers at most RW*16 slabs");
 
@@ -309,7 +295,7 @@ __global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
                 const int base[4] = {P_W1, P_B1, P_W2, P_B2};
                 const unsigned long long t = *A.step_next;
                 double m = A.m[pos], v = A.v[pos];
-                const double np = adam64((double)t, A.lr, A.b1, A.b2, A.eps, sum, m, v,
+                const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, sum, m, v,
                                          A.p[k][pos - base[k]]);
                 A.m[pos] = m;
                 A.v[pos] = v;

@@ -67,11 +67,10 @@ class DQNLearner:
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
         self.kind = qnet.kind_of(self.model) if self.loss_fn is None else None
         # float64 (the reference's precision): the dense 16-64-4 and conv nets have fused
-        # updates too (g2048_dense64_update_f64, g2048_convnet_update_f64); single process --
-        # with world > 1 they run the torch path
+        # updates too (g2048_dense64_update_f64, g2048_convnet_update_f64); with world > 1 the
+        # gradient is all-reduced and g2048_adam_step_sync_f64 applies Adam
         k64 = qnet.kind64_of(self.model)
-        self.f64 = (self.kind is None and self.loss_fn is None and self.world == 1
-                    and k64 is not None)
+        self.f64 = self.kind is None and self.loss_fn is None and k64 is not None
         if self.f64:
             self.kind = k64
         self.fused = self.kind is not None

@@ -270,13 +270,27 @@ class Adam64:
         self.exp_avg_sq = torch.zeros(n, dtype=torch.float64, device=dev)
         self.sync_every = 0
 
+        self._ptrs = (C.c_void_p * len(self.params))(*[p.data_ptr() for p in self.params])
+        self._numel = (C.c_int64 * len(self.params))(*[p.numel() for p in self.params])
+        self._tptrs = None
+
     def attach_target(self, target_params, sync_every: int) -> None:
         self._target = list(target_params)
+        self._tptrs = (C.c_void_p * len(self._target))(*[t.data_ptr() for t in self._target])
         self.sync_every = int(sync_every)
 
     def reset_state(self):
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
+
+    def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor):
+        """Adam over the flat float64 gradient (the data-parallel path: after the all-reduce);
+        step_counter: device u64 holding t; the target sync as attached."""
+        N.check(N.load().g2048_adam_step_sync_f64(
+            self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
+            N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
+            self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0,
+            N.stream_of(grad_flat.device)), "g2048_adam_step_sync_f64")
 
 
 class Dense64Update64:

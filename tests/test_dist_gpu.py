@@ -21,7 +21,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, net, out_dir):
+def _worker(rank, world, port, net, out_dir, dtype="fp32"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,9 +36,10 @@ def _worker(rank, world, port, net, out_dir):
     env = g2048.VecEnv2048(n, seed=7, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(8 * n, device=dev)
     env.rollout(8, replay=rb)
-    L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=1024, target_sync_every=2,
+    L = DQNLearner(rb, net=net, dtype=torch.float64 if dtype == "fp64" else torch.float32,
+                   batch_size=1024, target_sync_every=2,
                    seed=100 + rank)  # different seeds: the broadcast must equalise the init
-    assert L.world == world and L.fused
+    assert L.world == world and L.fused and L.f64 == (dtype == "fp64")
     init = torch.cat([p.detach().reshape(-1).clone() for p in L.model.parameters()])
     for _ in range(3):
         L.update()
@@ -59,11 +60,14 @@ def _worker(rank, world, port, net, out_dir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("net", ["conv", "dense64"])
-def test_two_ranks_stay_in_lockstep(tmp_path, net):
+def test_two_ranks_stay_in_lockstep(tmp_path, net, dtype):
+    """fp64: the fused float64 update writes the gradient, the flat bucket is all-reduced and
+    g2048_adam_step_sync_f64 applies Adam (+ target sync)."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
-    mp.spawn(_worker, args=(2, _free_port(), net, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), net, str(tmp_path), dtype), nprocs=2, join=True)
     res = torch.load(os.path.join(tmp_path, "res.pt"), weights_only=True)
     assert res["finite"] and res["moved"]
     assert res["diff_loss"], "ranks should see different minibatches"

@@ -266,3 +266,35 @@ def test_fused_f64_equals_torch_path(G, net):
             for p, q in zip(list(b.model.parameters()) + list(b.target.parameters()),
                             list(a.model.parameters()) + list(a.target.parameters())):
                 p.copy_(q)
+
+
+@pytest.mark.parametrize("net", ["dense64", "conv"])
+def test_fused_f64_adam_step_equals_folded(G, net):
+    """The data-parallel float64 split (fused gradient -> grad_out, then g2048_adam_step_sync_f64)
+    moves online and target weights bitwise like the single-process update with Adam folded into
+    the reduction, over three updates with a target sync every 2."""
+    from g2048 import qnet
+    from g2048.learner import DQNLearner
+
+    n = 2048
+    env = G.VecEnv2048(n, seed=21, device=DEV)
+    rb = G.ReplayBuffer(8 * n, device=DEV)
+    env.rollout(8, replay=rb)
+    a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=700, target_sync_every=2, seed=5,
+                   graph=False)
+    b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=700, target_sync_every=2, seed=5,
+                   graph=False)
+    assert a.f64 and b.f64
+    b.model.load_state_dict(a.model.state_dict())
+    b.target.load_state_dict(a.target.state_dict())
+    b._upd.adam = None  # b: gradient only; Adam64.step applies the update (the DP path)
+    assert isinstance(b._adam, qnet.Adam64)
+    for _ in range(3):
+        a.update()
+        b._compute_grads()
+        b._adam.step(b.grad_flat, b.step_dev)
+        torch.cuda.synchronize()
+        assert torch.equal(a.grad_flat, b.grad_flat)
+        for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
+                        list(b.model.parameters()) + list(b.target.parameters())):
+            assert torch.equal(p, q)
