@@ -111,16 +111,17 @@ __device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint
     const uint32_t o1 = bsel(AB, c1, b1);
     const uint32_t o2 = bsel(AB, l3 & ~CD, bsel(BC, l3, c1));
     const uint32_t o3 = l3 & ~(AB | BC | CD);
-    // 3) score = sum of 2^e over the merged tiles: 12 candidate bytes, zero bytes give 2^0 = 1
-    const uint32_t e0 = o0 & AB, e1 = b1 & BC, e2 = c1 & CD;
+    // 3) score = sum of 2^e over the merged tiles.  A line merges a+b or b+c, never both (bc
+    //    excludes ab), so their merged bytes share one word: 8 candidate bytes, and a zero byte
+    //    (no merge) gives 2^0 = 1, taken off at the end.
+    const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD;
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        s += 1u << ((e0 >> (8 * k)) & 31u);
-        s += 1u << ((e1 >> (8 * k)) & 31u);
+        s += 1u << ((e01 >> (8 * k)) & 31u);
         s += 1u << ((e2 >> (8 * k)) & 31u);
     }
-    s -= 12u - (uint32_t)(__popc(ab) + __popc(bc) + __popc(cd));
+    s -= 8u - (uint32_t)(__popc(ab | bc) + __popc(cd));
     l0 = o0;
     l1 = o1;
     l2 = o2;
