@@ -435,6 +435,16 @@ G2048_API int g2048_adam_step_sync_f64(double* const* params_dev, const int64_t*
                                        double* const* target_params_dev, uint64_t sync_every,
                                        void* stream);
 
+/* g2048_env_step_egreedy_dense64 for a float64 dense 16-64-4 net: Q(s) computed in the step
+ * kernel in double, the step as g2048_env_step_egreedy with f64 Q (q_out: f64[n][4] or NULL). */
+G2048_API int g2048_env_step_egreedy_dense64_f64(g2048_env* env,
+                                                 const g2048_dense64_params_f64* params,
+                                                 const double* eps_dev, double eps,
+                                                 double eps_decay_episodes, double eps_min,
+                                                 int32_t* reward_dev, uint8_t* done_dev,
+                                                 uint8_t* action_out_dev, g2048_replay* rb,
+                                                 double* q_out_dev, void* stream);
+
 /* ---- A* replay pre-fill (src/state_space_search.py:46-131), host code -------------------
  * Best-first search from one board (exponents start[16], merge score start_score) until a
  * popped board holds a tile of exponent goal_exp: priority -score // 2, ties in insertion

@@ -51,7 +51,8 @@ enum : int {
     MODE_EG_F32 = 2,
     MODE_EG_F64 = 3,
     MODE_INJECT = 4,
-    MODE_EG_REG = 5  // eps-greedy over f32 Q computed in-kernel (passed in registers)
+    MODE_EG_REG = 5,   // eps-greedy over f32 Q computed in-kernel (passed in registers)
+    MODE_EG_REG64 = 6  // eps-greedy over f64 Q computed in-kernel (passed in registers)
 };
 
 struct ReplayDev {
@@ -151,8 +152,10 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
                                          Board& b, uint2& m, double eps, double& qs,
                                          int32_t& rew_out, uint32_t& done_out, uint32_t& legal_out,
                                          uint32_t& act_out, uint4& ep,
-                                         float4 qreg = float4{0, 0, 0, 0}) {
-    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG;
+                                         float4 qreg = float4{0, 0, 0, 0},
+                                         double4 qreg64 = double4{0, 0, 0, 0}) {
+    constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64 || MODE == MODE_EG_REG ||
+                             MODE == MODE_EG_REG64;
     const Board s_old = b;
     uint32_t legal = 0u, act, r = 0u;
     bool done;
@@ -192,6 +195,11 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
                 act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
                             : greedy_compat(q.x, q.y, q.z, q.w, legal);
                 qs += (double)qmax4_torch(q.x, q.y, q.z, q.w);  // torch.max(Q) (:29)
+            } else if constexpr (MODE == MODE_EG_REG64) {
+                const double4 q = qreg64;
+                act = fixed ? greedy_fixed(q.x, q.y, q.z, q.w, legal)
+                            : greedy_compat(q.x, q.y, q.z, q.w, legal);
+                qs += qmax4_torch(q.x, q.y, q.z, q.w);
             } else {
                 const double2 q01 = reinterpret_cast<const double2*>(A.q)[2 * i];
                 const double2 q23 = reinterpret_cast<const double2*>(A.q)[2 * i + 1];
@@ -376,6 +384,88 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     double qs = A.qsum ? A.qsum[i] : 0.0;
     step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
                           act, ep, q);
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (lane == 0) A.clock[blockIdx.x] = t + 1u;  // wave 1 read it before the barrier
+    if (A.qsum) A.qsum[i] = qs;
+    if (A.reward) A.reward[i] = rew;
+    if (A.done) A.done[i] = (uint8_t)done;
+    if (A.action_out) A.action_out[i] = (uint8_t)act;
+    if (A.rb.rows && i == 0) bump_count(A, t + 1u);
+}
+
+// The float64 form (the reference's precision, src/configs/double_dqn_dense.py:15): the same
+// two-wave split and selection as k_step_dense64_split, the MLP in double (SGPR weight operands)
+// and Q (double) handed to the step in registers; Q = e + o with wave 0's chain holding b2.
+template <bool kFull>
+__global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const double* __restrict__ w1,
+                                                              const double* __restrict__ b1,
+                                                              const double* __restrict__ w2,
+                                                              const double* __restrict__ b2,
+                                                              double* q_out) {
+    __shared__ double4 so[64];
+    const int lane = threadIdx.x & 63;
+    const int half = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+    const bool live = kFull || i < A.n;
+    Board b{0u, 0u, 0u, 0u};
+    uint2 m = make_uint2(0u, 0u);
+    uint4 ep = make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t t = load_clock(A.clock, (int64_t)blockIdx.x * 64);
+    if (live) {
+        b = load_board(A.board[i]);
+        if (half == 0 || !q_out) {
+            m = A.meta[i];
+            ep = A.ep[i];
+        }
+    }
+    bool any_greedy = true;  // the model runs on the greedy branch only (src/dqn_lib.py:20-24)
+    if (!q_out) {
+        bool greedy = false;
+        if (live) {
+            const uint4 u = draw(A.seed_lo, A.seed_hi, A.board_offset + (uint64_t)i, DOMAIN_STEP, t);
+            greedy = !explores(u.y, step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, ep.x));
+        }
+        any_greedy = __ballot(greedy) != 0ull;
+    }
+    double x[16];
+    const uint32_t rw[4] = {b.r0, b.r1, b.r2, b.r3};
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x[4 * r + c] = (double)((rw[r] >> (8 * c)) & 0xFFu);
+    double acc[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) acc[a] = half == 0 ? b2[a] : 0.0;
+#pragma unroll 2
+    for (int jj = 0; jj < 32 && any_greedy; ++jj) {
+        const int j = 2 * jj + half;
+        double pa = b1[j], pb = 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) {
+            pa = fma(w1[j * 16 + k], x[k], pa);
+            pb = fma(w1[j * 16 + k + 1], x[k + 1], pb);
+        }
+        const double pre = pa + pb;
+        const double h = pre > 0.0 ? pre : 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a] = fma(w2[a * 64 + j], h, acc[a]);
+    }
+    if (half == 1) so[lane] = double4{acc[0], acc[1], acc[2], acc[3]};
+    __syncthreads();
+    if (half == 1 || !live) return;
+    const double4 o = so[lane];
+    const double4 q = double4{acc[0] + o.x, acc[1] + o.y, acc[2] + o.z, acc[3] + o.w};
+    const double eps = step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, ep.x);
+    if (q_out) {
+        reinterpret_cast<double2*>(q_out)[2 * i] = make_double2(q.x, q.y);
+        reinterpret_cast<double2*>(q_out)[2 * i + 1] = make_double2(q.z, q.w);
+    }
+    int32_t rew;
+    uint32_t done, legal, act;
+    double qs = A.qsum ? A.qsum[i] : 0.0;
+    step_one<MODE_EG_REG64>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done,
+                            legal, act, ep, float4{0, 0, 0, 0}, q);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
     if (lane == 0) A.clock[blockIdx.x] = t + 1u;  // wave 1 read it before the barrier
@@ -1005,6 +1095,38 @@ int g2048_env_step_egreedy_dense64(g2048_env* e, const g2048_dense64_params* p,
                            p->b1, p->w2, p->b2, q_out);
     else
         hipLaunchKernelGGL((k_step_dense64_split<false>), dim3(grid), dim3(128), 0, st, A, p->w1,
+                           p->b1, p->w2, p->b2, q_out);
+    G_HIP(hipGetLastError());
+    return G2048_OK;
+}
+
+int g2048_env_step_egreedy_dense64_f64(g2048_env* e, const g2048_dense64_params_f64* p,
+                                       const double* eps_dev, double eps,
+                                       double eps_decay_episodes, double eps_min, int32_t* reward,
+                                       uint8_t* done, uint8_t* action_out, g2048_replay* rb,
+                                       double* q_out, void* stream) {
+    if (!e || !p || !p->w1 || !p->b1 || !p->w2 || !p->b2)
+        return fail(G2048_EINVAL, "env_step_egreedy_dense64_f64: NULL env or parameter");
+    if (q_out && !aligned16(q_out))
+        return fail(G2048_EINVAL, "env_step_egreedy_dense64_f64: q_out must be 16-byte aligned");
+    StepArgs A;
+    int rc = make_args(e, rb, A);
+    if (rc) return rc;
+    A.eps_dev = eps_dev;
+    A.eps = eps;
+    A.eps_decay = eps_decay_episodes > 0.0 ? eps_decay_episodes : 0.0;
+    A.eps_min = eps_min;
+    A.reward = reward;
+    A.done = done;
+    A.action_out = action_out;
+    DeviceGuard g(e->device);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)((e->n + 63) / 64);
+    if (e->n % 64 == 0)
+        hipLaunchKernelGGL((k_step_dense64_split64<true>), dim3(grid), dim3(128), 0, st, A, p->w1,
+                           p->b1, p->w2, p->b2, q_out);
+    else
+        hipLaunchKernelGGL((k_step_dense64_split64<false>), dim3(grid), dim3(128), 0, st, A, p->w1,
                            p->b1, p->w2, p->b2, q_out);
     G_HIP(hipGetLastError());
     return G2048_OK;

@@ -44,6 +44,8 @@ SIGNATURES = {
     "g2048_env_legal_mask": (_int, [_vp, _vp, _vp]),
     "g2048_env_step_egreedy_dense64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp, _vp,
                                               _vp, _vp]),
+    "g2048_env_step_egreedy_dense64_f64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp, _vp,
+                                              _vp, _vp]),
     "g2048_replay_create": (_int, [_pp, _i64, _int, _vp]),
     "g2048_replay_wrap": (_int, [_pp, _i64, _int, _vp, _vp, _vp, _vp, _vp, _vp]),
     "g2048_replay_destroy": (None, [_vp]),

@@ -242,21 +242,25 @@ class VecEnv2048:
         return None, float(epsilon), 0.0, 0.0
 
     def step_egreedy_dense64(self, params, epsilon=0.0, replay: "ReplayBuffer | None" = None,
-                             reward=None, done=None, action=None, eps_schedule=None, q_out=None):
+                             reward=None, done=None, action=None, eps_schedule=None, q_out=None,
+                             f64: bool = False):
         """play_one_step for every board with the dense 16-64-4 Q-net computed INSIDE the step
-        kernel (g2048_env_step_egreedy_dense64): params = qnet.net_params(model) of an fp32
-        dense64 net.  Same epsilon forms as step_egreedy.  Returns (action, reward, done)."""
+        kernel (g2048_env_step_egreedy_dense64, or _f64 with f64=True): params = the parameter
+        struct of an fp32 (qnet.net_params) or float64 dense64 net.  Same epsilon forms as
+        step_egreedy.  Returns (action, reward, done)."""
         eps_ptr, eps_val, dec, mn = self.eps_args(epsilon, eps_schedule)
-        if q_out is not None and (q_out.shape != (self.n, 4) or q_out.dtype != torch.float32
+        qdt = torch.float64 if f64 else torch.float32
+        if q_out is not None and (q_out.shape != (self.n, 4) or q_out.dtype != qdt
                                   or not q_out.is_contiguous()):
-            raise ValueError(f"q_out must be a contiguous float32 [{self.n}, 4] tensor")
+            raise ValueError(f"q_out must be a contiguous {qdt} [{self.n}, 4] tensor")
         reward = self._out(reward, torch.int32)
         done = self._out(done, torch.uint8)
         action = self._out(action, torch.uint8)
-        N.check(N.load().g2048_env_step_egreedy_dense64(
+        name = "g2048_env_step_egreedy_dense64_f64" if f64 else "g2048_env_step_egreedy_dense64"
+        N.check(getattr(N.load(), name)(
             self._h, C.byref(params), eps_ptr, eps_val, dec, mn, N.ptr(reward), N.ptr(done),
             N.ptr(action), replay.handle if replay is not None else None, N.ptr(q_out),
-            self._stream()), "g2048_env_step_egreedy_dense64")
+            self._stream()), name)
         return action, reward, done
 
     def step_inject(self, actions, spawn_idx, spawn_exp):

@@ -347,10 +347,11 @@ class Trainer:
     def _rollout_step(self) -> None:
         """Device work of play_one_step for all boards (stream-ordered, capturable)."""
         sched = (self.eps_decay, self.min_eps)
-        if self.learner.kind == "dense64" and not self.learner.f64:  # Q inside the step kernel
-            self.env.step_egreedy_dense64(self.learner._p_on, replay=self.replay,
+        L = self.learner
+        if L.kind == "dense64":  # Q inside the step kernel (fp32 or float64)
+            self.env.step_egreedy_dense64(L._upd.on if L.f64 else L._p_on, replay=self.replay,
                                           reward=self._reward, done=self._done,
-                                          action=self._action, eps_schedule=sched)
+                                          action=self._action, eps_schedule=sched, f64=L.f64)
         else:
             if self._q is not None and self.learner._fwd64 is not None:  # greedy branch only
                 q = self.learner._fwd64.greedy(self.env, eps_schedule=sched, out=self._q)
@@ -367,7 +368,7 @@ class Trainer:
         outside the capture: hipBLASLt sets up a GEMM shape on its first call, which a stream
         under capture does not permit.  Pure: nothing is stepped."""
         L = self.learner
-        if L.f64 and L._fwd64 is None:
+        if L.f64 and L._fwd64 is None and L.kind != "dense64":
             side = torch.cuda.Stream(self.env.device)
             side.wait_stream(torch.cuda.current_stream(self.env.device))
             with torch.cuda.stream(side):

@@ -595,3 +595,39 @@ def test_fused_dense64_step_skips_explorers(g2048, mode):
     for f in g0:
         assert torch.equal(g0[f], g1[f]), f
     assert torch.equal(logs[0].qsum, logs[1].qsum)
+
+
+def test_fused_dense64_step_f64(g2048):
+    """g2048_env_step_egreedy_dense64_f64: the in-kernel float64 Q equals the torch float64 net to
+    1e-12 relative, and stepping on it equals g2048_env_step_egreedy fed the same Q, bit for bit
+    (actions, boards, rewards, replay, episode q-sums)."""
+    from g2048 import qnet
+    from g2048.nets import det_init, make_net
+
+    n = 4096 + 77
+    m = det_init(make_net("dense64", torch.float64, DEV), 0.7)
+    p = qnet.Dense64Update64(m, m, 64).on  # the float64 parameter struct
+    envs, rbs, logs = [], [], []
+    for _ in range(2):
+        e = g2048.VecEnv2048(n, seed=19, device=DEV)
+        rbs.append(g2048.ReplayBuffer(8 * n, device=DEV))
+        logs.append(e.attach_episode_log(16))
+        e.rollout(30)
+        envs.append(e)
+    qf = torch.empty((n, 4), dtype=torch.float64, device=DEV)
+    for t in range(40):
+        with torch.no_grad():
+            ref = m(envs[1].encode(torch.float64, conv=False)).reshape(n, 4)
+        a0, r0, d0 = envs[0].step_egreedy_dense64(p, 0.3, replay=rbs[0], q_out=qf, f64=True,
+                                                  eps_schedule=(30.0, 0.05))
+        torch.cuda.synchronize()
+        torch.testing.assert_close(qf, ref, rtol=1e-12, atol=1e-12 * float(ref.abs().max()))
+        a1, r1, d1 = envs[1].step_egreedy(qf.clone(), 0.3, replay=rbs[1],
+                                          eps_schedule=(30.0, 0.05))
+        torch.cuda.synchronize()
+        assert torch.equal(a0, a1) and torch.equal(r0, r1) and torch.equal(d0, d1), t
+    for name in ("board", "meta", "ep", "clock"):
+        assert torch.equal(getattr(envs[0], name), getattr(envs[1], name)), name
+    for name in ("s", "s2", "a", "r", "d", "count"):
+        assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name
+    assert torch.equal(logs[0].qsum, logs[1].qsum)

@@ -562,9 +562,11 @@ def test_conv_forward_greedy_f64_rows(G, n, form):
     assert torch.equal(envs[0].board, envs[1].board)
 
 
-def test_f64_conv_trainer_graphed_equals_eager(G):
-    """The float64 conv training loop (fused greedy forward + eps-greedy step + fused f64 update)
-    replayed from one hipGraph per iteration equals the eager loop bitwise."""
+@pytest.mark.parametrize("net", ["conv", "dense64"])
+def test_f64_trainer_graphed_equals_eager(G, net):
+    """The float64 training loops (conv: fused greedy forward + eps-greedy step; dense-64: Q in
+    the step kernel; both + the fused f64 update) replayed from one hipGraph per iteration equal
+    the eager loops bitwise."""
     from g2048.learner import DQNLearner, Trainer
 
     outs = []
@@ -572,7 +574,7 @@ def test_f64_conv_trainer_graphed_equals_eager(G):
         n = 2048
         env = G.VecEnv2048(n, device=DEV, seed=77)
         rb = G.ReplayBuffer(8 * n, device=DEV)
-        L = DQNLearner(rb, net="conv", dtype=torch.float64, batch_size=512, seed=4,
+        L = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=512, seed=4,
                        target_sync_every=3)
         T = Trainer(env, rb, L, updates_per_step=1, min_fill=0, eps_decay_episodes=3,
                     graph=graph)
