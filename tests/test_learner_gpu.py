@@ -226,8 +226,9 @@ def test_fused_f64_matches_reference(G, golden_dir, net):
     np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
 
 
+@pytest.mark.parametrize("double_dqn", [True, False])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
-def test_fused_f64_equals_torch_path(G, net):
+def test_fused_f64_equals_torch_path(G, net, double_dqn):
     """Three fused float64 updates (Philox sampler, Adam, target sync every 2) against the torch
     float64 learner on the same rows: losses and gradients to 1e-9 relative; weights to 1e-6
     absolute (Adam divides by |g| + eps, so a parameter whose summed gradient nearly cancels
@@ -240,11 +241,12 @@ def test_fused_f64_equals_torch_path(G, net):
     rb = G.ReplayBuffer(16 * n, device=DEV)
     env.rollout(16, replay=rb)
     a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=1000, target_sync_every=2,
-                   seed=9)
+                   seed=9, use_double_dqn=double_dqn)
     assert a.fused and a.f64
     rows = torch.zeros(1000, dtype=torch.int64, device=DEV)  # (captured by b's graphs)
     b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=1000, target_sync_every=2,
-                   seed=9, loss_fn=torch.nn.L1Loss(reduction="sum"))  # any torch-path learner
+                   seed=9, loss_fn=torch.nn.L1Loss(reduction="sum"),  # any torch-path learner
+                   use_double_dqn=double_dqn)
     b.loss_fn = None  # ... run with the MSE(sum) loss, fed the fused learner's rows
     b.sampler = lambda B, r: rows
     assert not b.fused
