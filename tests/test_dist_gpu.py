@@ -74,7 +74,7 @@ def test_two_ranks_stay_in_lockstep(tmp_path, net, dtype):
     assert res["same"], "replicas diverged"
 
 
-def _trainer_worker(rank, world, port, net, out_dir):
+def _trainer_worker(rank, world, port, net, out_dir, dtype="fp32"):
     """The graphed data-parallel training loop (graph A = fused step + gradient, RCCL/gloo
     all-reduce, graph B = Adam) against the eager loop: same boards, rings, weights, bitwise."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -92,8 +92,8 @@ def _trainer_worker(rank, world, port, net, out_dir):
     for graph in (True, False):
         env = g2048.VecEnv2048(n, seed=11, device=dev, board_offset=rank * n)
         rb = g2048.ReplayBuffer(16 * n, device=dev)
-        L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=512, target_sync_every=3,
-                       seed=5, graph=graph)
+        L = DQNLearner(rb, net=net, dtype=torch.float64 if dtype == "fp64" else torch.float32,
+                       batch_size=512, target_sync_every=3, seed=5, graph=graph)
         T = Trainer(env, rb, L, updates_per_step=1, min_fill=0, graph=graph,
                     eps_decay_episodes=20.0)
         T.prefill(4)
@@ -112,11 +112,13 @@ def _trainer_worker(rank, world, port, net, out_dir):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
 @pytest.mark.parametrize("net", ["conv", "dense64"])
-def test_graphed_dp_loop_equals_eager(tmp_path, net):
+def test_graphed_dp_loop_equals_eager(tmp_path, net, dtype):
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
-    mp.spawn(_trainer_worker, args=(2, _free_port(), net, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_trainer_worker, args=(2, _free_port(), net, str(tmp_path), dtype), nprocs=2,
+             join=True)
     res = torch.load(os.path.join(tmp_path, "res.pt"), weights_only=True)
     assert res["same"], "graphed DP loop differs from the eager DP loop"
 
@@ -132,7 +134,7 @@ def test_bench_two_ranks():
     env = dict(os.environ, G2048_BENCH_BACKEND="gloo")
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
                           "--steps", "20", "--warmup", "5", "--step-steps", "200",
-                          "--train", "dense64", "--train-dtypes", "fp32", "--train-updates", "20",
+                          "--train", "dense64", "--train-dtypes", "fp32,fp64", "--train-updates", "20",
                           "--no-cpu-baseline"], capture_output=True, text=True, env=env,
                          timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -141,3 +143,4 @@ def test_bench_two_ranks():
     assert line["config"]["global_boards"] == 2 * 65536
     assert line["value"] > 0 and line["step_kernel"]["env_steps_per_s"] > 0
     assert line["learner"]["dense64.fp32"]["graphed_loop"] is True
+    assert line["learner"]["dense64.fp64"]["path"] == "fused HIP kernels"
