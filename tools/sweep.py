@@ -13,7 +13,9 @@ import torch  # noqa: E402
 
 import g2048  # noqa: E402
 
-STEP_BYTES, ROLLOUT_BYTES = 70, 38
+# algorithmic bytes per env step: one launch per step in random mode 37 B (54 B with
+# the meta / legal bookkeeping the kernel also moves); the rollout's replay append 38 B
+STEP_BYTES, STEP_BYTES_BOOK, ROLLOUT_BYTES = 37, 54, 38
 
 
 def graph_of(fn, k):
@@ -52,15 +54,16 @@ def main():
         g = graph_of(lambda: env.step(None, reward=r, done=d, legal=lg), K)
         t = timed(g.replay, 4) / K
         row = {"boards": n, "step_us": t * 1e6, "steps_per_s": n / t,
-               "step_GBs": STEP_BYTES * n / t / 1e9}
-        if n >= (1 << 20):  # a plain device copy of the board + meta bytes (read + write 64 B)
-            src = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+               "step_GBs": STEP_BYTES * n / t / 1e9,
+               "step_GBs_with_bookkeeping": STEP_BYTES_BOOK * n / t / 1e9}
+        if n >= (1 << 20):  # a plain device copy of the board + meta bytes (read + write 48 B)
+            src = torch.empty((n, 24), dtype=torch.uint8, device="cuda:0")
             dst = torch.empty_like(src)
             tc = timed(lambda: dst.copy_(src), 10)
-            row["copy_GBs"] = 64 * n / tc / 1e9
+            row["copy_GBs"] = 48 * n / tc / 1e9
             del src, dst
         if n <= (1 << 22):
-            kk = 16
+            kk = 64 if n <= 65536 else 16
             rb = g2048.ReplayBuffer(n * kk, device="cuda:0")
             tr = timed(lambda: env.rollout(kk, replay=rb), 3)
             row.update(rollout_k=kk, rollout_step_us=tr / kk * 1e6,
