@@ -300,3 +300,35 @@ def test_fused_f64_adam_step_equals_folded(G, net):
         for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
                         list(b.model.parameters()) + list(b.target.parameters())):
             assert torch.equal(p, q)
+
+
+@pytest.mark.parametrize("net", ["dense64", "conv"])
+def test_fused_f32_matches_reference(G, golden_dir, net):
+    """The fp32 fast path (the fused kernels the bench times as learner.<net>.fp32) on the
+    reference train_step fixture's minibatch and weights: the loss within 2e-5 relative of the
+    reference's float64 loss, y within 1e-5, and every gradient tensor within 1e-3 relative
+    (L2) of the fixture's float64 gradient (fp32 accumulation over 512 rows)."""
+    from g2048.learner import DQNLearner
+    from g2048.nets import det_init, make_net
+
+    g = fixture(golden_dir, net)
+    rb = loaded_replay(G, g)
+    idx = torch.from_numpy(g["idx"]).to(DEV)
+    m = det_init(make_net(net, torch.float32, DEV), 0.5)
+    L = DQNLearner(rb, net=net, dtype=torch.float32, batch_size=len(idx), lr=float(g["lr"]),
+                   target_sync_every=0, model=m, sampler=lambda B, r: idx)
+    assert L.fused and not L.f64
+    det_init(L.target, 0.2)
+    L.update()
+    torch.cuda.synchronize()
+    ref = float(g["loss_ref"])
+    assert abs(float(L.last_loss) - ref) <= 2e-5 * abs(ref), (float(L.last_loss), ref)
+    np.testing.assert_allclose(L._y.cpu().numpy(), g["y"], rtol=1e-5, atol=1e-4)
+    grad = L.grad_flat.double().cpu().numpy()
+    gref = g["grads"]
+    off = 0
+    for p in L.model.parameters():
+        k = p.numel()
+        a, b = grad[off:off + k], gref[off:off + k]
+        assert np.linalg.norm(a - b) <= 1e-3 * max(np.linalg.norm(b), 1e-12), (off, k)
+        off += k
