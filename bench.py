@@ -176,7 +176,10 @@ def capture(fn, n_steps: int):
 # ------------------------------------------------------------------ headline: the rollout kernel
 def bench_rollout(args, world, rank, dev):
     """W untimed + `steps` timed k_rollout launches (K env steps of every board each, replay
-    append into an N*K-row ring)."""
+    append into an N*K-row ring), replayed from hipGraphs of --graph-steps launches (the kernel
+    reads its step clock and ring row from device memory, so a replay is a fresh rollout): back
+    to back on the GPU, so the events' time per launch is the kernel's own duration (what
+    rocprofv3 --kernel-trace reports), not kernel + host enqueue gap."""
     import g2048
 
     n, k = args.boards, args.rollout_k
@@ -186,10 +189,23 @@ def bench_rollout(args, world, rank, dev):
     def launch():
         env.rollout(k, replay=rb)
 
+    steps = args.steps
+    G = max(1, min(args.graph_steps, steps))
+    graphs = [(capture(launch, G), steps // G)]
+    if steps % G:
+        graphs.append((capture(launch, steps % G), 1))
+    for g, _ in graphs:  # no timed replay is the first replay of its graph
+        g.replay()
     for _ in range(max(args.warmup, 1)):
         launch()
     torch.cuda.synchronize()
-    wall, ev = timed(world, dev, launch, args.steps)
+
+    def run_all():
+        for g, reps in graphs:
+            for _ in range(reps):
+                g.replay()
+
+    wall, ev = timed(world, dev, run_all, 1)
     env.check_errors()
     assert int(rb.count) == n * k
     return dict(wall=wall, ev_s=ev, n=n, k=k)
