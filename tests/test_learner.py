@@ -118,3 +118,23 @@ def test_conv_net_state_dict_matches_reference_layout():
     assert sum(p.numel() for p in m.parameters()) == 33476
     assert sum(p.numel() for p in make_net("dense").parameters()) == 403716
     assert sum(p.numel() for p in make_net("dense64").parameters()) == 1348
+
+
+def test_fused_f64_routing_on_cpu():
+    """Which nets the float64 fused kernels take (qnet.kind64_of), and the wrappers' argument
+    checks, which fail before any device call: fp32 nets and the dense-ref net are refused."""
+    from g2048 import qnet
+
+    conv64, dense64 = make_net("conv", torch.float64, "cpu"), make_net("dense64", torch.float64, "cpu")
+    assert qnet.kind64_of(conv64) == "conv" and qnet.kind64_of(dense64) == "dense64"
+    assert qnet.kind64_of(make_net("dense", torch.float64, "cpu")) is None
+    assert qnet.kind64_of(make_net("conv", torch.float32, "cpu")) is None
+    conv32 = make_net("conv", torch.float32, "cpu")
+    with pytest.raises(TypeError):
+        qnet.ConvUpdate64(conv32, conv32, 512)
+    with pytest.raises(TypeError):
+        qnet.ConvForward64(conv32)
+    with pytest.raises(TypeError):
+        qnet.Dense64Update64(conv64, conv64, 512)
+    with pytest.raises(ValueError):  # float64 on the CPU: the fused kernels need CUDA tensors
+        qnet.ConvUpdate64(conv64, conv64, 512)
