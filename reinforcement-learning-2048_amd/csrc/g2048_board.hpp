@@ -45,6 +45,12 @@ __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
     return (a & m) | (b & ~m);
 }
 
+__device__ __forceinline__ uint32_t or3_v(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_or3_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 struct Board {
     uint32_t r0, r1, r2, r3;
 };
@@ -83,17 +89,24 @@ __device__ __forceinline__ uint32_t legal_mask(const Board& b) {
 }
 
 // Slide the four lines toward L0 (byte j of L_k = k-th cell of line j); returns the merge gain.
+// zany: 0x80 flags of the empty cells of the lines as given (non-zero iff a cell is empty);
+// pairs: 0x80 flags of the equal non-empty neighbours after compaction -- for a full board (no
+// compaction) the equal neighbours along the lines, which is_done needs for this axis.
 __device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint32_t& l2,
-                                                uint32_t& l3) {
+                                                uint32_t& l3, uint32_t& zany, uint32_t& pairs) {
     // 1) stable compaction, back to front: [c d] then [b c d] then [a b c d]
-    uint32_t m = expand80(z80(l2));
+    const uint32_t z2 = z80(l2), z3 = z80(l3);
+    uint32_t m = expand80(z2);
     l2 = bsel(m, l3, l2);
     l3 &= ~m;
-    m = expand80(z80(l1));
+    const uint32_t z1 = z80(l1);
+    m = expand80(z1);
     l1 = bsel(m, l2, l1);
     l2 = bsel(m, l3, l2);
     l3 &= ~m;
-    m = expand80(z80(l0));
+    const uint32_t z0 = z80(l0);
+    zany = or3_v(z0, z1, z2 | z3);
+    m = expand80(z0);
     l0 = bsel(m, l1, l0);
     l1 = bsel(m, l2, l1);
     l2 = bsel(m, l3, l2);
@@ -104,6 +117,7 @@ __device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint
     const uint32_t cd_raw = z80(l2 ^ l3) & nz80(l2);
     const uint32_t bc = bc_raw & ~ab;
     const uint32_t cd = cd_raw & (ab | ~bc_raw);
+    pairs = or3_v(ab, bc_raw, cd_raw);
     const uint32_t AB = expand80(ab), BC = expand80(bc), CD = expand80(cd);
     const uint32_t c1 = l2 + (cd >> 7);  // merged c+d (when that merge happens)
     const uint32_t b1 = l1 + (bc >> 7);  // merged b+c
@@ -129,14 +143,30 @@ __device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint
     return s;
 }
 
+__device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint32_t& l2,
+                                                uint32_t& l3) {
+    uint32_t zany, pairs;
+    return slide_lines(l0, l1, l2, l3, zany, pairs);
+}
+
 // Apply action a (0 up, 1 down, 2 left, 3 right) WITHOUT spawning; returns the merge gain.
-__device__ __forceinline__ uint32_t apply_move(Board& b, uint32_t act) {
+// done_flags (optional): zero iff the board as given is terminal and not empty -- full, with no
+// equal neighbours along the move's lines (the slide's own pair flags: a full board does not
+// compact) nor across them (adjacent bytes within the line words); see is_done.
+__device__ __forceinline__ uint32_t apply_move(Board& b, uint32_t act,
+                                               uint32_t* done_flags = nullptr) {
     const bool horiz = act >= 2u, rev = (act & 1u) != 0u;
     const Board t = transpose(b);
     const uint32_t a0 = horiz ? t.r0 : b.r0, a1 = horiz ? t.r1 : b.r1;
     const uint32_t a2 = horiz ? t.r2 : b.r2, a3 = horiz ? t.r3 : b.r3;
     uint32_t l0 = rev ? a3 : a0, l1 = rev ? a2 : a1, l2 = rev ? a1 : a2, l3 = rev ? a0 : a3;
-    const uint32_t score = slide_lines(l0, l1, l2, l3);
+    uint32_t zany, pairs;
+    const uint32_t score = slide_lines(l0, l1, l2, l3, zany, pairs);
+    if (done_flags) {
+        const uint32_t across = z80(a0 ^ (a0 >> 8)) | z80(a1 ^ (a1 >> 8)) |
+                                z80(a2 ^ (a2 >> 8)) | z80(a3 ^ (a3 >> 8));
+        *done_flags = or3_v(zany, pairs, across & 0x00808080u);
+    }
     Board o;
     o.r0 = rev ? l3 : l0;
     o.r1 = rev ? l2 : l1;
@@ -210,11 +240,6 @@ __device__ __forceinline__ uint32_t xor3_sk(uint32_t a, uint32_t b, uint32_t k) 
     return d;
 }
 
-__device__ __forceinline__ uint32_t or3_v(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t d;
-    asm("v_or3_b32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
 
 // Same rounds, constants and counter layout as rocRAND's philox4x32_10 engine: the block for
 // (seed, subsequence s, offset 4t) is philox10({t_lo, t_hi, s_lo, s_hi}, {seed_lo, seed_hi}).
@@ -327,13 +352,15 @@ __device__ __forceinline__ void spawn_if(Board& b, uint32_t u_cell, uint32_t u_v
 __device__ __forceinline__ uint32_t random_step(Board& b, uint32_t wa, uint32_t wb,
                                                 uint32_t p4_thresh, bool& done) {
     Board nb = b;
-    const uint32_t gain = apply_move(nb, wa >> 30);
+    uint32_t flags;
+    const uint32_t gain = apply_move(nb, wa >> 30, &flags);
     // all-ones iff the move changed the board.  The OR is opaque to the compiler (inline asm):
     // otherwise hipcc splits it into four v_cmp whose lane masks it merges with s_or_b64, and at
     // one wave per SIMD every SALU op costs an issue turn.
     const uint32_t diff = or3_v(nb.r0 ^ b.r0, nb.r1 ^ b.r1, (nb.r2 ^ b.r2) | (nb.r3 ^ b.r3));
     const uint32_t moved = (uint32_t)((int32_t)(diff | (0u - diff)) >> 31);
-    done = is_done(b);
+    // is_done(b) from the slide's own flags: min(flags, any tile) == 0 (an empty board is done)
+    done = min(flags, or3_v(b.r0, b.r1, b.r2 | b.r3)) == 0u;
     spawn_if(nb, wa << 2, wb, p4_thresh, moved);
     b = nb;
     return gain;
