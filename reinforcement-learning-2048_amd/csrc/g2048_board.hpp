@@ -88,6 +88,32 @@ __device__ __forceinline__ uint32_t legal_mask(const Board& b) {
            ((uint32_t)((L | H) != 0u) << 2) | ((uint32_t)((R | H) != 0u) << 3);
 }
 
+// 2^x0 + 2^x1 + 2^x2 + 2^x3 over the bytes x_k of x (each < 32): one SDWA shift per byte, whose
+// byte-select operand does the extraction (hipcc spends a v_lshrrev per byte otherwise).
+template <int K>
+__device__ __forceinline__ uint32_t pow2_byte(uint32_t x, uint32_t one) {
+    uint32_t d;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD"
+            : "=v"(d) : "v"(x), "v"(one));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD"
+            : "=v"(d) : "v"(x), "v"(one));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD"
+            : "=v"(d) : "v"(x), "v"(one));
+    else
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD"
+            : "=v"(d) : "v"(x), "v"(one));
+    return d;
+}
+
+__device__ __forceinline__ uint32_t pow2_bytes(uint32_t x) {
+    const uint32_t one = 1u;
+    return pow2_byte<0>(x, one) + pow2_byte<1>(x, one) + pow2_byte<2>(x, one) +
+           pow2_byte<3>(x, one);
+}
+
 // Slide the four lines toward L0 (byte j of L_k = k-th cell of line j); returns the merge gain.
 // zany: 0x80 flags of the empty cells of the lines as given (non-zero iff a cell is empty);
 // pairs: 0x80 flags of the equal non-empty neighbours after compaction -- for a full board (no
@@ -129,13 +155,8 @@ __device__ __forceinline__ uint32_t slide_lines(uint32_t& l0, uint32_t& l1, uint
     //    excludes ab), so their merged bytes share one word: 8 candidate bytes, and a zero byte
     //    (no merge) gives 2^0 = 1, taken off at the end.
     const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        s += 1u << ((e01 >> (8 * k)) & 31u);
-        s += 1u << ((e2 >> (8 * k)) & 31u);
-    }
-    s -= 8u - (uint32_t)(__popc(ab | bc) + __popc(cd));
+    const uint32_t s = (pow2_bytes(e01) + pow2_bytes(e2)) -
+                       (8u - (uint32_t)(__popc(ab | bc) + __popc(cd)));
     l0 = o0;
     l1 = o1;
     l2 = o2;
@@ -200,23 +221,45 @@ __device__ __forceinline__ bool cell_empty(const Board& b, uint32_t pos) {
     return ((w >> ((pos & 3u) * 8u)) & 0xFFu) == 0u;
 }
 
+__device__ __forceinline__ bool has_empty(const Board& b) {
+    return (z80(b.r0) | z80(b.r1) | z80(b.r2) | z80(b.r3)) != 0u;
+}
+
+// The k-th (0-based) empty cell in row-major order, k = floor(u_cell * n / 2^32) for the n > 0
+// empty cells, ORed with exponent e (e = 0 leaves the board as it is).  Binary search over the
+// board's halves {r0, r1} / {r2, r3}, then the row, then the byte pair, then the byte; the tile is
+// placed with one 64-bit shift into the chosen half.
+__device__ __forceinline__ void spawn_at(Board& b, uint32_t u_cell, uint32_t e) {
+    const uint32_t z0 = z80(b.r0), z1 = z80(b.r1), z2 = z80(b.r2), z3 = z80(b.r3);
+    const uint32_t p1 = __popc(z0), p2 = p1 + __popc(z1), p3 = p2 + __popc(z2);
+    const uint32_t n = p3 + __popc(z3);
+    uint32_t k = __umulhi(u_cell, n);
+    const bool hi = k >= p2;  // rows 2-3
+    const uint32_t za = hi ? z2 : z0, zb = hi ? z3 : z1;
+    const uint32_t c1 = hi ? p3 - p2 : p1;
+    k = hi ? k - p2 : k;
+    const bool w1 = k >= c1;  // the half's second row
+    k = w1 ? k - c1 : k;
+    uint32_t z = w1 ? zb : za;
+    const uint32_t c2 = __popc(z & 0x8080u);
+    const bool h2 = k >= c2;  // bytes 2-3
+    k = h2 ? k - c2 : k;
+    z = h2 ? z >> 16 : z;
+    const bool b1 = k >= ((z >> 7) & 1u);
+    const uint32_t sh = (w1 ? 32u : 0u) | (h2 ? 16u : 0u) | (b1 ? 8u : 0u);
+    const uint64_t v = (uint64_t)e << sh;
+    b.r0 |= hi ? 0u : (uint32_t)v;
+    b.r1 |= hi ? 0u : (uint32_t)(v >> 32);
+    b.r2 |= hi ? (uint32_t)v : 0u;
+    b.r3 |= hi ? (uint32_t)(v >> 32) : 0u;
+}
+
 // One spawn (src/board.py:41-51): the k-th empty cell in row-major order with
 // k = floor(u_cell * n / 2^32); exponent 2 (a "4") iff u_val < p4_thresh.
 __device__ __forceinline__ void spawn(Board& b, uint32_t u_cell, uint32_t u_val,
                                       uint32_t p4_thresh) {
-    const uint32_t z0 = z80(b.r0), z1 = z80(b.r1), z2 = z80(b.r2), z3 = z80(b.r3);
-    const uint32_t p1 = __popc(z0), p2 = p1 + __popc(z1), p3 = p2 + __popc(z2);
-    const uint32_t n = p3 + __popc(z3);
-    if (n == 0u) return;
-    uint32_t k = __umulhi(u_cell, n);
-    const uint32_t row = (uint32_t)(k >= p1) + (uint32_t)(k >= p2) + (uint32_t)(k >= p3);
-    uint32_t z = row == 0u ? z0 : row == 1u ? z1 : row == 2u ? z2 : z3;
-    k -= row == 0u ? 0u : row == 1u ? p1 : row == 2u ? p2 : p3;
-    uint32_t byte = 0;
-    const uint32_t c01 = __popc(z & 0x8080u);
-    if (k >= c01) { k -= c01; z >>= 16; byte = 2; }
-    byte += (uint32_t)(k >= ((z >> 7) & 1u));
-    set_cell(b, row * 4u + byte, u_val < p4_thresh ? 2u : 1u);
+    if (!has_empty(b)) return;
+    spawn_at(b, u_cell, u_val < p4_thresh ? 2u : 1u);
 }
 
 __device__ __forceinline__ uint32_t max_exp(const Board& b) {
@@ -329,21 +372,11 @@ __device__ __forceinline__ bool is_done(const Board& b) {
     return min(z | (H & 0x00808080u) | V, b.r0 | b.r1 | b.r2 | b.r3) == 0u;
 }
 
-// spawn() without branches; on_mask = 0 (spawn exponent 0) leaves the board as it is.
+// spawn() without branches; on_mask = 0 (spawn exponent 0) leaves the board as it is.  The
+// board must have an empty cell when on_mask is set (a move that changed it always leaves one).
 __device__ __forceinline__ void spawn_if(Board& b, uint32_t u_cell, uint32_t u_val,
                                          uint32_t p4_thresh, uint32_t on_mask) {
-    const uint32_t z0 = z80(b.r0), z1 = z80(b.r1), z2 = z80(b.r2), z3 = z80(b.r3);
-    const uint32_t p1 = __popc(z0), p2 = p1 + __popc(z1), p3 = p2 + __popc(z2);
-    const uint32_t n = p3 + __popc(z3);
-    uint32_t k = __umulhi(u_cell, n);
-    const uint32_t row = (uint32_t)(k >= p1) + (uint32_t)(k >= p2) + (uint32_t)(k >= p3);
-    uint32_t z = row == 0u ? z0 : row == 1u ? z1 : row == 2u ? z2 : z3;
-    k -= row == 0u ? 0u : row == 1u ? p1 : row == 2u ? p2 : p3;
-    uint32_t byte = 0;
-    const uint32_t c01 = __popc(z & 0x8080u);
-    if (k >= c01) { k -= c01; z >>= 16; byte = 2; }
-    byte += (uint32_t)(k >= ((z >> 7) & 1u));
-    set_cell(b, row * 4u + byte, (u_val < p4_thresh ? 2u : 1u) & on_mask);
+    spawn_at(b, u_cell, (u_val < p4_thresh ? 2u : 1u) & on_mask);
 }
 
 // One random-policy transition of board b with words (wa, wb): slide (a board the chosen move
