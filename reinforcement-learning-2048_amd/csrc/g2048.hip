@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -64,6 +65,11 @@ struct ReplayDev {
     unsigned long long* count;
     int64_t capacity;
     int64_t rows;  // capacity / n  (0 = no replay)
+    // one buffer-resource window over every section (k_rollout's buffer stores): base, size and
+    // the byte offset of each section in it; win_bytes = 0 when the sections do not fit 4 GiB
+    uint8_t* win;
+    uint32_t win_bytes;
+    uint32_t o_s, o_s2, o_a, o_r, o_d;
 };
 
 struct StepArgs {
@@ -489,7 +495,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // keeps its scalar bookkeeping to a 32-bit ring row and a 64-bit pair counter, and the episode
 // counters are stored once at the end (only the last finished episode's record survives in ep;
 // the log, when attached, gets every one).  See DESIGN.md section 4.1.
-//   kRing: a replay ring is attached; kBuf: its sections are below 2 GiB (buffer stores);
+//   kRing: a replay ring is attached; kBuf: its sections lie in one window below 4 GiB (buffer
+//   stores through ONE resource, so the loop holds 4 SGPRs of descriptor, not 20);
 //   kSum: per-board reward sums are accumulated.
 template <bool kRing, bool kBuf, bool kSum>
 __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
@@ -507,18 +514,15 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     const uint32_t rows = kRing ? (uint32_t)A.rb.rows : 1u;
     uint32_t row = kRing ? (uint32_t)ring_row(t0, A.rb.rows) : 0u;
     const uint32_t n32 = (uint32_t)A.n;
-    // (the global-store instance -- ring sections past 2 GiB -- builds empty descriptors)
-    const uint32_t cap = kBuf ? (uint32_t)A.rb.capacity : 0u;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(A.rb.s, 0, (int)(16u * cap), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rs2 =
-        __builtin_amdgcn_make_buffer_rsrc(A.rb.s2, 0, (int)(16u * cap), 0x00020000);
-    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(A.rb.a, 0, (int)cap, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rr =
-        __builtin_amdgcn_make_buffer_rsrc(A.rb.r, 0, (int)(4u * cap), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(A.rb.d, 0, (int)cap, 0x00020000);
-    const uint32_t lane_off = (uint32_t)i;
-    bool ended = false;  // some episode of this board ended in the launch
+    // (the global-store instance -- no 4 GiB window -- builds an empty descriptor)
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        A.rb.win, 0, (int)(kBuf ? A.rb.win_bytes : 0u), 0x00020000);
+    const uint32_t lane = (uint32_t)i;
+    // per-lane offsets of the five sections in the window (loop-invariant VGPRs)
+    const uint32_t v_s = kBuf ? A.rb.o_s + 16u * lane : 0u, v_s2 = kBuf ? A.rb.o_s2 + 16u * lane : 0u;
+    const uint32_t v_a = kBuf ? A.rb.o_a + lane : 0u, v_r = kBuf ? A.rb.o_r + 4u * lane : 0u;
+    const uint32_t v_d = kBuf ? A.rb.o_d + lane : 0u;
+    const uint32_t ep0 = ep.x;  // some episode of this board ended in the launch iff ep.x moved
     Board last = b;      // the final board of that episode (its max tile goes to ep.w at the end)
     // one transition with the words (wa, wb) of step t
     auto one = [&](uint32_t wa, uint32_t wb, uint64_t t) {
@@ -531,13 +535,13 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
         if constexpr (kRing) {
             if constexpr (kBuf) {
                 const uint32_t soff = row * n32;
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{so.r0, so.r1, so.r2, so.r3}, rs,
-                                                       lane_off * 16u, soff * 16u, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rs2,
-                                                       lane_off * 16u, soff * 16u, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), ra, lane_off, soff, 0);
-                __builtin_amdgcn_raw_buffer_store_b32(r, rr, lane_off * 4u, soff * 4u, 0);
-                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rd, lane_off, soff, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{so.r0, so.r1, so.r2, so.r3}, rw,
+                                                       v_s, soff * 16u, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2,
+                                                       soff * 16u, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), rw, v_a, soff, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(r, rw, v_r, soff * 4u, 0);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, v_d, soff, 0);
             } else {
                 const int64_t slot = (int64_t)row * A.n + i;
                 A.rb.s[slot] = make_uint4(so.r0, so.r1, so.r2, so.r3);
@@ -564,7 +568,6 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
             ep = make_uint4(ep.x + 1u, m.x, m.y, 0u);
             last = b;
             qs = 0.0;
-            ended = true;
             if (autoreset) {
                 b = fresh_board_random(wa, wb, p4_16);
                 m = make_uint2(0u, 0u);
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     const uint64_t t1 = t0 + (uint64_t)(K > 0 ? K : 0);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
-    if (ended) {
+    if (ep.x != ep0) {
         ep.w = max_exp(last);
         A.ep[i] = ep;
         if (A.qsum) A.qsum[i] = 0.0;
@@ -807,6 +810,26 @@ int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
         A.rb.count = rb->count;
         A.rb.capacity = rb->capacity;
         A.rb.rows = rb->capacity / e->n;
+        // the window: lowest section start to highest section end, when below 4 GiB
+        const int64_t c = rb->capacity;
+        const uintptr_t st[5] = {(uintptr_t)rb->s, (uintptr_t)rb->s2, (uintptr_t)rb->a,
+                                 (uintptr_t)rb->r, (uintptr_t)rb->d};
+        const uint64_t sz[5] = {16u * (uint64_t)c, 16u * (uint64_t)c, (uint64_t)c,
+                                4u * (uint64_t)c, (uint64_t)c};
+        uintptr_t lo = st[0], hi = st[0] + sz[0];
+        for (int k = 1; k < 5; ++k) {
+            lo = std::min(lo, st[k]);
+            hi = std::max(hi, (uintptr_t)(st[k] + sz[k]));
+        }
+        if ((uint64_t)(hi - lo) < ((uint64_t)1 << 32)) {
+            A.rb.win = reinterpret_cast<uint8_t*>(lo);
+            A.rb.win_bytes = (uint32_t)(hi - lo);
+            A.rb.o_s = (uint32_t)(st[0] - lo);
+            A.rb.o_s2 = (uint32_t)(st[1] - lo);
+            A.rb.o_a = (uint32_t)(st[2] - lo);
+            A.rb.o_r = (uint32_t)(st[3] - lo);
+            A.rb.o_d = (uint32_t)(st[4] - lo);
+        }
     }
     return G2048_OK;
 }
@@ -1160,12 +1183,12 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
     A.reward_sum = reinterpret_cast<long long*>(reward_sum);
     DeviceGuard g(e->device);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // buffer-resource stores while every ring section (16 B per row at most) stays below 2^31 B
+    // buffer-resource stores while the ring's sections fit one 4 GiB window
     const dim3 grid(grid_for(e->n)), block(kBlock);
     if (!rb) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<false, false, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<false, false, false>), grid, block, 0, st, A);
-    } else if (rb->capacity <= ((int64_t)1 << 27)) {
+    } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<true, true, false>), grid, block, 0, st, A);
     } else {

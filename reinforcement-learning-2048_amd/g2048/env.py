@@ -346,13 +346,24 @@ class ReplayBuffer:
     def __init__(self, capacity: int, device="cuda"):
         self.device = N.require_gpu(device)
         self.capacity = int(capacity)
-        kw = dict(device=self.device)
-        self.s = torch.zeros((self.capacity, 16), dtype=torch.uint8, **kw)
-        self.s2 = torch.zeros((self.capacity, 16), dtype=torch.uint8, **kw)
-        self.a = torch.zeros(self.capacity, dtype=torch.uint8, **kw)
-        self.r = torch.zeros(self.capacity, dtype=torch.int32, **kw)
-        self.d = torch.zeros(self.capacity, dtype=torch.uint8, **kw)
-        self.count = torch.zeros(1, dtype=torch.int64, **kw)
+        # one allocation, 256-byte aligned sections s | s2 | r | a | d | count (as
+        # g2048_replay_create lays them out), so the rollout's ring stores go through one buffer
+        # resource whenever the ring is below 4 GiB
+        c = self.capacity
+        up = lambda x: (x + 255) // 256 * 256  # noqa: E731
+        o_s2 = up(16 * c)
+        o_r = o_s2 + up(16 * c)
+        o_a = o_r + up(4 * c)
+        o_d = o_a + up(c)
+        o_c = o_d + up(c)
+        self._mem = torch.zeros(o_c + 256, dtype=torch.uint8, device=self.device)
+        m = self._mem
+        self.s = m[0:16 * c].view(c, 16)
+        self.s2 = m[o_s2:o_s2 + 16 * c].view(c, 16)
+        self.r = m[o_r:o_r + 4 * c].view(torch.int32)
+        self.a = m[o_a:o_a + c]
+        self.d = m[o_d:o_d + c]
+        self.count = m[o_c:o_c + 8].view(torch.int64)
         self._h = C.c_void_p()
         self._destroy = N.load().g2048_replay_destroy
         with torch.cuda.device(self.device):
