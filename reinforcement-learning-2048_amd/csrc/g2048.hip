@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -525,7 +526,10 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     const uint32_t ep0 = ep.x;  // some episode of this board ended in the launch iff ep.x moved
     Board last = b;      // the final board of that episode (its max tile goes to ep.w at the end)
     // one transition with the words (wa, wb) of step t
-    auto one = [&](uint32_t wa, uint32_t wb, uint64_t t) {
+    // lean (std::true_type): no episode log and auto-reset on -- the loop then carries neither
+    // uniform test (each an SALU op per step at one wave per SIMD)
+    auto one = [&](auto lean, uint32_t wa, uint32_t wb, uint64_t t) {
+        constexpr bool kLean = decltype(lean)::value;
         const Board so = b;
         bool done;
         const uint32_t r = random_step(b, wa, wb, A.p4_thresh, done);
@@ -553,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
             row = row + 1u == rows ? 0u : row + 1u;
         }
         if (done) {  // taken by some lane of the wave on roughly 40 % of the steps
-            if (A.log) {
+            if (!kLean && A.log) {
                 g2048_episode rec;
                 rec.step = t;
                 rec.q_sum = qs;
@@ -568,31 +572,35 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
             ep = make_uint4(ep.x + 1u, m.x, m.y, 0u);
             last = b;
             qs = 0.0;
-            if (autoreset) {
+            if (kLean || autoreset) {
                 b = fresh_board_random(wa, wb, p4_16);
                 m = make_uint2(0u, 0u);
             }
         }
     };
-    const int K = A.k_steps;
-    uint64_t pair = t0 >> 1;
-    int s = 0;
-    if (K > 0 && (t0 & 1u)) {  // odd start: the second half of the current pair
-        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-        one(blk.z, blk.w, t0);
-        ++pair;
-        s = 1;
-    }
-    for (; s + 1 < K; s += 2, ++pair) {
-        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-        one(blk.x, blk.y, 2u * pair);
-        one(blk.z, blk.w, 2u * pair + 1u);
-    }
-    if (s < K) {
-        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-        one(blk.x, blk.y, 2u * pair);
-    }
-    const uint64_t t1 = t0 + (uint64_t)(K > 0 ? K : 0);
+    const int K = A.k_steps > 0 ? A.k_steps : 0;
+    auto run = [&](auto lean) {
+        uint64_t pair = t0 >> 1;
+        int rest = K;
+        if (rest > 0 && (t0 & 1u)) {  // odd start: the second half of the current pair
+            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+            one(lean, blk.z, blk.w, t0);
+            ++pair;
+            --rest;
+        }
+        for (int np = rest >> 1; np > 0; --np, ++pair) {  // a down-counter: one SALU op less
+            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+            one(lean, blk.x, blk.y, 2u * pair);
+            one(lean, blk.z, blk.w, 2u * pair + 1u);
+        }
+        if (rest & 1) {
+            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+            one(lean, blk.x, blk.y, 2u * pair);
+        }
+    };
+    if (!A.log && autoreset) run(std::true_type{});
+    else run(std::false_type{});
+    const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
     if (ep.x != ep0) {
