@@ -514,9 +514,12 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
     double qs = A.qsum ? A.qsum[i] : 0.0;  // random policy: reset (0) on done only
     const uint32_t rows = kRing ? (uint32_t)A.rb.rows : 1u;
     uint32_t row = kRing ? (uint32_t)ring_row(t0, A.rb.rows) : 0u;
+    // buffer path: the row's first slot (row * n) kept running, wrapped at the capacity
+    const uint32_t cap32 = kBuf ? (uint32_t)A.rb.capacity : 0u;
+    uint32_t soff = kBuf ? row * (uint32_t)A.n : 0u;
     const uint32_t n32 = (uint32_t)A.n;
     // (the global-store instance -- no 4 GiB window -- builds an empty descriptor)
-    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+    __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
         A.rb.win, 0, (int)(kBuf ? A.rb.win_bytes : 0u), 0x00020000);
     const uint32_t lane = (uint32_t)i;
     // per-lane offsets of the five sections in the window (loop-invariant VGPRs)
@@ -538,7 +541,6 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
         if constexpr (kSum) rsum += r;
         if constexpr (kRing) {
             if constexpr (kBuf) {
-                const uint32_t soff = row * n32;
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{so.r0, so.r1, so.r2, so.r3}, rw,
                                                        v_s, soff * 16u, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2,
@@ -554,7 +556,8 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
                 A.rb.r[slot] = (int32_t)r;
                 A.rb.d[slot] = (uint8_t)done;
             }
-            row = row + 1u == rows ? 0u : row + 1u;
+            if constexpr (kBuf) soff = soff + n32 == cap32 ? 0u : soff + n32;
+            else row = row + 1u == rows ? 0u : row + 1u;
         }
         if (done) {  // taken by some lane of the wave on roughly 40 % of the steps
             if (!kLean && A.log) {
@@ -589,6 +592,7 @@ __global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
             --rest;
         }
         for (int np = rest >> 1; np > 0; --np, ++pair) {  // a down-counter: one SALU op less
+            if constexpr (kBuf) asm volatile("" : "+s"(rw));  // one SGPR quad for the descriptor
             const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
             one(lean, blk.x, blk.y, 2u * pair);
             one(lean, blk.z, blk.w, 2u * pair + 1u);
