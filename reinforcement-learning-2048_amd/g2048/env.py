@@ -343,27 +343,36 @@ class ReplayBuffer:
     deque(maxlen=replay_buffer_length) of (Board2048, action, reward, Board2048, done) tuples
     (src/dqn_lib.py:106,172), 38 bytes per transition instead of two Python objects."""
 
-    def __init__(self, capacity: int, device="cuda"):
+    def __init__(self, capacity: int, device="cuda", sections=None):
+        """sections: optional caller-owned (s, s2, a, r, d, count) device tensors to wrap
+        (u8 [capacity, 16] x 2, u8 / i32 / u8 [capacity], i64 [1]); by default one allocation
+        holds them all."""
         self.device = N.require_gpu(device)
         self.capacity = int(capacity)
-        # one allocation, 256-byte aligned sections s | s2 | r | a | d | count (as
-        # g2048_replay_create lays them out), so the rollout's ring stores go through one buffer
-        # resource whenever the ring is below 4 GiB
         c = self.capacity
-        up = lambda x: (x + 255) // 256 * 256  # noqa: E731
-        o_s2 = up(16 * c)
-        o_r = o_s2 + up(16 * c)
-        o_a = o_r + up(4 * c)
-        o_d = o_a + up(c)
-        o_c = o_d + up(c)
-        self._mem = torch.zeros(o_c + 256, dtype=torch.uint8, device=self.device)
-        m = self._mem
-        self.s = m[0:16 * c].view(c, 16)
-        self.s2 = m[o_s2:o_s2 + 16 * c].view(c, 16)
-        self.r = m[o_r:o_r + 4 * c].view(torch.int32)
-        self.a = m[o_a:o_a + c]
-        self.d = m[o_d:o_d + c]
-        self.count = m[o_c:o_c + 8].view(torch.int64)
+        if sections is None:
+            # one allocation, 256-byte aligned sections s | s2 | r | a | d | count (as
+            # g2048_replay_create lays them out), so the rollout's ring stores go through one
+            # buffer resource whenever the ring is below 4 GiB
+            up = lambda x: (x + 255) // 256 * 256  # noqa: E731
+            o_s2 = up(16 * c)
+            o_r = o_s2 + up(16 * c)
+            o_a = o_r + up(4 * c)
+            o_d = o_a + up(c)
+            o_c = o_d + up(c)
+            self._mem = torch.zeros(o_c + 256, dtype=torch.uint8, device=self.device)
+            m = self._mem
+            sections = (m[0:16 * c].view(c, 16), m[o_s2:o_s2 + 16 * c].view(c, 16),
+                        m[o_a:o_a + c], m[o_r:o_r + 4 * c].view(torch.int32), m[o_d:o_d + c],
+                        m[o_c:o_c + 8].view(torch.int64))
+        want = [((c, 16), torch.uint8), ((c, 16), torch.uint8), ((c,), torch.uint8),
+                ((c,), torch.int32), ((c,), torch.uint8), ((1,), torch.int64)]
+        for t, (shape, dt) in zip(sections, want):
+            if (tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous()
+                    or t.device != self.device):
+                raise ValueError(f"replay section must be a contiguous {dt} {shape} tensor on "
+                                 f"{self.device}")
+        self.s, self.s2, self.a, self.r, self.d, self.count = sections
         self._h = C.c_void_p()
         self._destroy = N.load().g2048_replay_destroy
         with torch.cuda.device(self.device):

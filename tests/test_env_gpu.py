@@ -296,6 +296,50 @@ def test_rollout_equals_single_steps(g2048, n, p4):
     assert torch.equal(l1.qsum, l2.qsum)
 
 
+def _rollout_ring(g2048, n, k, rb, seed=31):
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    env.step(None, replay=rb)  # odd start
+    env.rollout(k, replay=rb)
+    torch.cuda.synchronize()
+    return env
+
+
+def test_rollout_ring_layouts(g2048):
+    """The rollout's ring stores through its three address paths give the same rows: one
+    allocation (one buffer window), separately allocated sections in shuffled order (a window
+    based at the lowest section), and a ring whose sections span more than 4 GiB (global
+    stores)."""
+    n, k = 4096 + 77, 21
+    ref = g2048.ReplayBuffer(32 * n, device=DEV)
+    e0 = _rollout_ring(g2048, n, k, ref)
+    # separately allocated sections, in an order that puts d lowest and s highest
+    c = 32 * n
+    d = torch.zeros(c, dtype=torch.uint8, device=DEV)
+    r = torch.zeros(c, dtype=torch.int32, device=DEV)
+    a = torch.zeros(c, dtype=torch.uint8, device=DEV)
+    s2 = torch.zeros((c, 16), dtype=torch.uint8, device=DEV)
+    s = torch.zeros((c, 16), dtype=torch.uint8, device=DEV)
+    cnt = torch.zeros(1, dtype=torch.int64, device=DEV)
+    sep = g2048.ReplayBuffer(c, device=DEV, sections=(s, s2, a, r, d, cnt))
+    e1 = _rollout_ring(g2048, n, k, sep)
+    # 2^27 + n rows (5.1 GB): past the 4 GiB window, the global-store instance
+    big = g2048.ReplayBuffer((1 << 27) // n * n + n, device=DEV)
+    e2 = _rollout_ring(g2048, n, k, big)
+    rows = (k + 1) * n
+    for e in (e1, e2):
+        assert torch.equal(e.board, e0.board) and torch.equal(e.meta, e0.meta)
+        assert torch.equal(e.ep, e0.ep)
+    for name in ["s", "s2", "a", "r", "d"]:
+        want = getattr(ref, name)[:rows]
+        assert torch.equal(getattr(sep, name)[:rows], want), name
+        assert torch.equal(getattr(big, name)[:rows], want), name
+        assert int(getattr(big, name)[rows:].abs().sum() if name == "r"
+                   else getattr(big, name)[rows:].sum()) == 0, name
+    assert int(ref.count) == int(sep.count) == int(big.count) == rows
+    del big
+    torch.cuda.empty_cache()
+
+
 def test_rollout_vs_oracle(g2048):
     """The rollout against the CPU oracle directly (random-policy draws: half a Philox block per
     step), starting from an odd clock."""
