@@ -819,6 +819,26 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
     __shared__ double2 part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 128 + 2 * lane;  // positions pos, pos + 1 (SLAB is even)
+    // wave 0's Adam operands (m, v, parameter of both positions, the update counter) are loaded
+    // with the slabs: independent of the sums, so the update adds no round trip after them
+    const int base[8] = {P_W1, P_B1, P_W2, P_B2, P_F1, P_FB1, P_F2, P_FB2};
+    double am[2] = {0.0, 0.0}, av[2] = {0.0, 0.0}, ap[2] = {0.0, 0.0};
+    int kk[2] = {0, 0};
+    unsigned long long tt = 0;
+    if (A.adam && wave == 0) {
+        tt = *A.step_next;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int ps = pos + h;
+            if (ps >= P_N) continue;
+            int k = 7;
+            while (ps < base[k]) --k;
+            kk[h] = k;
+            am[h] = A.m[ps];
+            av[h] = A.v[ps];
+            ap[h] = A.p[k][ps - base[k]];
+        }
+    }
     double2 r = make_double2(0.0, 0.0);
     if (pos <= P_N) {
         double2 v[MAX_WG / RW];
@@ -853,13 +873,10 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             }
             if (A.grad) A.grad[ps] = sums[h];
             if (A.adam) {
-                const int base[8] = {P_W1, P_B1, P_W2, P_B2, P_F1, P_FB1, P_F2, P_FB2};
-                int k = 7;
-                while (ps < base[k]) --k;
-                const unsigned long long tt = *A.step_next;
-                double m = A.m[ps], v = A.v[ps];
-                const double np = g2048::adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v,
-                                         A.p[k][ps - base[k]]);
+                const int k = kk[h];
+                double m = am[h], v = av[h];
+                const double np =
+                    g2048::adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v, ap[h]);
                 A.m[ps] = m;
                 A.v[ps] = v;
                 A.p[k][ps - base[k]] = np;

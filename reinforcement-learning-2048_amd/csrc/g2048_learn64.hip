@@ -272,33 +272,46 @@ struct RedArgs64 {
     int adam;
 };
 
-// block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... in order, then wave 0
-// combines the 16 partials in order and (adam) applies the update to the parameter in place.
+// block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... in order (all of its
+// loads in flight at once), then wave 0 combines the 16 partials in order and (adam) applies the
+// update to the parameter in place; wave 0's Adam operands are loaded with the slabs.
 __global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
     __shared__ double part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int pos = blockIdx.x * 64 + lane;
+    const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
+    const int base[4] = {P_W1, P_B1, P_W2, P_B2};
+    const bool adam = A.adam && wave == 0 && pos < P_N;
+    double am = 0.0, av = 0.0, ap = 0.0;
+    unsigned long long t = 0;
+    if (adam) {
+        t = *A.step_next;
+        am = A.m[pos];
+        av = A.v[pos];
+        ap = A.p[k][pos - base[k]];
+    }
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+        const int g = wave + RW * u;
+        v[u] = (pos <= P_N && g < A.nslab) ? A.slab[(int64_t)g * SLAB + pos] : 0.0;
+    }
     double r = 0.0;
-    for (int g = wave; g < A.nslab; g += RW)
-        if (pos <= P_N) r += A.slab[(int64_t)g * SLAB + pos];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) r += v[u];
     part[wave][lane] = r;
     __syncthreads();
     if (wave == 0 && pos <= P_N) {
         double sum = part[0][lane];
-        for (int k = 1; k < RW; ++k) sum += part[k][lane];
+        for (int j = 1; j < RW; ++j) sum += part[j][lane];
         if (pos == P_N) {
             if (A.loss) *A.loss = sum;
         } else {
             if (A.grad) A.grad[pos] = sum;
-            if (A.adam) {
-                const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
-                const int base[4] = {P_W1, P_B1, P_W2, P_B2};
-                const unsigned long long t = *A.step_next;
-                double m = A.m[pos], v = A.v[pos];
-                const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, sum, m, v,
-                                         A.p[k][pos - base[k]]);
-                A.m[pos] = m;
-                A.v[pos] = v;
+            if (adam) {
+                const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, sum, am, av, ap);
+                A.m[pos] = am;
+                A.v[pos] = av;
                 A.p[k][pos - base[k]] = np;
                 if (A.sync_every && t % A.sync_every == 0ull) A.tp[k][pos - base[k]] = np;
             }
