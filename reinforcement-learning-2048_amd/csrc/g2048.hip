@@ -500,7 +500,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 //   stores through ONE resource, so the loop holds 4 SGPRs of descriptor, not 20);
 //   kSum: per-board reward sums are accumulated.
 template <bool kRing, bool kBuf, bool kSum>
-__global__ __launch_bounds__(kBlock) void k_rollout(StepArgs A) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5 : 6))) void k_rollout(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= A.n) return;
     const uint64_t t0 = load_clock(A.clock, i);
