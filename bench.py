@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=20, help="untimed rollout launches")
     p.add_argument("--boards", type=int, default=65536)
     p.add_argument("--rollout-k", type=int, default=64, help="env steps per rollout launch")
+    p.add_argument("--rollout-k-extra", default="256",
+                   help="further K values timed beside the headline (rollout_k_sweep field)")
     p.add_argument("--step-steps", type=int, default=2000,
                    help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
@@ -174,7 +176,7 @@ def capture(fn, n_steps: int):
 
 
 # ------------------------------------------------------------------ headline: the rollout kernel
-def bench_rollout(args, world, rank, dev):
+def bench_rollout(args, world, rank, dev, k_override=None):
     """W untimed + `steps` timed k_rollout launches (K env steps of every board each, replay
     append into an N*K-row ring), replayed from hipGraphs of --graph-steps launches (the kernel
     reads its step clock and ring row from device memory, so a replay is a fresh rollout): back
@@ -182,7 +184,7 @@ def bench_rollout(args, world, rank, dev):
     rocprofv3 --kernel-trace reports), not kernel + host enqueue gap."""
     import g2048
 
-    n, k = args.boards, args.rollout_k
+    n, k = args.boards, (args.rollout_k if k_override is None else k_override)
     env = g2048.VecEnv2048(n, seed=args.seed, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(n * k, device=dev)
 
@@ -331,6 +333,14 @@ def main():
     value = n * k * world * args.steps / ro["wall"]
     launch_s = ro["ev_s"] / args.steps
     achieved = ROLLOUT_BYTES * n * k / launch_s / 1e9
+    # the same launch at further K: a launch's first steps run slower than its steady state
+    # (DESIGN.md 4.2), so the per-step time falls with K
+    ksweep = []
+    for kx in [int(x) for x in args.rollout_k_extra.split(",") if x]:
+        rx = bench_rollout(args, world, rank, dev, k_override=kx)
+        lx = rx["ev_s"] / args.steps
+        ksweep.append({"k": kx, "env_steps_per_s": n * kx * world * args.steps / rx["wall"],
+                       "launch_us": lx * 1e6, "frac": ROLLOUT_BYTES * n * kx / lx / 1e9 / HBM_PEAK_GBS})
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
     for net in [x for x in args.train.split(",") if x]:
@@ -371,6 +381,8 @@ def main():
                          "issue": rec.get("issue") if rec else None},
             "cpu_baseline": cpu,
         }
+        if ksweep:
+            line["rollout_k_sweep"] = ksweep
         if step:
             line["step_kernel"] = step
         if train:
