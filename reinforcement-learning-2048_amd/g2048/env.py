@@ -351,16 +351,21 @@ class ReplayBuffer:
         self.capacity = int(capacity)
         c = self.capacity
         if sections is None:
-            # separately allocated sections; the rollout kernel takes its one-descriptor buffer
-            # path whenever they span less than 4 GiB (measured equal to one carved allocation
-            # from 64k to 4M boards)
-            kw = dict(device=self.device)
-            sections = (torch.zeros((c, 16), dtype=torch.uint8, **kw),
-                        torch.zeros((c, 16), dtype=torch.uint8, **kw),
-                        torch.zeros(c, dtype=torch.uint8, **kw),
-                        torch.zeros(c, dtype=torch.int32, **kw),
-                        torch.zeros(c, dtype=torch.uint8, **kw),
-                        torch.zeros(1, dtype=torch.int64, **kw))
+            # one allocation, 256-byte aligned sections s | s2 | r | a | d | count (as
+            # g2048_replay_create lays them out): the rollout's ring stores then always take the
+            # one-descriptor buffer path (sections within 4 GiB), whereas separately allocated
+            # tensors land wherever the allocator puts them
+            up = lambda x: (x + 255) // 256 * 256  # noqa: E731
+            o_s2 = up(16 * c)
+            o_r = o_s2 + up(16 * c)
+            o_a = o_r + up(4 * c)
+            o_d = o_a + up(c)
+            o_c = o_d + up(c)
+            self._mem = torch.zeros(o_c + 256, dtype=torch.uint8, device=self.device)
+            m = self._mem
+            sections = (m[0:16 * c].view(c, 16), m[o_s2:o_s2 + 16 * c].view(c, 16),
+                        m[o_a:o_a + c], m[o_r:o_r + 4 * c].view(torch.int32), m[o_d:o_d + c],
+                        m[o_c:o_c + 8].view(torch.int64))
         want = [((c, 16), torch.uint8), ((c, 16), torch.uint8), ((c,), torch.uint8),
                 ((c,), torch.int32), ((c,), torch.uint8), ((1,), torch.int64)]
         for t, (shape, dt) in zip(sections, want):
