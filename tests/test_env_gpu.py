@@ -296,6 +296,24 @@ def test_rollout_equals_single_steps(g2048, n, p4):
     assert torch.equal(l1.qsum, l2.qsum)
 
 
+def test_rollout_no_autoreset_equals_single_steps(g2048):
+    """Without auto-reset (and no episode log: the rollout's general loop, not its lean one)
+    finished boards stay terminal; K steps in one launch == K single steps, ring included."""
+    n, seed = 2048 + 77, 515
+    e1 = g2048.VecEnv2048(n, seed=seed, device=DEV, autoreset=False)
+    e2 = g2048.VecEnv2048(n, seed=seed, device=DEV, autoreset=False)
+    r1, r2 = g2048.ReplayBuffer(300 * n, device=DEV), g2048.ReplayBuffer(300 * n, device=DEV)
+    for k in (1, 150, 99):
+        e1.rollout(k, replay=r1)
+        for _ in range(k):
+            e2.step(None, replay=r2)
+        assert torch.equal(e1.board, e2.board) and torch.equal(e1.meta, e2.meta), k
+    assert torch.equal(e1.ep, e2.ep)
+    assert int(e1.ep[:, 0].max()) > 0  # some boards finished (and stayed finished)
+    for name in ["s", "s2", "a", "r", "d", "count"]:
+        assert torch.equal(getattr(r1, name), getattr(r2, name)), name
+
+
 def _rollout_ring(g2048, n, k, rb, seed=31):
     env = g2048.VecEnv2048(n, seed=seed, device=DEV)
     env.step(None, replay=rb)  # odd start
