@@ -98,6 +98,70 @@ __global__ __launch_bounds__(256) void kfma(double* out, int iters) {
     for (int k = 0; k < 8; ++k) s += x[k];
     out[blockIdx.x * 256 + l] = s;
 }
+// co-issue probes: (a) 2 waves per SIMD, one running 8 f64 MFMA chains, the other 8 v_fma_f64
+// chains (fiters FMAs per chain); (b) one wave interleaving 8 MFMA chains with 8 FMA chains
+__global__ __launch_bounds__(512) void kmix2(double* out, int iters, int fiters) {
+    const int l = threadIdx.x, w = l >> 6;
+    double a = 1.0 + l * 1e-9, b = 1.0 - l * 1e-9;
+    double s = 0;
+    if (w < 4) {
+        d4 c[8];
+        for (int k = 0; k < 8; ++k) c[k] = d4{0, 0, 0, 0};
+        for (int it = 0; it < iters; ++it) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[k], 0, 0, 0);
+        }
+        for (int k = 0; k < 8; ++k) s += c[k][k & 3];
+    } else {
+        double x[8];
+        for (int k = 0; k < 8; ++k) x[k] = k;
+        for (int it = 0; it < fiters; ++it) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = fma(a, x[k], b);
+        }
+        for (int k = 0; k < 8; ++k) s += x[k];
+    }
+    out[blockIdx.x * 512 + l] = s;
+}
+__global__ __launch_bounds__(256) void kmix1(double* out, int iters) {
+    const int l = threadIdx.x;
+    double a = 1.0 + l * 1e-9, b = 1.0 - l * 1e-9;
+    d4 c[8];
+    double x[8];
+    for (int k = 0; k < 8; ++k) { c[k] = d4{0, 0, 0, 0}; x[k] = k; }
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            c[k] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[k], 0, 0, 0);
+            x[k] = fma(a, x[k], b);
+        }
+    }
+    double s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k][k & 3] + x[k];
+    out[blockIdx.x * 256 + l] = s;
+}
+// 8 chains at one wave per SIMD with the accumulators pinned by inline asm: in AGPRs ("+a") or in
+// VGPRs ("+v") -- the compiler-generated kmfma8 loop above copies its accumulators between the
+// register files every iteration, which is what capped it at 47.6 TF
+template <bool kAgpr>
+__global__ __launch_bounds__(256) void kmfma_pinned(double* out, int iters) {
+    const int l = threadIdx.x;
+    double a = 1.0 + l * 1e-9, b = 1.0 - l * 1e-9;
+    d4 c[8];
+    for (int k = 0; k < 8; ++k) c[k] = d4{0, 0, 0, 0};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if constexpr (kAgpr)
+                asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+a"(c[k]) : "v"(a), "v"(b));
+            else
+                asm volatile("v_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(c[k]) : "v"(a), "v"(b));
+        }
+    }
+    double s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k][k & 3];
+    out[blockIdx.x * 256 + l] = s;
+}
 struct Tm { hipEvent_t a, b; };
 int main2() {
     double* d;
@@ -106,6 +170,42 @@ int main2() {
     (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     for (int rep = 0; rep < 2; ++rep) {
         const int it = 20000;
+        for (int pin = 0; pin < 2; ++pin) {
+            float ms;
+            (void)hipEventRecord(e0);
+            if (pin) kmfma_pinned<true><<<1024, 256>>>(d, it / 2);
+            else kmfma_pinned<false><<<1024, 256>>>(d, it / 2);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double fm = 1024.0 * 4 * (it / 2) * 8 * 2048.0;
+            printf("mfma f64 8 chains, accumulators pinned in %s: %.3f ms  %.1f TF\n",
+                   pin ? "AGPRs" : "VGPRs", ms, fm / ms / 1e9);
+        }
+        for (int fit = 0; fit <= 4 * it; fit += it) {
+            float ms;
+            (void)hipEventRecord(e0);
+            kmix2<<<1024, 512>>>(d, it / 2, fit);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double fm = 1024.0 * 4 * (it / 2) * 8 * 2048.0;
+            const double ff = 1024.0 * 256 * (double)fit * 8 * 2.0;
+            printf("mix2 (MFMA wave + FMA wave per SIMD, fma iters %d): %.3f ms  MFMA %.1f + VALU %.1f = %.1f TF\n",
+                   fit, ms, fm / ms / 1e9, ff / ms / 1e9, (fm + ff) / ms / 1e9);
+        }
+        {
+            float ms;
+            (void)hipEventRecord(e0);
+            kmix1<<<1024, 256>>>(d, it / 2);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double fm = 1024.0 * 4 * (it / 2) * 8 * 2048.0;
+            const double ff = 1024.0 * 256 * (double)(it / 2) * 8 * 2.0;
+            printf("mix1 (one wave, MFMA + FMA interleaved): %.3f ms  MFMA %.1f + VALU %.1f TF\n", ms,
+                   fm / ms / 1e9, ff / ms / 1e9);
+        }
         (void)hipEventRecord(e0);
         kmfma<<<1024, 256>>>(d, it);
         (void)hipEventRecord(e1);
