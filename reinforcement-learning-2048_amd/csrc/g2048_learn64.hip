@@ -5,9 +5,9 @@
 // (float64) and the target sync applied in place.  train_step: src/dqn_lib.py:119-164; the
 // target sync: :227-228.
 //
-// Tile = 64 minibatch rows per 256-thread workgroup, VALU float64 (on MI355X the f64 vector FMA
-// rate equals the f64 MFMA rate, and at 1 280 MAC per row the update is latency-bound, not
-// FLOP-bound).  Every output element has one owner thread and every sum runs in a fixed order,
+// Tile = 64 minibatch rows per 256-thread workgroup, VALU float64 (57 TF of f64 vector FMA
+// against 74 TF of f64 MFMA with VGPR accumulators, and at 1 280 MAC per row the update is
+// latency-bound, not FLOP-bound).  Every output element has one owner thread and every sum runs in a fixed order,
 // so the update is run-to-run bitwise reproducible:
 //   h[s][j] = relu(b1[j] + W1[j] . x[s])        thread (j = t & 63, rows 16 (t >> 6) ..)
 //   Q[s][a] = b2[a] + W2[a] . h[s]              thread (s = t >> 2, a = t & 3)
