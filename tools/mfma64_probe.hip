@@ -162,6 +162,27 @@ __global__ __launch_bounds__(256) void kmfma_pinned(double* out, int iters) {
     for (int k = 0; k < 8; ++k) s += c[k][k & 3];
     out[blockIdx.x * 256 + l] = s;
 }
+// the same for f32 v_mfma_f32_16x16x4_f32 (8 chains, accumulators pinned)
+typedef float f4 __attribute__((ext_vector_type(4)));
+template <bool kAgpr>
+__global__ __launch_bounds__(256) void kmfma32_pinned(double* out, int iters) {
+    const int l = threadIdx.x;
+    float a = 1.0f + l * 1e-6f, b = 1.0f - l * 1e-6f;
+    f4 c[8];
+    for (int k = 0; k < 8; ++k) c[k] = f4{0, 0, 0, 0};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if constexpr (kAgpr)
+                asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+a"(c[k]) : "v"(a), "v"(b));
+            else
+                asm volatile("v_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(c[k]) : "v"(a), "v"(b));
+        }
+    }
+    float s = 0;
+    for (int k = 0; k < 8; ++k) s += c[k][k & 3];
+    out[blockIdx.x * 256 + l] = s;
+}
 struct Tm { hipEvent_t a, b; };
 int main2() {
     double* d;
@@ -180,6 +201,18 @@ int main2() {
             (void)hipEventElapsedTime(&ms, e0, e1);
             const double fm = 1024.0 * 4 * (it / 2) * 8 * 2048.0;
             printf("mfma f64 8 chains, accumulators pinned in %s: %.3f ms  %.1f TF\n",
+                   pin ? "AGPRs" : "VGPRs", ms, fm / ms / 1e9);
+        }
+        for (int pin = 0; pin < 2; ++pin) {
+            float ms;
+            (void)hipEventRecord(e0);
+            if (pin) kmfma32_pinned<true><<<1024, 256>>>(d, it);
+            else kmfma32_pinned<false><<<1024, 256>>>(d, it);
+            (void)hipEventRecord(e1);
+            (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            const double fm = 1024.0 * 4 * it * 8 * 2048.0;
+            printf("mfma f32 16x16x4 8 chains, accumulators pinned in %s: %.3f ms  %.1f TF\n",
                    pin ? "AGPRs" : "VGPRs", ms, fm / ms / 1e9);
         }
         for (int fit = 0; fit <= 4 * it; fit += it) {
