@@ -488,6 +488,12 @@ __global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const 
 // step spends no VALU on addresses.  Used when every section of the ring is below 4 GiB.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// tools/prof_roll.hip: per-pair s_memtime ticks of a few waves (no-op in the library)
+#ifndef G2048_ROLL_TICK
+#define G2048_ROLL_TICK(np)
+#define G2048_ROLL_MARK(k)
+#endif
+
 // g2048_env_rollout: k_steps random-policy steps of every board with the board, score, moves and
 // episode counters held in registers; step t of the launch draws its two words from the Philox
 // block of its step pair (one block per two steps, see random_block) and appends (s, a, r, s', d)
@@ -503,6 +509,7 @@ template <bool kRing, bool kBuf, bool kSum>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5 : 6))) void k_rollout(StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= A.n) return;
+    G2048_ROLL_MARK(0);
     const uint64_t t0 = load_clock(A.clock, i);
     Board b = load_board(A.board[i]);
     uint2 m = A.meta[i];
@@ -591,7 +598,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
             ++pair;
             --rest;
         }
+        G2048_ROLL_MARK(1);
         for (int np = rest >> 1; np > 0; --np, ++pair) {  // a down-counter: one SALU op less
+            G2048_ROLL_TICK(np);
             if constexpr (kBuf) asm volatile("" : "+s"(rw));  // one SGPR quad for the descriptor
             const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
             one(lean, blk.x, blk.y, 2u * pair);
@@ -604,6 +613,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     };
     if (!A.log && autoreset) run(std::true_type{});
     else run(std::false_type{});
+    G2048_ROLL_MARK(2);
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;
@@ -615,6 +625,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     if ((i & 63) == 0) A.clock[i >> 6] = t1;
     if constexpr (kSum) A.reward_sum[i] += rsum;
     if (kRing && i == 0) bump_count(A, t1);
+    G2048_ROLL_MARK(3);
 }
 
 __global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint2* meta, int64_t n,
