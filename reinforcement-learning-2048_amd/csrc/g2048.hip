@@ -33,6 +33,7 @@
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
 #include "g2048_common.hpp"
+#include "g2048_roll.hpp"
 
 using namespace g2048;
 
@@ -628,6 +629,132 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     G2048_ROLL_MARK(3);
 }
 
+// The headline instance of g2048_env_rollout -- ring in one buffer window, auto-reset on, no
+// episode log -- with the step of g2048_roll.hpp: same results as k_rollout<true, true, kSum>
+// (tested), fewer issue turns per step.  Each workgroup stages the direction-selector table
+// (kDirNet, 128 B) in LDS; a step reads its action's two selector quads from it.
+template <bool kSum>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5 : 6))) void k_rollout_lean(StepArgs A) {
+    __shared__ uint4 s_dir[8];
+    if (threadIdx.x < 8)
+        s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.n) return;
+    const uint64_t t0 = load_clock(A.clock, i);
+    Board b = load_board(A.board[i]);
+    uint2 m = A.meta[i];
+    uint4 ep = A.ep[i];
+    const uint64_t gid = A.board_offset + (uint64_t)i;
+    const uint32_t p4 = A.p4_thresh, p4_16 = p4_thresh16(A.p4_thresh);
+    long long rsum = 0;
+    const uint32_t row = (uint32_t)ring_row(t0, A.rb.rows);
+    const uint32_t cap32 = (uint32_t)A.rb.capacity, n32 = (uint32_t)A.n;
+    uint32_t soff = row * n32;
+    __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(A.rb.win, 0, (int)A.rb.win_bytes, 0x00020000);
+    const uint32_t lane = (uint32_t)i;
+    const uint32_t v_s = A.rb.o_s + 16u * lane, v_s2 = A.rb.o_s2 + 16u * lane;
+    const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
+    const uint32_t ep0 = ep.x;
+    Board last = b;
+    // one transition with the words (wa, wb) and the action's selector quads (F, I)
+    auto one = [&](uint32_t wa, uint32_t wb, const uint4& F, const uint4& I) {
+        G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s, soff * 16u,
+                                               0);
+        bool done;
+        const uint32_t r = lean_step(b, wa, wb, p4, F, I, done);
+        m.x += r;
+        m.y += 1u;
+        if constexpr (kSum) rsum += r;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2, soff * 16u,
+                                               0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), rw, v_a, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(r, rw, v_r, soff * 4u, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, v_d, soff, 0);
+        soff = soff + n32 == cap32 ? 0u : soff + n32;
+        // a wave-uniform branch whose body is selects: every value keeps its registers (a
+        // lane-masked `if (done)` made hipcc copy the board and counters through phi moves, and
+        // a v_mov costs a full issue turn)
+        G2048_MARK(reset, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
+        if (__builtin_amdgcn_ballot_w64(done) != 0u) {
+            const Board f = fresh_board_random(wa, wb, p4_16);
+            last.r0 = done ? b.r0 : last.r0;
+            last.r1 = done ? b.r1 : last.r1;
+            last.r2 = done ? b.r2 : last.r2;
+            last.r3 = done ? b.r3 : last.r3;
+            ep.x += done ? 1u : 0u;
+            ep.y = done ? m.x : ep.y;
+            ep.z = done ? m.y : ep.z;
+            b.r0 = done ? f.r0 : b.r0;
+            b.r1 = done ? f.r1 : b.r1;
+            b.r2 = done ? f.r2 : b.r2;
+            b.r3 = done ? f.r3 : b.r3;
+            m.x = done ? 0u : m.x;
+            m.y = done ? 0u : m.y;
+        }
+    };
+    auto sel = [&](uint32_t wa, uint4& F, uint4& I) {
+        const uint32_t a2 = (wa >> 30) * 2u;
+        F = s_dir[a2];
+        I = s_dir[a2 + 1u];
+    };
+    const int K = A.k_steps > 0 ? A.k_steps : 0;
+    uint64_t pair = t0 >> 1;
+    int rest = K;
+    uint4 F, I, F2, I2;
+    if (rest > 0 && (t0 & 1u)) {
+        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+        sel(blk.z, F, I);
+        one(blk.z, blk.w, F, I);
+        ++pair;
+        --rest;
+    }
+    // software-pipelined by one pair: the selector reads of pair p are in flight while the block
+    // of pair p + 1 is drawn (the loop draws up to two blocks it does not use); two pairs per
+    // iteration, so the blocks alternate between two register quads instead of being copied
+    uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
+    auto pair_of = [&](const uint4& cur, uint4& nxt, uint64_t p_next) {
+        G2048_MARK(selectors, "+v"(cur.x), "+v"(cur.z));
+        sel(cur.x, F, I);
+        sel(cur.z, F2, I2);
+        G2048_MARK(philox, "+v"(F.x), "+v"(F2.x));
+        nxt = random_block(A.seed_lo, A.seed_hi, gid, p_next);
+        G2048_MARK(step, "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
+        one(cur.x, cur.y, F, I);
+        one(cur.z, cur.w, F2, I2);
+    };
+    int np = rest >> 1;
+    for (; np >= 2; np -= 2, pair += 2) {
+        asm volatile("" : "+s"(rw));
+        uint4 b1;
+        pair_of(blk, b1, pair + 1u);
+        pair_of(b1, blk, pair + 2u);
+    }
+    if (np) {
+        uint4 b1;
+        pair_of(blk, b1, pair + 1u);
+        blk = b1;
+        ++pair;
+    }
+    if (rest & 1) {
+        sel(blk.x, F, I);
+        one(blk.x, blk.y, F, I);
+    }
+    const uint64_t t1 = t0 + (uint64_t)K;
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (ep.x != ep0) {
+        ep.w = max_exp(last);
+        A.ep[i] = ep;
+        if (A.qsum) A.qsum[i] = 0.0;
+    }
+    if ((i & 63) == 0) A.clock[i >> 6] = t1;
+    if constexpr (kSum) A.reward_sum[i] += rsum;
+    if (i == 0) bump_count(A, t1);
+}
+
 __global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint2* meta, int64_t n,
                                                   uint64_t board_offset, uint32_t seed_lo,
                                                   uint32_t seed_hi, uint32_t p4_thresh,
@@ -1211,6 +1338,10 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
     if (!rb) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<false, false, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<false, false, false>), grid, block, 0, st, A);
+    } else if (A.rb.win_bytes && !A.log && !(A.flags & G2048_NO_AUTORESET)) {
+        // the headline case: g2048_roll.hpp's step
+        if (reward_sum) hipLaunchKernelGGL((k_rollout_lean<true>), grid, block, 0, st, A);
+        else hipLaunchKernelGGL((k_rollout_lean<false>), grid, block, 0, st, A);
     } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<true, true, false>), grid, block, 0, st, A);

@@ -121,12 +121,12 @@ def make_net(kind: str, dtype=torch.float32, device=None) -> nn.Module:
     return NETS[kind][0]().to(dtype=dtype, device=device)
 
 
-def det_init(model: nn.Module, phase: float) -> nn.Module:
-    """Deterministic weights p.flat[k] = sin(1.3 k + phase) / sqrt(fan_in) -- the pattern the
+def det_init(model: nn.Module, phase: float, freq: float = 1.3) -> nn.Module:
+    """Deterministic weights p.flat[k] = sin(freq k + phase) / sqrt(fan_in) -- the pattern the
     golden learner fixtures were generated with (tests/golden/gen_goldens.py)."""
     with torch.no_grad():
         for p in model.parameters():
             k = torch.arange(p.numel(), dtype=torch.float64)
             fan_in = int(math.prod(p.shape[1:])) if p.dim() > 1 else 4
-            p.copy_((torch.sin(1.3 * k + phase) / math.sqrt(fan_in)).reshape(p.shape).to(p.dtype))
+            p.copy_((torch.sin(freq * k + phase) / math.sqrt(fan_in)).reshape(p.shape).to(p.dtype))
     return model

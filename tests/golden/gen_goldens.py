@@ -23,6 +23,8 @@ Fixtures (all boards are stored as log2 exponents, 0 = empty, row-major):
   learner_<net>.npz    dqn_lib.train_step on a seeded buffer, B=512, deterministic weights
                        (src/dqn_lib.py:119-164) + restated intermediates, correct-order
                        grads and one Adam step (lr 1e-2)
+  learner_{conv,dense64}_vanilla.npz  the same with use_double_dqn=False (src/dqn_lib.py:133-144)
+  learner_dense_b5000.npz  dense-ref (double_dqn_dense.py) at B=5000, BASELINE configs[0]'s batch
 """
 from __future__ import annotations
 
@@ -270,13 +272,13 @@ def gen_egreedy_nonfinite(n=3000, seed=11):
 
 
 # ---------------------------------------------------------------- learner_<net>.npz
-def det_init(model, phase: float):
-    """Deterministic weights: p.flat[k] = sin(1.3 k + phase) / sqrt(fan_in)."""
+def det_init(model, phase: float, freq: float = 1.3):
+    """Deterministic weights: p.flat[k] = sin(freq k + phase) / sqrt(fan_in)."""
     with torch.no_grad():
         for p in model.parameters():
             k = torch.arange(p.numel(), dtype=torch.float64)
             fan_in = int(np.prod(p.shape[1:])) if p.dim() > 1 else 4
-            p.copy_((torch.sin(1.3 * k + phase) / math.sqrt(fan_in)).reshape(p.shape).to(p.dtype))
+            p.copy_((torch.sin(freq * k + phase) / math.sqrt(fan_in)).reshape(p.shape).to(p.dtype))
 
 
 def make_net(kind):
@@ -309,11 +311,15 @@ def build_buffer(n_trans=2000, seed=99):
     return buf, dict(buf_s=s, buf_a=a, buf_r=r, buf_s2=s2, buf_d=d)
 
 
-def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234):
+def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234, use_double=True,
+                name=None, tgt_phase=0.2, freq=1.3):
+    """One reference train_step (src/dqn_lib.py:119-164) on a seeded minibatch -> learner_<name>.npz.
+    use_double=False takes the vanilla branch (:133-144): y = r + (1-d)*gamma*max_a Q_tgt(s')."""
+    name = name or kind
     model, to_tensor, extract = make_net(kind)
     target = copy.deepcopy(model)
-    det_init(model, 0.5)
-    det_init(target, 0.2)
+    det_init(model, 0.5, freq)
+    det_init(target, tgt_phase, freq)
     init_params = [p.detach().clone() for p in model.parameters()]
     loss_fn = torch.nn.MSELoss(reduction="sum")
     opt = torch.optim.Adam(model.parameters(), lr=lr)
@@ -321,7 +327,7 @@ def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234):
     np.random.seed(seed)
     idx = np.random.randint(len(buf), size=B)  # src/dqn_lib.py:68 (re-drawn below)
     np.random.seed(seed)
-    loss_ref = dqn_lib.train_step(B, gamma, model, target, buf, loss_fn, opt, "cpu", True,
+    loss_ref = dqn_lib.train_step(B, gamma, model, target, buf, loss_fn, opt, "cpu", use_double,
                                   to_tensor, extract)
     # F1: the reference's zero_grad-before-step leaves params untouched
     compat_unchanged = all(torch.equal(p, q) for p, q in zip(model.parameters(), init_params))
@@ -339,7 +345,10 @@ def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234):
         q_on_s2 = model(s2)
         a_star = torch.argmax(q_on_s2, dim=1)
         q_tgt_s2 = target(s2)
-        y = (r + (1 - d) * gamma * q_tgt_s2.gather(1, a_star[:, None])[:, 0]).double()
+        if use_double:
+            y = (r + (1 - d) * gamma * q_tgt_s2.gather(1, a_star[:, None])[:, 0]).double()
+        else:
+            y = r + ((1 - d) * gamma * torch.max(q_tgt_s2, 1).values)
     q_on_s = model(s)
     q = q_on_s.gather(1, a[:, None])[:, 0]
     loss = ((q - y) ** 2).sum()
@@ -359,6 +368,10 @@ def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234):
                a_star=a_star.numpy(), y=y.numpy(), q=q.detach().numpy(),
                n_params=np.int64(sum(p.numel() for p in model.parameters())),
                param_shapes=np.array(json.dumps([list(p.shape) for p in model.parameters()])))
+    if not use_double:  # (the keys are absent from the Double-DQN fixtures, which predate them)
+        out["use_double_dqn"] = np.bool_(False)
+        out["tgt_phase"] = np.float64(tgt_phase)
+        out["init_freq"] = np.float64(freq)
     g, pa = flat(grads), flat(after)
     if g.size <= 50000:
         out.update(grads=g, params_after=pa)
@@ -368,8 +381,8 @@ def gen_learner(kind, buf, bufarrs, B=512, gamma=0.8, lr=1e-2, seed=1234):
                    grad_sum=np.float64(g.sum()), grad_sumsq=np.float64((g * g).sum()),
                    params_after_sum=np.float64(pa.sum()))
     out.update(bufarrs)
-    np.savez_compressed(os.path.join(OUT, f"learner_{kind}.npz"), **out)
-    print(f"learner {kind}: loss {float(loss_ref):.6f}")
+    np.savez_compressed(os.path.join(OUT, f"learner_{name}.npz"), **out)
+    print(f"learner {name}: loss {float(loss_ref):.6f}")
 
 
 if __name__ == "__main__":
@@ -382,3 +395,12 @@ if __name__ == "__main__":
     buf, arrs = build_buffer()
     for k in ["conv", "dense", "dense64"]:
         gen_learner(k, buf, arrs)
+    # round 3: the vanilla-DQN branch (src/dqn_lib.py:133-144) and BASELINE configs[0]'s batch
+    # (double_dqn_dense.py:17, batch_size=5000; rows drawn with replacement from the 2000)
+    # (weights at another frequency / target phase, so that max_a Q_tgt(s') differs from
+    # Q_tgt(s', argmax Q_on(s')) on most rows: with the Double-DQN fixtures' weights the two nets'
+    # argmax agree on every row, and a vanilla fixture would not tell the branches apart)
+    gen_learner("conv", buf, arrs, use_double=False, name="conv_vanilla", tgt_phase=2.9, freq=3.7)
+    gen_learner("dense64", buf, arrs, use_double=False, name="dense64_vanilla", tgt_phase=2.9,
+                freq=3.7)
+    gen_learner("dense", buf, arrs, B=5000, name="dense_b5000")

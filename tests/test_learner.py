@@ -30,10 +30,53 @@ def batch(g, device="cpu", dtype=torch.float64):
     return s, t(g["buf_a"][idx]), t(g["buf_r"][idx]).to(dtype), s2, t(g["buf_d"][idx]).to(dtype)
 
 
-def nets(net, device="cpu"):
-    m = det_init(make_net(net, torch.float64, device), 0.5)
-    tg = det_init(make_net(net, torch.float64, device), 0.2)
+def nets(net, device="cpu", g=None):
+    """The fixture's weights: online phase 0.5, target phase 0.2 (or the fixture's tgt_phase),
+    frequency 1.3 (or its init_freq)."""
+    freq = float(g["init_freq"]) if g is not None and "init_freq" in g else 1.3
+    tph = float(g["tgt_phase"]) if g is not None and "tgt_phase" in g else 0.2
+    m = det_init(make_net(net, torch.float64, device), 0.5, freq)
+    tg = det_init(make_net(net, torch.float64, device), tph, freq)
     return m, tg
+
+
+# round 3: the vanilla-DQN branch (src/dqn_lib.py:133-144: y = r + (1-d)*gamma*max_a Q_tgt(s')) on
+# weights where it differs from Double DQN on most rows, and dense-ref at BASELINE configs[0]'s
+# batch of 5000 (src/configs/double_dqn_dense.py:17)
+EXTRA = [("conv_vanilla", "conv", False), ("dense64_vanilla", "dense64", False),
+         ("dense_b5000", "dense", True)]
+
+
+@pytest.mark.parametrize("name,net,double", EXTRA)
+def test_vanilla_and_b5000_match_reference(golden_dir, name, net, double):
+    g = load(golden_dir, name)
+    assert bool(g["use_double_dqn"]) == double if "use_double_dqn" in g else double
+    m, tg = nets(net, g=g)
+    s, a, r, s2, d = batch(g)
+    if net == "conv":
+        s, s2 = dqn_lib.extract_samples_conv(s), dqn_lib.extract_samples_conv(s2)
+    loss, q, y = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]), use_double_dqn=double)
+    assert abs(float(loss) - float(g["loss_ref"])) <= ATOL + 1e-14 * abs(float(g["loss_ref"]))
+    np.testing.assert_allclose(q.detach().numpy(), g["q"], rtol=1e-12, atol=ATOL)
+    np.testing.assert_allclose(y.numpy(), g["y"], rtol=1e-12, atol=ATOL)
+    if not double:  # the fixture really exercises the vanilla branch
+        _, _, y_dbl = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]), use_double_dqn=True)
+        assert (y_dbl.numpy() != g["y"]).mean() > 0.9
+    opt = torch.optim.Adam(m.parameters(), lr=float(g["lr"]))
+    opt.zero_grad()
+    loss.backward()
+    grads = torch.cat([p.grad.reshape(-1) for p in m.parameters()]).numpy()
+    opt.step()
+    after = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).numpy()
+    if "grads" in g:
+        np.testing.assert_allclose(grads, g["grads"], rtol=1e-9, atol=1e-9 * np.abs(g["grads"]).max())
+        np.testing.assert_allclose(after, g["params_after"], rtol=1e-12, atol=1e-12)
+    else:
+        sel = g["grad_sel"]
+        np.testing.assert_allclose(grads[sel], g["grads_sampled"], rtol=1e-9,
+                                   atol=1e-9 * np.abs(g["grads_sampled"]).max())
+        np.testing.assert_allclose(grads.sum(), g["grad_sum"], rtol=1e-9)
+        np.testing.assert_allclose(after[sel], g["params_after_sampled"], rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.parametrize("net", NETS)

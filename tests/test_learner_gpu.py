@@ -23,6 +23,16 @@ def fixture(golden_dir, net):
     return np.load(os.path.join(golden_dir, f"learner_{net}.npz"))
 
 
+def fixture_nets(g, net, dtype=torch.float64):
+    """Online / target weights of a fixture (tests/golden/gen_goldens.py det_init)."""
+    from g2048.nets import det_init, make_net
+
+    freq = float(g["init_freq"]) if "init_freq" in g else 1.3
+    tph = float(g["tgt_phase"]) if "tgt_phase" in g else 0.2
+    return (det_init(make_net(net, dtype, DEV), 0.5, freq),
+            det_init(make_net(net, dtype, DEV), tph, freq))
+
+
 def loaded_replay(G, g):
     rb = G.ReplayBuffer(len(g["buf_a"]), device=DEV)
     rb.load(g["buf_s"], g["buf_a"], g["buf_r"], g["buf_s2"], g["buf_d"])
@@ -332,3 +342,65 @@ def test_fused_f32_matches_reference(G, golden_dir, net):
         a, b = grad[off:off + k], gref[off:off + k]
         assert np.linalg.norm(a - b) <= 1e-3 * max(np.linalg.norm(b), 1e-12), (off, k)
         off += k
+
+
+@pytest.mark.parametrize("net", ["dense64", "conv"])
+def test_fused_f64_vanilla_matches_reference(G, golden_dir, net):
+    """The fused float64 updates on the vanilla-DQN branch (use_double_dqn=False,
+    src/dqn_lib.py:133-144: y = r + (1-d)*gamma*max_a Q_tgt(s')) against the reference-run
+    fixture learner_<net>_vanilla.npz, whose weights make the branch differ from Double DQN on
+    most rows: loss within 1e-6 absolute, y to 1e-12, gradient and one Adam step to 1e-10."""
+    from g2048.learner import DQNLearner
+    from g2048.nets import det_init
+
+    g = fixture(golden_dir, f"{net}_vanilla")
+    assert not bool(g["use_double_dqn"])
+    rb = loaded_replay(G, g)
+    idx = torch.from_numpy(g["idx"]).to(DEV)
+    m, _ = fixture_nets(g, net)
+    L = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=len(idx), lr=float(g["lr"]),
+                   target_sync_every=0, model=m, sampler=lambda B, r: idx, use_double_dqn=False)
+    assert L.fused and L.f64 and L.kind == net
+    det_init(L.target, float(g["tgt_phase"]), float(g["init_freq"]))
+    L.update()
+    torch.cuda.synchronize()
+    ref = float(g["loss_ref"])
+    assert abs(float(L.last_loss) - ref) <= 1e-6 + 1e-13 * abs(ref), (float(L.last_loss), ref)
+    np.testing.assert_allclose(L._y.cpu().numpy(), g["y"], rtol=1e-12, atol=1e-9)
+    gref = g["grads"]
+    np.testing.assert_allclose(L.grad_flat.cpu().numpy(), gref, rtol=1e-10,
+                               atol=1e-10 * max(1.0, float(np.abs(gref).max())))
+    after = torch.cat([p.detach().reshape(-1) for p in L.model.parameters()]).cpu().numpy()
+    np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("name,net,double", [("conv_vanilla", "conv", False),
+                                             ("dense64_vanilla", "dense64", False),
+                                             ("dense_b5000", "dense", True)])
+def test_torch_path_vanilla_and_b5000_match_reference(G, golden_dir, name, net, double):
+    """The torch-ROCm float64 learner path (HIP gather + encode, then torch) on the vanilla-DQN
+    fixtures and on dense-ref at BASELINE configs[0]'s batch of 5000
+    (src/configs/double_dqn_dense.py:17): loss within 1e-6 absolute, y and Q to 1e-12."""
+    from g2048 import dqn_lib
+
+    g = fixture(golden_dir, name)
+    rb = loaded_replay(G, g)
+    m, tg = fixture_nets(g, net)
+    idx = torch.from_numpy(g["idx"]).to(DEV)
+    ext = dqn_lib.extract_samples_conv if net == "conv" else dqn_lib.extract_samples_dense
+    s, a, r, s2, d = dqn_lib.sample_experiences(len(idx), rb, DEV, None, ext, idx=idx)
+    loss, q, y = dqn_lib.dqn_loss(m, tg, s, a, r, s2, d, float(g["gamma"]), use_double_dqn=double)
+    ref = float(g["loss_ref"])
+    assert abs(float(loss.detach()) - ref) <= 1e-6 + 1e-13 * abs(ref), (float(loss.detach()), ref)
+    np.testing.assert_allclose(q.detach().cpu().numpy(), g["q"], rtol=1e-12, atol=1e-6)
+    np.testing.assert_allclose(y.cpu().numpy(), g["y"], rtol=1e-12, atol=1e-6)
+    opt = torch.optim.Adam(m.parameters(), lr=float(g["lr"]))
+    l2 = dqn_lib.train_step(len(idx), float(g["gamma"]), m, tg, rb, None, opt, DEV,
+                            use_double_dqn=double, extract_samples_function=ext, idx=idx)
+    assert abs(float(l2) - ref) <= 1e-6 + 1e-13 * abs(ref)
+    after = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+    if "params_after" in g:
+        np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
+    else:
+        np.testing.assert_allclose(after[g["grad_sel"]], g["params_after_sampled"], rtol=1e-10,
+                                   atol=1e-10)

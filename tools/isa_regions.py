@@ -1,0 +1,59 @@
+"""Instruction counts per region of the rollout kernel's lean loop, from a marker build:
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -S -DG2048_ISA_MARKS \\
+          tools/rollexp.hip -o /tmp/roll_marks.s
+    python tools/isa_regions.py /tmp/roll_marks.s
+Counts every instruction between consecutive ';; region X' markers inside the pair loop (both
+steps of a pair are summed, so the per-step figures are half), split into VALU / SALU / VMEM / LDS
+/ other.  The markers fix the instruction order, so the counts describe the marker build; the
+timed library is built without them."""
+import re
+import sys
+from collections import Counter, defaultdict
+
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0EEEvNS_8StepArgsE"
+
+
+def kind(op):
+    if op.startswith(("buffer_", "global_")):
+        return "VMEM"
+    if op.startswith("ds_"):
+        return "LDS"
+    if op.startswith(("s_waitcnt", "s_nop")):
+        return "wait/nop"
+    if op.startswith(("s_cbranch", "s_branch")):
+        return "branch"
+    if op.startswith("s_"):
+        return "SALU"
+    return "VALU"
+
+
+def main(path):
+    lines = open(path).read().split("\n")
+    st = next(i for i, l in enumerate(lines) if l.startswith(KERNEL + ":"))
+    en = next(i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    f = lines[st:en]
+    head = next(i for i, l in enumerate(f) if "Inner Loop Header" in l)
+    # the loop body: from the header to the back-edge branch to it
+    label = f[head].split(":")[0]
+    tail = max(i for i, l in enumerate(f) if label in l and ("s_branch" in l or "s_cbranch" in l))
+    region = "loop_head"
+    per = defaultdict(Counter)
+    for l in f[head:tail + 1]:
+        t = l.strip()
+        m = re.match(r";; region (\w+)", t)
+        if m:
+            region = m.group(1)
+            continue
+        if not t or t.startswith((";", ".")) or t.endswith(":"):
+            continue
+        per[region][kind(t.split()[0])] += 1
+    tot = Counter()
+    print(f"{'region':14s} {'all':>5s}  " + "  ".join(f"{k:>8s}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
+    for r, c in per.items():
+        tot.update(c)
+        print(f"{r:14s} {sum(c.values()):5d}  " + "  ".join(f"{c[k]:8d}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
+    print(f"{'pair total':14s} {sum(tot.values()):5d}  " + "  ".join(f"{tot[k]:8d}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
