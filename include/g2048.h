@@ -21,10 +21,20 @@
  *  - Randomness is counter-based Philox4x32-10.  Board g (global id = board_offset + i) owns
  *    rocRAND philox4x32_10 subsequence g: its step draw at step t is the 4-word block
  *    rocrand_init(seed, g, 4t) would return first (domain bits 30-31 of the subsequence word
- *    select step / random-policy / explicit-reset / sampler draws).  The random policy
- *    (actions == NULL, g2048_env_rollout) spends half a block per step: step t takes words
- *    (x, y) (t even) or (z, w) (t odd) of block t >> 1 of the random-policy domain.  No per-lane
- *    RNG state in HBM: the counter t is the env's step clock (one u64 per 64 boards).
+ *    select step / random-policy / explicit-reset / sampler draws).  No per-lane RNG state in
+ *    HBM: the counter t is the env's step clock (one u64 per 64 boards).
+ *  - The random policy (actions == NULL, g2048_env_rollout), ABI v3: step t takes ONE word
+ *    w = word (t & 3) of block t >> 2 of the random-policy domain (a block per four steps).
+ *    Action w >> 30; a 4 spawns iff bit 29 is set (p = 0.5, src/board.py:12,49); the spawn cell
+ *    is the k-th empty cell of the slid board, k = floor((w << 3) * n / 2^32), in move-space
+ *    line-major order (up/down: column j = 0..3, then rows from the top / bottom; left/right:
+ *    row j, then columns from the left / right) -- uniform over the empty cells like the
+ *    reference's np.random.choice.  A terminal step's auto-reset: a tile at cell (w >> 26) & 15
+ *    (a 4 iff bit 25), one at the k2-th of the other 15 cells in row-major order,
+ *    k2 = floor((w << 8) * 15 / 2^32) (a 4 iff bit 24).  With G2048_P4_10 the values come from
+ *    word t & 3 of the blocks at counters (t >> 2) | 2^63 (spawn, first reset tile) and
+ *    (t >> 2) | 2^62 (second reset tile): a 4 iff the word < round(0.1 * 2^32).
+ *    (ABI v2 drew half a block per step and spawned in row-major order.)
  */
 #ifndef G2048_H
 #define G2048_H
@@ -35,7 +45,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 2
+#define G2048_ABI_VERSION 3
 
 #ifndef G2048_API
 #define G2048_API __attribute__((visibility("default")))
@@ -167,7 +177,7 @@ G2048_API int g2048_env_step_inject(g2048_env* env, const uint8_t* actions_dev, 
  * env-only throughput).  Identical results to k_steps calls of g2048_env_step(actions=NULL).
  * reward_sum_dev (i64[n], accumulated, or NULL).  A step's transition is appended with five
  * stores whose per-step offset is a scalar (row * n), the board never leaves the VGPRs, and the
- * Philox block of a step pair is drawn once. */
+ * Philox block of a 4-step quad is drawn once. */
 G2048_API int g2048_env_rollout(g2048_env* env, int32_t k_steps, g2048_replay* rb, int64_t* reward_sum_dev,
                       void* stream);
 

@@ -191,19 +191,54 @@ static void fresh_board(uint8_t b[16], const uint32_t u[4], uint32_t flags) {
     spawn(b, u[2] << 4, u[0] << 2, flags);
 }
 
-/* Auto-reset of a terminal random-policy step from its two words (wa, wb) (include/g2048.h,
- * g2048_board.hpp random_block): a tile at cell (wa >> 26) & 15, then one at the k2-th of the 15
- * remaining empty cells in row-major order, k2 = floor((wa << 6) * 15 / 2^32); each a 4 iff its
- * 16-bit half of wb is below p4 * 2^16 (rounded). */
-static void fresh_board_random(uint8_t b[16], uint32_t wa, uint32_t wb, uint32_t flags) {
-    const uint32_t thresh = (flags & 1u) ? 429496730u : 2147483648u;
-    const uint32_t th16 = (thresh + 0x8000u) >> 16;
+/* ---- the random policy (actions = NULL, g2048_env_rollout): include/g2048.h ABI v3,
+ * csrc/g2048_roll.hpp.  Step t draws ONE word w = word (t & 3) of the random-policy block t >> 2
+ * (with G2048_P4_10 also v, v2 = word t & 3 of the blocks at counters (t >> 2) | 2^63 and
+ * (t >> 2) | 2^62).  Action w >> 30; spawn value 4 iff bit 29 (or v < 0.1 * 2^32); spawn cell the
+ * k-th empty cell, k = floor((w << 3) * n / 2^32), in MOVE-SPACE LINE-MAJOR order (line_cell);
+ * auto-reset: a tile at cell (w >> 26) & 15 (a 4 iff bit 25, or v below the threshold), one at the
+ * k2-th of the other 15 cells in row-major order, k2 = floor((w << 8) * 15 / 2^32) (a 4 iff bit
+ * 24, or v2 below the threshold). */
+
+/* Cell of position q along the move's line j (src/board.py:147-183 directions): up and down move
+ * along columns (line j = column j; q counts from the top / bottom), left and right along rows. */
+static int line_cell(int a, int j, int q) {
+    switch (a) {
+        case 0: return 4 * q + j;
+        case 1: return 4 * (3 - q) + j;
+        case 2: return 4 * j + q;
+        default: return 4 * j + (3 - q);
+    }
+}
+
+static uint32_t p4_thresh_of(uint32_t flags) {
+    return (flags & 1u) ? 429496730u : 2147483648u; /* G2048_P4_10: round(0.1 * 2^32) */
+}
+
+static void spawn_random(uint8_t b[16], int a, uint32_t w, uint32_t v, uint32_t flags) {
+    int n = 0;
+    for (int i = 0; i < 16; ++i) n += (b[i] == 0);
+    if (n == 0) return;
+    uint32_t k = (uint32_t)(((uint64_t)(uint32_t)(w << 3) * (uint64_t)n) >> 32);
+    const uint8_t e = (flags & 1u) ? (v < p4_thresh_of(flags) ? 2 : 1) : (uint8_t)(1 + ((w >> 29) & 1u));
+    for (int j = 0; j < 4; ++j)
+        for (int q = 0; q < 4; ++q) {
+            const int c = line_cell(a, j, q);
+            if (b[c] != 0) continue;
+            if (k == 0) { b[c] = e; return; }
+            --k;
+        }
+}
+
+static void fresh_board_random(uint8_t b[16], uint32_t w, uint32_t v, uint32_t v2, uint32_t flags) {
+    const int p410 = (flags & 1u) != 0;
+    const uint32_t th = p4_thresh_of(flags);
     memset(b, 0, 16);
-    b[(wa >> 26) & 15u] = ((wb & 0xFFFFu) < th16) ? 2 : 1;
-    uint32_t k = (uint32_t)(((uint64_t)(uint32_t)(wa << 6) * 15u) >> 32);
+    b[(w >> 26) & 15u] = p410 ? (v < th ? 2 : 1) : (uint8_t)(1 + ((w >> 25) & 1u));
+    uint32_t k = (uint32_t)(((uint64_t)(uint32_t)(w << 8) * 15u) >> 32);
     for (int i = 0; i < 16; ++i) {
         if (b[i] != 0) continue;
-        if (k == 0) { b[i] = ((wb >> 16) < th16) ? 2 : 1; return; }
+        if (k == 0) { b[i] = p410 ? (v2 < th ? 2 : 1) : (uint8_t)(1 + ((w >> 24) & 1u)); return; }
         --k;
     }
 }
@@ -236,11 +271,17 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
         uint32_t u[4];
         /* random policy: words (x, y) or (z, w) of block t/2 of domain 1; other modes: block t
          * of domain 0 (include/g2048.h) */
-        uint32_t wa = 0, wb = 0;
+        uint32_t w = 0, v = 0, v2 = 0;
         if (mode == 1) {
-            draw(e->seed, gid, 1u, t >> 1, u);
-            wa = (t & 1) ? u[2] : u[0];
-            wb = (t & 1) ? u[3] : u[1];
+            draw(e->seed, gid, 1u, t >> 2, u);
+            w = u[t & 3];
+            if (e->flags & 1u) {
+                uint32_t x[4];
+                draw(e->seed, gid, 1u, (t >> 2) | (1ull << 63), x);
+                v = x[t & 3];
+                draw(e->seed, gid, 1u, (t >> 2) | (1ull << 62), x);
+                v2 = x[t & 3];
+            }
         } else {
             draw(e->seed, gid, 0u, t, u);
         }
@@ -252,7 +293,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
         if (mode == 0 || mode == 4) {
             a = actions[i];
         } else if (mode == 1) {
-            a = (int)(wa >> 30);                     /* np.random.randint(4) */
+            a = (int)(w >> 30);                      /* np.random.randint(4) */
         } else {
             double eps_i = eps;
             if (eps_decay > 0) {  /* dqn_lib.py:184-188, ep = this board's episode count */
@@ -300,7 +341,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
                     if (si >= 0 && si < 16 && nb[si] == 0) nb[si] = spawn_exp[i];
                     else ++bad;
                 } else if (mode == 1) {
-                    spawn(nb, wa << 2, wb, e->flags);
+                    spawn_random(nb, a, w, v, e->flags);
                 } else {
                     spawn(nb, u[2], u[3], e->flags);
                 }
@@ -344,7 +385,7 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             qs = 0.0;
             ep[0] += 1; ep[1] = m[0]; ep[2] = m[1]; ep[3] = mx;
             if (autoreset) {
-                if (mode == 1) fresh_board_random(b, wa, wb, e->flags);
+                if (mode == 1) fresh_board_random(b, w, v, v2, e->flags);
                 else fresh_board(b, u, e->flags);   /* the step's own block (see fresh_board) */
                 m[0] = 0; m[1] = 0;
             }

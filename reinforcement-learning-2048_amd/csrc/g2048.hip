@@ -168,22 +168,16 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     uint32_t legal = 0u, act, r = 0u;
     bool done;
     uint4 u;
-    uint32_t wa = 0u, wb = 0u;
-    if constexpr (MODE == MODE_RANDOM) {
-        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, t >> 1);
-        wa = (t & 1u) ? blk.z : blk.x;
-        wb = (t & 1u) ? blk.w : blk.y;
-        act = wa >> 30;
-        if (A.legal_out) {  // the mask is wanted anyway: it decides done and the move's legality
-            legal = legal_mask(b);
-            done = legal == 0u;
-            if (!done && ((legal >> act) & 1u)) {
-                r = apply_move(b, act);
-                spawn(b, wa << 2, wb, A.p4_thresh);
-            }
-        } else {
-            r = random_step(b, wa, wb, A.p4_thresh, done);
-        }
+    RandWords rw{0u, 0u, 0u};
+    if constexpr (MODE == MODE_RANDOM) {  // the random-policy contract of g2048_roll.hpp
+        const bool p410 = (A.flags & G2048_P4_10) != 0u;
+        rw = random_words(A.seed_lo, A.seed_hi, gid, t, p410);
+        act = rw.w >> 30;
+        if (A.legal_out) legal = legal_mask(b);
+        uint4 F, I;
+        dir_sel_const(act, F, I);
+        r = lean_step(b, rw.w, p410 ? spawn_exp<true>(rw.w, rw.v, A.p4_thresh)
+                                   : spawn_exp<false>(rw.w, rw.v, A.p4_thresh), F, I, done);
     } else {
         u = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_STEP, t);
         legal = legal_mask(b);
@@ -253,7 +247,8 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         end_episode<kGreedy>(A, i, gid, t, b, m, ep, qs);
         if (!(A.flags & G2048_NO_AUTORESET)) {
             if constexpr (MODE == MODE_RANDOM)
-                b = fresh_board_random(wa, wb, p4_thresh16(A.p4_thresh));
+                b = (A.flags & G2048_P4_10) ? fresh_board_w<true>(rw.w, rw.v, rw.v2, A.p4_thresh)
+                                            : fresh_board_w<false>(rw.w, rw.v, rw.v2, A.p4_thresh);
             else
                 b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m = make_uint2(0u, 0u);
@@ -508,6 +503,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 //   kSum: per-board reward sums are accumulated.
 template <bool kRing, bool kBuf, bool kSum>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5 : 6))) void k_rollout(StepArgs A) {
+    __shared__ uint4 s_dir[8];  // the direction-selector table (g2048_roll.hpp kDirNet)
+    if (threadIdx.x < 8)
+        s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= A.n) return;
     G2048_ROLL_MARK(0);
@@ -516,7 +515,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     uint2 m = A.meta[i];
     uint4 ep = A.ep[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
-    const uint32_t p4_16 = p4_thresh16(A.p4_thresh);
     const bool autoreset = !(A.flags & G2048_NO_AUTORESET);
     long long rsum = 0;
     double qs = A.qsum ? A.qsum[i] : 0.0;  // random policy: reset (0) on done only
@@ -536,14 +534,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     const uint32_t v_d = kBuf ? A.rb.o_d + lane : 0u;
     const uint32_t ep0 = ep.x;  // some episode of this board ended in the launch iff ep.x moved
     Board last = b;      // the final board of that episode (its max tile goes to ep.w at the end)
-    // one transition with the words (wa, wb) of step t
+    const bool p410 = (A.flags & G2048_P4_10) != 0u;
+    // one transition of step t with its draws rw (g2048_roll.hpp)
     // lean (std::true_type): no episode log and auto-reset on -- the loop then carries neither
-    // uniform test (each an SALU op per step at one wave per SIMD)
-    auto one = [&](auto lean, uint32_t wa, uint32_t wb, uint64_t t) {
+    // uniform test
+    auto one = [&](auto lean, const RandWords& rd, uint64_t t) {
         constexpr bool kLean = decltype(lean)::value;
+        const uint32_t wa = rd.w;
         const Board so = b;
         bool done;
-        const uint32_t r = random_step(b, wa, wb, A.p4_thresh, done);
+        const uint32_t a2 = (wa >> 30) * 2u;
+        const uint32_t r = lean_step(b, wa,
+                                     p410 ? spawn_exp<true>(wa, rd.v, A.p4_thresh)
+                                          : spawn_exp<false>(wa, rd.v, A.p4_thresh),
+                                     s_dir[a2], s_dir[a2 + 1u], done);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
@@ -584,32 +588,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
             last = b;
             qs = 0.0;
             if (kLean || autoreset) {
-                b = fresh_board_random(wa, wb, p4_16);
+                b = p410 ? fresh_board_w<true>(wa, rd.v, rd.v2, A.p4_thresh)
+                         : fresh_board_w<false>(wa, rd.v, rd.v2, A.p4_thresh);
                 m = make_uint2(0u, 0u);
             }
         }
     };
     const int K = A.k_steps > 0 ? A.k_steps : 0;
     auto run = [&](auto lean) {
-        uint64_t pair = t0 >> 1;
-        int rest = K;
-        if (rest > 0 && (t0 & 1u)) {  // odd start: the second half of the current pair
-            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-            one(lean, blk.z, blk.w, t0);
-            ++pair;
-            --rest;
-        }
+        // the quad's blocks are drawn when t enters it (a wave-uniform branch)
+        uint4 blk = make_uint4(0, 0, 0, 0), vb = blk, vb2 = blk;
         G2048_ROLL_MARK(1);
-        for (int np = rest >> 1; np > 0; --np, ++pair) {  // a down-counter: one SALU op less
-            G2048_ROLL_TICK(np);
-            if constexpr (kBuf) asm volatile("" : "+s"(rw));  // one SGPR quad for the descriptor
-            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-            one(lean, blk.x, blk.y, 2u * pair);
-            one(lean, blk.z, blk.w, 2u * pair + 1u);
-        }
-        if (rest & 1) {
-            const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-            one(lean, blk.x, blk.y, 2u * pair);
+        for (int s = 0; s < K; ++s) {
+            const uint64_t t = t0 + (uint64_t)s;
+            if (s == 0 || (t & 3u) == 0u) {
+                if constexpr (kBuf) asm volatile("" : "+s"(rw));  // one SGPR quad for the descriptor
+                blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, t >> 2);
+                if (p410) value_blocks<true>(A.seed_lo, A.seed_hi, gid, t >> 2, vb, vb2);
+            }
+            const uint32_t k = (uint32_t)t & 3u;
+            one(lean, RandWords{word_of(blk, k), word_of(vb, k), word_of(vb2, k)}, t);
         }
     };
     if (!A.log && autoreset) run(std::true_type{});
@@ -630,11 +628,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 }
 
 // The headline instance of g2048_env_rollout -- ring in one buffer window, auto-reset on, no
-// episode log -- with the step of g2048_roll.hpp: same results as k_rollout<true, true, kSum>
-// (tested), fewer issue turns per step.  Each workgroup stages the direction-selector table
-// (kDirNet, 128 B) in LDS; a step reads its action's two selector quads from it.
-template <bool kSum>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5 : 6))) void k_rollout_lean(StepArgs A) {
+// episode log: four steps per iteration from one Philox block (one word per step), the next
+// quad's block drawn while this quad's direction selectors are read from LDS.  Each workgroup
+// stages the selector table (kDirNet, 128 B) in LDS; a step reads its action's two quads.
+template <bool kSum, bool kP410>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_lean(StepArgs A) {
     __shared__ uint4 s_dir[8];
     if (threadIdx.x < 8)
         s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
@@ -646,7 +644,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     uint2 m = A.meta[i];
     uint4 ep = A.ep[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
-    const uint32_t p4 = A.p4_thresh, p4_16 = p4_thresh16(A.p4_thresh);
+    const uint32_t p4 = A.p4_thresh;
     long long rsum = 0;
     const uint32_t row = (uint32_t)ring_row(t0, A.rb.rows);
     const uint32_t cap32 = (uint32_t)A.rb.capacity, n32 = (uint32_t)A.n;
@@ -658,19 +656,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
     const uint32_t ep0 = ep.x;
     Board last = b;
-    // one transition with the words (wa, wb) and the action's selector quads (F, I)
-    auto one = [&](uint32_t wa, uint32_t wb, const uint4& F, const uint4& I) {
+    // one transition with the word w (+ value words v, v2 under G2048_P4_10) and the action's
+    // selector quads (F, I)
+    auto one = [&](uint32_t w, uint32_t v, uint32_t v2, const uint4& F, const uint4& I) {
         G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s, soff * 16u,
                                                0);
         bool done;
-        const uint32_t r = lean_step(b, wa, wb, p4, F, I, done);
+        const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2, soff * 16u,
                                                0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), rw, v_a, soff, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, v_a, soff, 0);
         __builtin_amdgcn_raw_buffer_store_b32(r, rw, v_r, soff * 4u, 0);
         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, v_d, soff, 0);
         soff = soff + n32 == cap32 ? 0u : soff + n32;
@@ -679,7 +678,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
         // a v_mov costs a full issue turn)
         G2048_MARK(reset, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
         if (__builtin_amdgcn_ballot_w64(done) != 0u) {
-            const Board f = fresh_board_random(wa, wb, p4_16);
+            const Board f = fresh_board_w<kP410>(w, v, v2, p4);
             last.r0 = done ? b.r0 : last.r0;
             last.r1 = done ? b.r1 : last.r1;
             last.r2 = done ? b.r2 : last.r2;
@@ -695,52 +694,70 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
             m.y = done ? 0u : m.y;
         }
     };
-    auto sel = [&](uint32_t wa, uint4& F, uint4& I) {
-        const uint32_t a2 = (wa >> 30) * 2u;
+    auto sel = [&](uint32_t w, uint4& F, uint4& I) {
+        const uint32_t a2 = (w >> 30) * 2u;
         F = s_dir[a2];
         I = s_dir[a2 + 1u];
     };
     const int K = A.k_steps > 0 ? A.k_steps : 0;
-    uint64_t pair = t0 >> 1;
-    int rest = K;
-    uint4 F, I, F2, I2;
-    if (rest > 0 && (t0 & 1u)) {
-        const uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-        sel(blk.z, F, I);
-        one(blk.z, blk.w, F, I);
-        ++pair;
-        --rest;
+    // steps up to the first quad boundary, one at a time
+    const int nh = min(K, (int)((4u - ((uint32_t)t0 & 3u)) & 3u));
+    uint4 blk = make_uint4(0, 0, 0, 0), vb = blk, vb2 = blk;
+    if (nh > 0) {
+        blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, t0 >> 2);
+        value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, t0 >> 2, vb, vb2);
+        for (int s = 0; s < nh; ++s) {
+            const uint32_t k = ((uint32_t)t0 + (uint32_t)s) & 3u;
+            uint4 F, I;
+            const uint32_t w = word_of(blk, k);
+            sel(w, F, I);
+            one(w, word_of(vb, k), word_of(vb2, k), F, I);
+        }
     }
-    // software-pipelined by one pair: the selector reads of pair p are in flight while the block
-    // of pair p + 1 is drawn (the loop draws up to two blocks it does not use); two pairs per
-    // iteration, so the blocks alternate between two register quads instead of being copied
-    uint4 blk = random_block(A.seed_lo, A.seed_hi, gid, pair);
-    auto pair_of = [&](const uint4& cur, uint4& nxt, uint64_t p_next) {
-        G2048_MARK(selectors, "+v"(cur.x), "+v"(cur.z));
-        sel(cur.x, F, I);
+    // whole quads, software-pipelined by one quad: the selector reads of quad j are in flight
+    // while the block(s) of quad j + 1 are drawn (the last iteration draws blocks it does not
+    // use); two quads per iteration, so the blocks alternate between two register sets
+    uint64_t quad = (t0 + (uint64_t)nh) >> 2;
+    blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, quad);
+    value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, quad, vb, vb2);
+    auto quad_of = [&](const uint4& cur, const uint4& cv, const uint4& cv2, uint4& nxt, uint4& nv,
+                       uint4& nv2, uint64_t q_next) {
+        uint4 F0, I0, F1, I1, F2, I2, F3, I3;
+        G2048_MARK(selectors, "+v"(F0.x));
+        sel(cur.x, F0, I0);
+        sel(cur.y, F1, I1);
         sel(cur.z, F2, I2);
-        G2048_MARK(philox, "+v"(F.x), "+v"(F2.x));
-        nxt = random_block(A.seed_lo, A.seed_hi, gid, p_next);
+        sel(cur.w, F3, I3);
+        G2048_MARK(philox, "+v"(F0.x), "+v"(F3.x));
+        nxt = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, q_next);
+        value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, q_next, nv, nv2);
         G2048_MARK(step, "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
-        one(cur.x, cur.y, F, I);
-        one(cur.z, cur.w, F2, I2);
+        one(cur.x, cv.x, cv2.x, F0, I0);
+        one(cur.y, cv.y, cv2.y, F1, I1);
+        one(cur.z, cv.z, cv2.z, F2, I2);
+        one(cur.w, cv.w, cv2.w, F3, I3);
     };
-    int np = rest >> 1;
-    for (; np >= 2; np -= 2, pair += 2) {
+    int nq = (K - nh) >> 2;
+    for (; nq >= 2; nq -= 2, quad += 2) {
         asm volatile("" : "+s"(rw));
-        uint4 b1;
-        pair_of(blk, b1, pair + 1u);
-        pair_of(b1, blk, pair + 2u);
+        uint4 b1, v1, w1;
+        quad_of(blk, vb, vb2, b1, v1, w1, quad + 1u);
+        quad_of(b1, v1, w1, blk, vb, vb2, quad + 2u);
     }
-    if (np) {
-        uint4 b1;
-        pair_of(blk, b1, pair + 1u);
+    if (nq) {
+        uint4 b1, v1, w1;
+        quad_of(blk, vb, vb2, b1, v1, w1, quad + 1u);
         blk = b1;
-        ++pair;
+        vb = v1;
+        vb2 = w1;
+        ++quad;
     }
-    if (rest & 1) {
-        sel(blk.x, F, I);
-        one(blk.x, blk.y, F, I);
+    // the last K mod 4 steps (a partial quad)
+    for (int k = 0; k < ((K - nh) & 3); ++k) {
+        uint4 F, I;
+        const uint32_t w = word_of(blk, (uint32_t)k);
+        sel(w, F, I);
+        one(w, word_of(vb, (uint32_t)k), word_of(vb2, (uint32_t)k), F, I);
     }
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
@@ -1339,9 +1356,15 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
         if (reward_sum) hipLaunchKernelGGL((k_rollout<false, false, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<false, false, false>), grid, block, 0, st, A);
     } else if (A.rb.win_bytes && !A.log && !(A.flags & G2048_NO_AUTORESET)) {
-        // the headline case: g2048_roll.hpp's step
-        if (reward_sum) hipLaunchKernelGGL((k_rollout_lean<true>), grid, block, 0, st, A);
-        else hipLaunchKernelGGL((k_rollout_lean<false>), grid, block, 0, st, A);
+        // the headline case
+        const bool p410 = (A.flags & G2048_P4_10) != 0u;
+        if (reward_sum) {
+            if (p410) hipLaunchKernelGGL((k_rollout_lean<true, true>), grid, block, 0, st, A);
+            else hipLaunchKernelGGL((k_rollout_lean<true, false>), grid, block, 0, st, A);
+        } else {
+            if (p410) hipLaunchKernelGGL((k_rollout_lean<false, true>), grid, block, 0, st, A);
+            else hipLaunchKernelGGL((k_rollout_lean<false, false>), grid, block, 0, st, A);
+        }
     } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<true, true, false>), grid, block, 0, st, A);

@@ -70,18 +70,123 @@ __device__ __forceinline__ uint32_t xad(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 
+// sum over the bytes b of x of (byte b of f) << (byte b of x): one SDWA shift per byte, whose
+// byte-select operands do both extractions
+template <int K>
+__device__ __forceinline__ uint32_t shl_byte(uint32_t x, uint32_t f) {
+    uint32_t d;
+    if constexpr (K == 0)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0"
+            : "=v"(d) : "v"(x), "v"(f));
+    else if constexpr (K == 1)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1"
+            : "=v"(d) : "v"(x), "v"(f));
+    else if constexpr (K == 2)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2"
+            : "=v"(d) : "v"(x), "v"(f));
+    else
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3"
+            : "=v"(d) : "v"(x), "v"(f));
+    return d;
+}
+
+__device__ __forceinline__ uint32_t shl_bytes(uint32_t x, uint32_t f) {
+    return shl_byte<0>(x, f) + shl_byte<1>(x, f) + shl_byte<2>(x, f) + shl_byte<3>(x, f);
+}
+
 // bits [31:0] of {hi, lo} >> s
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
 }
 
+// ------------------------------------------------------------------ random-policy draws (ABI v3)
+// Step t of board g takes ONE 32-bit word w = word (t & 3) of the DOMAIN_RANDOM block t >> 2 (a
+// Philox block per four steps).  Bits of w:
+//   action              w >> 30                      (np.random.randint(4), src/dqn_lib.py:20)
+//   spawn cell          k = floor((w << 3) * n / 2^32), bits 0..28: the k-th empty cell of the
+//                       slid board in move-space line-major order (see lean_step)
+//   spawn value         a 4 iff bit 29 is set (p(4) = 0.5, src/board.py:12,49)
+//   auto-reset (terminal steps, which spawn nothing): first tile at cell (w >> 26) & 15, a 4 iff
+//                       bit 25; second at the k2-th of the other 15 cells (row-major),
+//                       k2 = floor((w << 8) * 15 / 2^32), a 4 iff bit 24
+// With G2048_P4_10 the values come from two more blocks of the same quad, at counters
+// (t >> 2) | 2^63 (v: the spawn and the reset's first tile) and (t >> 2) | 2^62 (v2: the reset's
+// second tile), word t & 3 of each: a 4 iff v < round(0.1 * 2^32) -- exact 32-bit thresholds.
+struct RandWords {
+    uint32_t w, v, v2;
+};
+
+__device__ __forceinline__ uint32_t word_of(const uint4& u, uint32_t k) {
+    return k == 0u ? u.x : k == 1u ? u.y : k == 2u ? u.z : u.w;
+}
+
+template <bool kP410>
+__device__ __forceinline__ void value_blocks(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
+                                             uint64_t quad, uint4& vb, uint4& vb2) {
+    if constexpr (kP410) {
+        vb = draw(seed_lo, seed_hi, gid, DOMAIN_RANDOM, quad | (1ull << 63));
+        vb2 = draw(seed_lo, seed_hi, gid, DOMAIN_RANDOM, quad | (1ull << 62));
+    }
+}
+
+// The draws of step t (any t; the rollout kernels fetch one block per quad instead)
+__device__ __forceinline__ RandWords random_words(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
+                                                  uint64_t t, bool p410) {
+    const uint4 u = draw(seed_lo, seed_hi, gid, DOMAIN_RANDOM, t >> 2);
+    RandWords r{word_of(u, (uint32_t)t & 3u), 0u, 0u};
+    if (p410) {
+        uint4 vb, vb2;
+        value_blocks<true>(seed_lo, seed_hi, gid, t >> 2, vb, vb2);
+        r.v = word_of(vb, (uint32_t)t & 3u);
+        r.v2 = word_of(vb2, (uint32_t)t & 3u);
+    }
+    return r;
+}
+
+// Spawn exponent of a moving step: 2 (a "4") or 1 (a "2").
+template <bool kP410>
+__device__ __forceinline__ uint32_t spawn_exp(uint32_t w, uint32_t v, uint32_t p4_thresh) {
+    if constexpr (kP410) return v < p4_thresh ? 2u : 1u;
+    else return 1u + ((w >> 29) & 1u);
+}
+
+// Auto-reset board of a terminal random-policy step (bits: see above).  The two tiles are placed
+// with 64-bit shifts into the board's halves {r0, r1} / {r2, r3}.
+template <bool kP410>
+__device__ __forceinline__ Board fresh_board_w(uint32_t w, uint32_t v, uint32_t v2,
+                                               uint32_t p4_thresh) {
+    const uint32_t ca = (w >> 26) & 15u;
+    const uint32_t k2 = __umulhi(w << 8, 15u);
+    const uint32_t cb = k2 + (uint32_t)(k2 >= ca);
+    const uint32_t va = kP410 ? (v < p4_thresh ? 2u : 1u) : 1u + ((w >> 25) & 1u);
+    const uint32_t vb = kP410 ? (v2 < p4_thresh ? 2u : 1u) : 1u + ((w >> 24) & 1u);
+    const uint64_t ta = (uint64_t)va << (8u * (ca & 7u));
+    const uint64_t tb = (uint64_t)vb << (8u * (cb & 7u));
+    const uint64_t lo = (ca < 8u ? ta : 0u) | (cb < 8u ? tb : 0u);
+    const uint64_t hi = (ca < 8u ? 0u : ta) | (cb < 8u ? 0u : tb);
+    return Board{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+}
+
+// The selector quads of action a from the constant table (the kernels that run one step per
+// launch; the rollout stages the table in LDS).
+__device__ __forceinline__ void dir_sel_const(uint32_t a, uint4& F, uint4& I) {
+    const uint4* t = reinterpret_cast<const uint4*>(&kDirNet[0][0][0]);
+    F = t[2u * a];
+    I = t[2u * a + 1u];
+}
+
 // The random-policy transition of board b (rows) along the line words given by the selector
 // quads F (rows -> lines) and I (lines -> rows): slide, terminal test of the board as given,
-// spawn (k-th empty cell of the result in row-major order, spawn_at) when the board moved.
-// Returns the merge gain; done as random_step.
-__device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t wa, uint32_t wb,
-                                              uint32_t p4_thresh, const uint4& F, const uint4& I,
-                                              bool& done) {
+// spawn of exponent e (1 or 2) when the board moved.  The spawn cell is the k-th empty cell,
+// k = floor((w << 3) * n / 2^32), in MOVE-SPACE LINE-MAJOR order: lines j = 0..3 (byte j of the
+// line words), within a line positions q = 0..3 along the move -- after the slide a line's empties
+// are its last E_j positions, so the k-th is line j* (the first with S_j* > k, S = inclusive
+// prefix of E over lines) at position q = 4 + k - S_j*.  Any fixed order of the empty cells gives
+// the reference's uniform choice (src/board.py:41-51); this one needs no search.  Returns the merge
+// gain; done: the board as given was terminal (no legal move, src/dqn_lib.py:17-18).
+// Domain: exponents < 32 (the 0x20-flag sums below; a 4x4 game cannot pass 17).
+__device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, const uint4& F,
+                                              const uint4& I, bool& done) {
     uint32_t L0, L1, L2, L3;
     G2048_MARK(net_fwd, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
     dir_net(b.r0, b.r1, b.r2, b.r3, F, L0, L1, L2, L3);
@@ -109,33 +214,52 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t wa, uint32_t wb
     const uint32_t bc = bc_raw & ~ab;
     const uint32_t cd = cd_raw & (ab | ~bc_raw);
     const uint32_t AB = expand80(ab), BC = expand80(bc), CD = expand80(cd);
-    const uint32_t c1 = C2 + (cd >> 7);
-    const uint32_t b1 = C1 + (bc >> 7);
-    uint32_t o0 = C0 + (ab >> 7);
+    const uint32_t f_ab = ab >> 7, f_bc = bc >> 7, f_cd = cd >> 7;  // 0x01 per merging line
+    const uint32_t c1 = C2 + f_cd;
+    const uint32_t b1 = C1 + f_bc;
+    uint32_t o0 = C0 + f_ab;
     uint32_t o1 = bsel(AB, c1, b1);
     uint32_t o2 = bsel(AB, C3 & ~CD, bsel(BC, C3, c1));
     uint32_t o3 = C3 & ~(AB | BC | CD);
     G2048_MARK(score, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
-    const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD;
-    uint32_t gain = (pow2_bytes(e01) + pow2_bytes(e2)) -
-                          (8u - (uint32_t)(__popc(ab | bc) + __popc(cd)));
+    // 3) score = sum of 2^e over the merged tiles: a line merges a+b or b+c (never both), and
+    //    c+d, so two words of candidates; shifting the 0x01 merge flag (not 1) by each byte makes
+    //    a line without a merge contribute 0
+    const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD, f01 = f_ab | f_bc;
+    uint32_t gain = shl_bytes(e01, f01) + shl_bytes(e2, f_cd);
     G2048_MARK(moved_done, "+v"(gain));
-    // 3) moved: a hole before a tile along a line, or a merge
+    // 4) moved: a hole before a tile along a line, or a merge
     const uint32_t hb = ((D0 & ~D1) | (D1 & ~D2) | (D2 & ~D3)) & K80;
     uint32_t mv = hb | or3_v(ab, bc_raw, cd_raw);
-    // 4) terminal (board as given): nothing moves along these lines, no empty cell, no equal
-    //    neighbours across them (adjacent bytes of a line word; v_xad: bit 7 of (x ^ y) + 0x7F
-    //    is set iff the bytes differ), or the board is empty
+    // 5) terminal (board as given): nothing moves along these lines, no empty cell, no equal
+    //    neighbours across them (adjacent bytes of a line word), or the board is empty
     const uint32_t Y0 = xad(L0, alignbit(L1, L0, 8u), K7F), Y1 = xad(L1, alignbit(L2, L1, 8u), K7F);
     const uint32_t Y2 = xad(L2, alignbit(L3, L2, 8u), K7F), Y3 = xad(L3, L3 >> 8, K7F);
     const uint32_t across = ~(Y0 & Y1 & Y2 & Y3) & 0x00808080u;
     const uint32_t zany = (D0 | D1 | D2 | D3) & K80;
     done = min(or3_v(mv, zany, across), or3_v(L0, L1, L2 | L3)) == 0u;
-    // 5) back to rows, spawn iff moved (min(e, mv) = 0 iff mv == 0: mv is 0 or >= 0x80)
-    G2048_MARK(net_inv, "+v"(mv));
+    G2048_MARK(spawn, "+v"(mv));
+    // 6) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
+    //    line words (exponents < 32: no borrow; at most 4 * 0x20 per byte: no carry)
+    constexpr uint32_t K20 = 0x20202020u;
+    const uint32_t E20 = ((K20 - o0) & K20) + ((K20 - o1) & K20) + ((K20 - o2) & K20) +
+                         ((K20 - o3) & K20);
+    const uint32_t S = (E20 >> 5) * 0x01010101u;  // byte j: empties in lines 0..j; byte 3: n
+    const uint32_t k = __umulhi(w << 3, S >> 24);
+    // bit 7 of byte j < 3: S_j > k; the target line j* = the number of lines with S_j <= k
+    const uint32_t T = (S | K80) - (k * 0x010101u + 0x010101u);
+    const uint32_t j8 = (uint32_t)__popc(~T & 0x00808080u) << 3;
+    const uint32_t q = k + 4u - __builtin_amdgcn_ubfe(S, j8, 8u);
+    // exponent min(e, mv): mv is 0 (no move: no spawn) or >= 0x80
+    const uint64_t tile = (uint64_t)min(e, mv) << (((q << 5) & 32u) | j8);
+    const bool qhi = q >= 2u;
+    o0 |= qhi ? 0u : (uint32_t)tile;
+    o1 |= qhi ? 0u : (uint32_t)(tile >> 32);
+    o2 |= qhi ? (uint32_t)tile : 0u;
+    o3 |= qhi ? (uint32_t)(tile >> 32) : 0u;
+    // 7) back to rows
+    G2048_MARK(net_inv, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
     dir_net(o0, o1, o2, o3, I, b.r0, b.r1, b.r2, b.r3);
-    G2048_MARK(spawn, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
-    spawn_at(b, wa << 2, min(wb < p4_thresh ? 2u : 1u, mv));
     G2048_MARK(stores, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
     return gain;
 }

@@ -18,7 +18,7 @@ G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOMEM, G2048_EBADINPUT = 0, -1, -2, -
 P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
 ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
-ABI_VERSION = 2  # include/g2048.h G2048_ABI_VERSION
+ABI_VERSION = 3  # include/g2048.h G2048_ABI_VERSION
 
 # every symbol include/g2048.h declares, with (restype, argtypes)
 _vp, _i64, _u64, _i32, _u32, _int, _dbl = (C.c_void_p, C.c_int64, C.c_uint64, C.c_int32,

@@ -10,7 +10,7 @@ import re
 import sys
 from collections import Counter, defaultdict
 
-KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0EEEvNS_8StepArgsE"
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0EEEvNS_8StepArgsE"
 
 
 def kind(op):

@@ -22,7 +22,7 @@ void launch_lean(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
     make_args(e, rb, A);
     A.k_steps = K;
-    hipLaunchKernelGGL((k_rollout_lean<false>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+    hipLaunchKernelGGL((k_rollout_lean<false, false>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
 }
 
 struct Variant {
@@ -31,7 +31,7 @@ struct Variant {
 };
 
 const Variant kVariants[] = {
-    {"k_rollout (round 2)", launch_old},
+    {"k_rollout (general path)", launch_old},
     {"k_rollout_lean", launch_lean},
 };
 
