@@ -677,21 +677,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // lane-masked `if (done)` made hipcc copy the board and counters through phi moves, and
         // a v_mov costs a full issue turn)
         G2048_MARK(reset, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
-        if (__builtin_amdgcn_ballot_w64(done) != 0u) {
+        const uint64_t dl = __builtin_amdgcn_ballot_w64(done);
+        if (dl != 0u) {
             const Board f = fresh_board_w<kP410>(w, v, v2, p4);
-            last.r0 = done ? b.r0 : last.r0;
-            last.r1 = done ? b.r1 : last.r1;
-            last.r2 = done ? b.r2 : last.r2;
-            last.r3 = done ? b.r3 : last.r3;
-            ep.x += done ? 1u : 0u;
-            ep.y = done ? m.x : ep.y;
-            ep.z = done ? m.y : ep.z;
-            b.r0 = done ? f.r0 : b.r0;
-            b.r1 = done ? f.r1 : b.r1;
-            b.r2 = done ? f.r2 : b.r2;
-            b.r3 = done ? f.r3 : b.r3;
-            m.x = done ? 0u : m.x;
-            m.y = done ? 0u : m.y;
+            last.r0 = sel_lanes(dl, b.r0, last.r0);
+            last.r1 = sel_lanes(dl, b.r1, last.r1);
+            last.r2 = sel_lanes(dl, b.r2, last.r2);
+            last.r3 = sel_lanes(dl, b.r3, last.r3);
+            ep.x = sel_lanes(dl, ep.x + 1u, ep.x);
+            ep.y = sel_lanes(dl, m.x, ep.y);
+            ep.z = sel_lanes(dl, m.y, ep.z);
+            b.r0 = sel_lanes(dl, f.r0, b.r0);
+            b.r1 = sel_lanes(dl, f.r1, b.r1);
+            b.r2 = sel_lanes(dl, f.r2, b.r2);
+            b.r3 = sel_lanes(dl, f.r3, b.r3);
+            m.x = sel_lanes(dl, 0u, m.x);
+            m.y = sel_lanes(dl, 0u, m.y);
         }
     };
     auto sel = [&](uint32_t w, uint4& F, uint4& I) {

@@ -94,6 +94,15 @@ __device__ __forceinline__ uint32_t shl_bytes(uint32_t x, uint32_t f) {
     return shl_byte<0>(x, f) + shl_byte<1>(x, f) + shl_byte<2>(x, f) + shl_byte<3>(x, f);
 }
 
+// lanes set in the wave mask `on` take a, the others b (v_cndmask_b32 with an SGPR-pair mask).
+// Opaque to the compiler: plain selects on `done` in the auto-reset block were turned back into
+// a lane-masked branch whose phi copies cost a v_mov per value.
+__device__ __forceinline__ uint32_t sel_lanes(uint64_t on, uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(d) : "v"(b), "v"(a), "s"(on));
+    return d;
+}
+
 // bits [31:0] of {hi, lo} >> s
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
@@ -158,13 +167,18 @@ __device__ __forceinline__ Board fresh_board_w(uint32_t w, uint32_t v, uint32_t 
     const uint32_t ca = (w >> 26) & 15u;
     const uint32_t k2 = __umulhi(w << 8, 15u);
     const uint32_t cb = k2 + (uint32_t)(k2 >= ca);
-    const uint32_t va = kP410 ? (v < p4_thresh ? 2u : 1u) : 1u + ((w >> 25) & 1u);
-    const uint32_t vb = kP410 ? (v2 < p4_thresh ? 2u : 1u) : 1u + ((w >> 24) & 1u);
-    const uint64_t ta = (uint64_t)va << (8u * (ca & 7u));
-    const uint64_t tb = (uint64_t)vb << (8u * (cb & 7u));
-    const uint64_t lo = (ca < 8u ? ta : 0u) | (cb < 8u ? tb : 0u);
-    const uint64_t hi = (ca < 8u ? 0u : ta) | (cb < 8u ? 0u : tb);
-    return Board{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    // a tile of exponent 1 + x is 1 << x: the value bit joins the 64-bit shift amount
+    const uint32_t xa = kP410 ? (uint32_t)(v < p4_thresh) : (w >> 25) & 1u;
+    const uint32_t xb = kP410 ? (uint32_t)(v2 < p4_thresh) : (w >> 24) & 1u;
+    const uint64_t ta = 1ull << (((ca << 3) & 56u) + xa);
+    const uint64_t tb = 1ull << (((cb << 3) & 56u) + xb);
+    // half masks: bit 3 of the cell sign-extended (cells 8..15 live in {r2, r3})
+    const uint32_t ma = (uint32_t)__builtin_amdgcn_sbfe((int32_t)ca, 3u, 1u);
+    const uint32_t mb = (uint32_t)__builtin_amdgcn_sbfe((int32_t)cb, 3u, 1u);
+    return Board{((uint32_t)ta & ~ma) | ((uint32_t)tb & ~mb),
+                 ((uint32_t)(ta >> 32) & ~ma) | ((uint32_t)(tb >> 32) & ~mb),
+                 ((uint32_t)ta & ma) | ((uint32_t)tb & mb),
+                 ((uint32_t)(ta >> 32) & ma) | ((uint32_t)(tb >> 32) & mb)};
 }
 
 // The selector quads of action a from the constant table (the kernels that run one step per
@@ -231,32 +245,36 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     // 4) moved: a hole before a tile along a line, or a merge
     const uint32_t hb = ((D0 & ~D1) | (D1 & ~D2) | (D2 & ~D3)) & K80;
     uint32_t mv = hb | or3_v(ab, bc_raw, cd_raw);
-    // 5) terminal (board as given): nothing moves along these lines, no empty cell, no equal
-    //    neighbours across them (adjacent bytes of a line word), or the board is empty
-    const uint32_t Y0 = xad(L0, alignbit(L1, L0, 8u), K7F), Y1 = xad(L1, alignbit(L2, L1, 8u), K7F);
-    const uint32_t Y2 = xad(L2, alignbit(L3, L2, 8u), K7F), Y3 = xad(L3, L3 >> 8, K7F);
-    const uint32_t across = ~(Y0 & Y1 & Y2 & Y3) & 0x00808080u;
-    const uint32_t zany = (D0 | D1 | D2 | D3) & K80;
-    done = min(or3_v(mv, zany, across), or3_v(L0, L1, L2 | L3)) == 0u;
     G2048_MARK(spawn, "+v"(mv));
-    // 6) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
+    // 5) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
     //    line words (exponents < 32: no borrow; at most 4 * 0x20 per byte: no carry)
     constexpr uint32_t K20 = 0x20202020u;
     const uint32_t E20 = ((K20 - o0) & K20) + ((K20 - o1) & K20) + ((K20 - o2) & K20) +
                          ((K20 - o3) & K20);
     const uint32_t S = (E20 >> 5) * 0x01010101u;  // byte j: empties in lines 0..j; byte 3: n
-    const uint32_t k = __umulhi(w << 3, S >> 24);
+    const uint32_t n = S >> 24;
+    const uint32_t k = __umulhi(w << 3, n);
     // bit 7 of byte j < 3: S_j > k; the target line j* = the number of lines with S_j <= k
     const uint32_t T = (S | K80) - (k * 0x010101u + 0x010101u);
     const uint32_t j8 = (uint32_t)__popc(~T & 0x00808080u) << 3;
     const uint32_t q = k + 4u - __builtin_amdgcn_ubfe(S, j8, 8u);
-    // exponent min(e, mv): mv is 0 (no move: no spawn) or >= 0x80
-    const uint64_t tile = (uint64_t)min(e, mv) << (((q << 5) & 32u) | j8);
-    const bool qhi = q >= 2u;
-    o0 |= qhi ? 0u : (uint32_t)tile;
-    o1 |= qhi ? 0u : (uint32_t)(tile >> 32);
-    o2 |= qhi ? (uint32_t)tile : 0u;
-    o3 |= qhi ? (uint32_t)(tile >> 32) : 0u;
+    // the tile min(e, mv) (mv is 0 -- no move, no spawn -- or >= 0x80) at bit 8 j* + 32 (q & 1)
+    // of the half {o0, o1} (q < 2) or {o2, o3}: v_lshlrev_b64 reads 6 bits of the shift, and the
+    // half's mask is bit 1 of q sign-extended (q = 4 only without a move, when the tile is 0)
+    const uint64_t tile = (uint64_t)min(e, mv) << ((q << 5) + j8);
+    const uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)q, 1u, 1u);
+    o0 |= (uint32_t)tile & ~qm;
+    o1 |= (uint32_t)(tile >> 32) & ~qm;
+    o2 |= (uint32_t)tile & qm;
+    o3 |= (uint32_t)(tile >> 32) & qm;
+    // 6) terminal (board as given, src/dqn_lib.py:17-18): no empty cell after a non-move (a move
+    //    always leaves one, so n == 0 iff nothing moved and the board is full) and no equal
+    //    neighbours across the lines (adjacent bytes of a line word; v_xad: bit 7 of
+    //    (x ^ y) + 0x7F is set iff the bytes differ) -- or the board is empty (n == 16)
+    const uint32_t Y0 = xad(L0, alignbit(L1, L0, 8u), K7F), Y1 = xad(L1, alignbit(L2, L1, 8u), K7F);
+    const uint32_t Y2 = xad(L2, alignbit(L3, L2, 8u), K7F), Y3 = xad(L3, L3 >> 8, K7F);
+    const uint32_t across = ~(Y0 & Y1 & Y2 & Y3) & 0x00808080u;
+    done = min(n | across, 16u - n) == 0u;
     // 7) back to rows
     G2048_MARK(net_inv, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
     dir_net(o0, o1, o2, o3, I, b.r0, b.r1, b.r2, b.r3);

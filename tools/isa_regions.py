@@ -10,7 +10,7 @@ import re
 import sys
 from collections import Counter, defaultdict
 
-KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0EEEvNS_8StepArgsE"
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0EEEvNS_8StepArgsE"  # <kSum=false, kP410=false>
 
 
 def kind(op):
@@ -27,15 +27,21 @@ def kind(op):
     return "VALU"
 
 
-def main(path):
+def main(path, dump=None):
     lines = open(path).read().split("\n")
     st = next(i for i, l in enumerate(lines) if l.startswith(KERNEL + ":"))
     en = next(i for i in range(st, len(lines)) if lines[i].startswith(".Lfunc_end"))
     f = lines[st:en]
-    head = next(i for i, l in enumerate(f) if "Inner Loop Header" in l)
-    # the loop body: from the header to the back-edge branch to it
-    label = f[head].split(":")[0]
-    tail = max(i for i, l in enumerate(f) if label in l and ("s_branch" in l or "s_cbranch" in l))
+    # the main loop: the largest body from a loop header to the last branch back to it
+    best = None
+    for head, l in enumerate(f):
+        if "Loop Header" not in l:
+            continue
+        label = l.split(":")[0]
+        backs = [i for i, x in enumerate(f) if label in x and ("s_branch" in x or "s_cbranch" in x)]
+        if backs and (best is None or max(backs) - head > best[1] - best[0]):
+            best = (head, max(backs))
+    head, tail = best
     region = "loop_head"
     per = defaultdict(Counter)
     for l in f[head:tail + 1]:
@@ -44,6 +50,8 @@ def main(path):
         if m:
             region = m.group(1)
             continue
+        if dump == region and t and not t.startswith(";;#ASM"):
+            print("   ", t)
         if not t or t.startswith((";", ".")) or t.endswith(":"):
             continue
         per[region][kind(t.split()[0])] += 1
@@ -56,4 +64,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
