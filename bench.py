@@ -295,6 +295,14 @@ def bench_train(args, world, rank, dev, net, dtype):
     late_wall, _ = timed(world, dev, T.step, K2)
     loss = float(L.last_loss)
     env.check_errors()
+    lockstep = None
+    if world > 1:  # the replicas (online + target nets) must agree bit for bit on every rank
+        flat = torch.cat([p.detach().reshape(-1) for p in
+                          list(L.model.parameters()) + list(L.target.parameters())])
+        flat = flat if BACKEND == "nccl" else flat.cpu()
+        got = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(got, flat)
+        lockstep = all(torch.equal(got[0], g) for g in got[1:])
     fl = flops_per_update(net, args.batch)
     peak = FP32_PEAK_TF if dtype == "fp32" else FP64_PEAK_TF
     tf = fl / (upd_ev / K) / 1e12
@@ -309,7 +317,7 @@ def bench_train(args, world, rank, dev, net, dtype):
             "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
             "loop_late_epsilon_mean": eps_late,
             "batch": args.batch, "replay": C, "dtype": dtype, "loss": loss,
-            "params": L.n_params, "graphed_loop": T.graph}
+            "params": L.n_params, "graphed_loop": T.graph, "ranks_lockstep": lockstep}
 
 
 # ------------------------------------------------------------------ CPU baselines

@@ -491,8 +491,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 
 // g2048_env_rollout: k_steps random-policy steps of every board with the board, score, moves and
-// episode counters held in registers; step t of the launch draws its two words from the Philox
-// block of its step pair (one block per two steps, see random_block) and appends (s, a, r, s', d)
+// episode counters held in registers; step t of the launch draws its word from the Philox block
+// of its 4-step quad (ABI v3, g2048_roll.hpp random_words) and appends (s, a, r, s', d)
 // to the ring.  Identical to k_steps g2048_env_step(actions = NULL) calls.  Issue-bound at 64k
 // boards (one wave per SIMD, so SALU instructions cost issue turns like VALU ones): the loop
 // keeps its scalar bookkeeping to a 32-bit ring row and a 64-bit pair counter, and the episode
@@ -629,20 +629,39 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 
 // The headline instance of g2048_env_rollout -- ring in one buffer window, auto-reset on, no
 // episode log: four steps per iteration from one Philox block (one word per step), the next
-// quad's block drawn while this quad's direction selectors are read from LDS.  Each workgroup
-// stages the selector table (kDirNet, 128 B) in LDS; a step reads its action's two quads.
-template <bool kSum, bool kP410>
+// quad's block drawn at the top of a quad, and each step's direction selectors read from LDS one
+// step ahead.  Each workgroup stages the selector table in LDS (64 B per action: F, I, 32 B
+// unused, so a step's table offset is one v_and of its word's top byte).
+//   kQR: the ring's rows (capacity / n) are a multiple of 4, so a quad never wraps: its four
+//   steps take their row offsets from loop-invariant VGPRs (section offset + j * size * n) and
+//   the quad's base from three SGPRs updated once per quad -- 1.25 SALU per step instead of 5
+//   (at one wave per SIMD an SALU op costs an issue turn like a VALU op).
+template <bool kSum, bool kP410, bool kQR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_lean(StepArgs A) {
-    __shared__ uint4 s_dir[8];
-    if (threadIdx.x < 8)
-        s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
-    __syncthreads();
+    __shared__ uint4 s_dir[16];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= A.n) return;
-    const uint64_t t0 = load_clock(A.clock, i);
-    Board b = load_board(A.board[i]);
-    uint2 m = A.meta[i];
-    uint4 ep = A.ep[i];
+    const bool live = i < A.n;
+    // the board state's loads go out before the table staging and its barrier, so their
+    // latencies overlap (the prologue is a few steps' worth of a 64-step launch)
+    uint64_t c0 = 0;
+    uint4 bv = make_uint4(0, 0, 0, 0), ep = bv;
+    uint2 m = make_uint2(0, 0);
+    if (live) {
+        c0 = A.clock[i >> 6];
+        bv = A.board[i];
+        m = A.meta[i];
+        ep = A.ep[i];
+    }
+    if (threadIdx.x < 16)
+        s_dir[threadIdx.x] =
+            (threadIdx.x & 2u) ? make_uint4(0, 0, 0, 0)
+                               : reinterpret_cast<const uint4*>(
+                                     &kDirNet[0][0][0])[(threadIdx.x >> 2) * 2u + (threadIdx.x & 1u)];
+    __syncthreads();
+    if (!live) return;
+    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    Board b = load_board(bv);
     const uint64_t gid = A.board_offset + (uint64_t)i;
     const uint32_t p4 = A.p4_thresh;
     long long rsum = 0;
@@ -656,23 +675,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
     const uint32_t ep0 = ep.x;
     Board last = b;
-    // one transition with the word w (+ value words v, v2 under G2048_P4_10) and the action's
-    // selector quads (F, I)
-    auto one = [&](uint32_t w, uint32_t v, uint32_t v2, const uint4& F, const uint4& I) {
+    // the ring offsets of one step: per-lane voffsets (section + lane) and the row's soffsets
+    struct Off {
+        uint32_t s, s2, a, r, d;  // VGPR
+        uint32_t o16, o4, o1;     // SGPR: row * n * {16, 4, 1}
+    };
+    // one transition with the word w (+ value words v, v2 under G2048_P4_10), the action's
+    // selector quads (F, I) and the ring offsets o
+    auto one = [&](uint32_t w, uint32_t v, uint32_t v2, const uint4& F, const uint4& I,
+                   const Off& o) {
         G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s, soff * 16u,
-                                               0);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, o.s, o.o16, 0);
         bool done;
         const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2, soff * 16u,
-                                               0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, v_a, soff, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(r, rw, v_r, soff * 4u, 0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, v_d, soff, 0);
-        soff = soff + n32 == cap32 ? 0u : soff + n32;
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, o.s2, o.o16, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, o.a, o.o1, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(r, rw, o.r, o.o4, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, o.d, o.o1, 0);
         // a wave-uniform branch whose body is selects: every value keeps its registers (a
         // lane-masked `if (done)` made hipcc copy the board and counters through phi moves, and
         // a v_mov costs a full issue turn)
@@ -695,10 +717,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             m.y = sel_lanes(dl, 0u, m.y);
         }
     };
+    // F, I of the action in w's top two bits: 64 B per action in s_dir
     auto sel = [&](uint32_t w, uint4& F, uint4& I) {
-        const uint32_t a2 = (w >> 30) * 2u;
-        F = s_dir[a2];
-        I = s_dir[a2 + 1u];
+        const uint32_t off = (w >> 24) & 0xC0u;
+        F = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s_dir) + off);
+        I = *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(s_dir) + off + 16u);
+    };
+    // the running offsets of the one-at-a-time steps (wrap checked per step)
+    auto step_off = [&]() {
+        const Off o{v_s, v_s2, v_a, v_r, v_d, soff * 16u, soff * 4u, soff};
+        soff = soff + n32 == cap32 ? 0u : soff + n32;
+        return o;
     };
     const int K = A.k_steps > 0 ? A.k_steps : 0;
     // steps up to the first quad boundary, one at a time
@@ -712,31 +741,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             uint4 F, I;
             const uint32_t w = word_of(blk, k);
             sel(w, F, I);
-            one(w, word_of(vb, k), word_of(vb2, k), F, I);
+            one(w, word_of(vb, k), word_of(vb2, k), F, I, step_off());
         }
     }
-    // whole quads, software-pipelined by one quad: the selector reads of quad j are in flight
-    // while the block(s) of quad j + 1 are drawn (the last iteration draws blocks it does not
-    // use); two quads per iteration, so the blocks alternate between two register sets
+    // whole quads: the block(s) of quad j + 1 are drawn at the top of quad j; each step issues
+    // the selector reads of the next step before its own work (the last quad reads selectors
+    // and draws blocks it does not use); two quads per iteration, so the blocks alternate
+    // between two register sets
     uint64_t quad = (t0 + (uint64_t)nh) >> 2;
     blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, quad);
     value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, quad, vb, vb2);
+    // kQR: the quad's row offsets -- loop-invariant VGPRs for its four rows, SGPR quad base
+    const uint32_t st16 = 16u * n32, st4 = 4u * n32;
+    const uint32_t vq_s[4] = {v_s, v_s + st16, v_s + 2u * st16, v_s + 3u * st16};
+    const uint32_t vq_s2[4] = {v_s2, v_s2 + st16, v_s2 + 2u * st16, v_s2 + 3u * st16};
+    const uint32_t vq_a[4] = {v_a, v_a + n32, v_a + 2u * n32, v_a + 3u * n32};
+    const uint32_t vq_r[4] = {v_r, v_r + st4, v_r + 2u * st4, v_r + 3u * st4};
+    const uint32_t vq_d[4] = {v_d, v_d + n32, v_d + 2u * n32, v_d + 3u * n32};
+    uint4 F, I;
+    sel(blk.x, F, I);
     auto quad_of = [&](const uint4& cur, const uint4& cv, const uint4& cv2, uint4& nxt, uint4& nv,
                        uint4& nv2, uint64_t q_next) {
-        uint4 F0, I0, F1, I1, F2, I2, F3, I3;
-        G2048_MARK(selectors, "+v"(F0.x));
-        sel(cur.x, F0, I0);
-        sel(cur.y, F1, I1);
-        sel(cur.z, F2, I2);
-        sel(cur.w, F3, I3);
-        G2048_MARK(philox, "+v"(F0.x), "+v"(F3.x));
+        G2048_MARK(philox, "+v"(F.x));
         nxt = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, q_next);
         value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, q_next, nv, nv2);
         G2048_MARK(step, "+v"(nxt.x), "+v"(nxt.y), "+v"(nxt.z), "+v"(nxt.w));
-        one(cur.x, cv.x, cv2.x, F0, I0);
-        one(cur.y, cv.y, cv2.y, F1, I1);
-        one(cur.z, cv.z, cv2.z, F2, I2);
-        one(cur.w, cv.w, cv2.w, F3, I3);
+        const uint32_t ws[5] = {cur.x, cur.y, cur.z, cur.w, nxt.x};
+        const uint32_t vs[4] = {cv.x, cv.y, cv.z, cv.w}, v2s[4] = {cv2.x, cv2.y, cv2.z, cv2.w};
+        const uint32_t q16 = soff * 16u, q4 = soff * 4u, q1 = soff;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint4 Fn, In;
+            sel(ws[j + 1], Fn, In);  // the next step's selectors, in flight during this step
+            asm volatile("" ::: "memory");
+            if constexpr (kQR)
+                one(ws[j], vs[j], v2s[j], F, I,
+                    Off{vq_s[j], vq_s2[j], vq_a[j], vq_r[j], vq_d[j], q16, q4, q1});
+            else
+                one(ws[j], vs[j], v2s[j], F, I, step_off());
+            F = Fn;
+            I = In;
+        }
+        if constexpr (kQR) soff = soff + 4u * n32 == cap32 ? 0u : soff + 4u * n32;
     };
     int nq = (K - nh) >> 2;
     for (; nq >= 2; nq -= 2, quad += 2) {
@@ -753,12 +799,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         vb2 = w1;
         ++quad;
     }
-    // the last K mod 4 steps (a partial quad)
+    // the last K mod 4 steps (a partial quad): F, I already hold the first one's selectors
     for (int k = 0; k < ((K - nh) & 3); ++k) {
-        uint4 F, I;
         const uint32_t w = word_of(blk, (uint32_t)k);
-        sel(w, F, I);
-        one(w, word_of(vb, (uint32_t)k), word_of(vb2, (uint32_t)k), F, I);
+        if (k) sel(w, F, I);
+        one(w, word_of(vb, (uint32_t)k), word_of(vb2, (uint32_t)k), F, I, step_off());
     }
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
@@ -1358,14 +1403,16 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
         else hipLaunchKernelGGL((k_rollout<false, false, false>), grid, block, 0, st, A);
     } else if (A.rb.win_bytes && !A.log && !(A.flags & G2048_NO_AUTORESET)) {
         // the headline case
-        const bool p410 = (A.flags & G2048_P4_10) != 0u;
+        const bool p410 = (A.flags & G2048_P4_10) != 0u, qr = A.rb.rows % 4 == 0;
+#define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q>), grid, block, 0, st, A)
         if (reward_sum) {
-            if (p410) hipLaunchKernelGGL((k_rollout_lean<true, true>), grid, block, 0, st, A);
-            else hipLaunchKernelGGL((k_rollout_lean<true, false>), grid, block, 0, st, A);
+            if (p410) { if (qr) G2048_LEAN(true, true, true); else G2048_LEAN(true, true, false); }
+            else { if (qr) G2048_LEAN(true, false, true); else G2048_LEAN(true, false, false); }
         } else {
-            if (p410) hipLaunchKernelGGL((k_rollout_lean<false, true>), grid, block, 0, st, A);
-            else hipLaunchKernelGGL((k_rollout_lean<false, false>), grid, block, 0, st, A);
+            if (p410) { if (qr) G2048_LEAN(false, true, true); else G2048_LEAN(false, true, false); }
+            else { if (qr) G2048_LEAN(false, false, true); else G2048_LEAN(false, false, false); }
         }
+#undef G2048_LEAN
     } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);
         else hipLaunchKernelGGL((k_rollout<true, true, false>), grid, block, 0, st, A);

@@ -341,25 +341,8 @@ __device__ __forceinline__ Board fresh_board(uint4 u, uint32_t p4_thresh) {
     return b;
 }
 
-// ------------------------------------------------------------------ random policy, lean step
-// The random-policy step (np.random.randint(4) actions, src/dqn_lib.py:20-21) draws two words
-// (wa, wb) -- half of a DOMAIN_RANDOM block, see random_block.  Bits:
-//   action      wa >> 30
-//   spawn cell  the k-th empty cell, k = floor((wa << 2) * n / 2^32)   (wa bits 0..29)
-//   spawn value a 4 (exponent 2) iff wb < p4_thresh
-//   auto-reset  (terminal steps, which neither move nor spawn): first cell (wa >> 26) & 15,
-//               second the k2-th of the other 15 with k2 = floor((wa << 6) * 15 / 2^32), a 4
-//               iff (wb & 0xFFFF) < p4_16 resp. (wb >> 16) < p4_16, p4_16 = p4_thresh / 2^16
-//               rounded (0.5 -> 32768 exactly; 0.1 -> 6554 = 0.100006).
-__device__ __forceinline__ uint4 random_block(uint32_t seed_lo, uint32_t seed_hi, uint64_t gid,
-                                              uint64_t pair) {
-    return draw(seed_lo, seed_hi, gid, DOMAIN_RANDOM, pair);
-}
-
-__device__ __forceinline__ uint32_t p4_thresh16(uint32_t p4_thresh) {
-    return (p4_thresh + 0x8000u) >> 16;
-}
-
+// ------------------------------------------------------------------ terminal test
+// The random policy's step (ABI v3, include/g2048.h) lives in g2048_roll.hpp.
 // No legal move (src/dqn_lib.py:17-18: max(available_moves) == 0) without the 4-direction mask:
 // a board with both an empty and a non-empty cell always has one (some tile borders a hole), so
 // it is terminal iff it is full with no equal neighbours, or empty.
@@ -370,46 +353,6 @@ __device__ __forceinline__ bool is_done(const Board& b) {
     const uint32_t V = z80(b.r0 ^ b.r1) | z80(b.r1 ^ b.r2) | z80(b.r2 ^ b.r3);
     // one compare: min(no-move witnesses, any tile) == 0
     return min(z | (H & 0x00808080u) | V, b.r0 | b.r1 | b.r2 | b.r3) == 0u;
-}
-
-// spawn() without branches; on_mask = 0 (spawn exponent 0) leaves the board as it is.  The
-// board must have an empty cell when on_mask is set (a move that changed it always leaves one).
-__device__ __forceinline__ void spawn_if(Board& b, uint32_t u_cell, uint32_t u_val,
-                                         uint32_t p4_thresh, uint32_t on_mask) {
-    spawn_at(b, u_cell, (u_val < p4_thresh ? 2u : 1u) & on_mask);
-}
-
-// One random-policy transition of board b with words (wa, wb): slide (a board the chosen move
-// leaves unchanged is its own slide, so an invalid or terminal move spawns nothing), spawn,
-// terminal test of the board BEFORE the move.  Returns the merge gain (0 unless it moved).
-__device__ __forceinline__ uint32_t random_step(Board& b, uint32_t wa, uint32_t wb,
-                                                uint32_t p4_thresh, bool& done) {
-    Board nb = b;
-    uint32_t flags;
-    const uint32_t gain = apply_move(nb, wa >> 30, &flags);
-    // all-ones iff the move changed the board.  The OR is opaque to the compiler (inline asm):
-    // otherwise hipcc splits it into four v_cmp whose lane masks it merges with s_or_b64, and at
-    // one wave per SIMD every SALU op costs an issue turn.
-    const uint32_t diff = or3_v(nb.r0 ^ b.r0, nb.r1 ^ b.r1, (nb.r2 ^ b.r2) | (nb.r3 ^ b.r3));
-    const uint32_t moved = (uint32_t)((int32_t)(diff | (0u - diff)) >> 31);
-    // is_done(b) from the slide's own flags: min(flags, any tile) == 0 (an empty board is done)
-    done = min(flags, or3_v(b.r0, b.r1, b.r2 | b.r3)) == 0u;
-    spawn_if(nb, wa << 2, wb, p4_thresh, moved);
-    b = nb;
-    return gain;
-}
-
-// Auto-reset board of a terminal random-policy step (bits: see above).  The two tiles are placed
-// with 64-bit shifts into the board's halves {r0, r1} / {r2, r3} (fewer selects than set_cell).
-__device__ __forceinline__ Board fresh_board_random(uint32_t wa, uint32_t wb, uint32_t p4_16) {
-    const uint32_t ca = (wa >> 26) & 15u;
-    const uint32_t k2 = __umulhi(wa << 6, 15u);
-    const uint32_t cb = k2 + (uint32_t)(k2 >= ca);
-    const uint64_t ta = (uint64_t)((wb & 0xFFFFu) < p4_16 ? 2u : 1u) << (8u * (ca & 7u));
-    const uint64_t tb = (uint64_t)((wb >> 16) < p4_16 ? 2u : 1u) << (8u * (cb & 7u));
-    const uint64_t lo = (ca < 8u ? ta : 0u) | (cb < 8u ? tb : 0u);
-    const uint64_t hi = (ca < 8u ? 0u : ta) | (cb < 8u ? 0u : tb);
-    return Board{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 }
 
 // ------------------------------------------------------------------ policy (src/dqn_lib.py:16-30)

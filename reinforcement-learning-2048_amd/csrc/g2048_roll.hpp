@@ -3,9 +3,9 @@
 // (tools/opcost.hip, tools/pairbench.hip): with one wave per SIMD every VALU op costs one issue
 // turn of ~5.1-5.9 shader cycles whatever it computes, v_mad_u64_u32 / v_lshlrev_b64 / v_mov
 // cost 8-10, SALU ops 8-10; a second wave per SIMD adds throughput only for plain VOP2 ops.  So the
-// step is bound by its instruction count, and this file minimises it.  Same results as
-// random_step + fresh_board_random (g2048_board.hpp), bit for bit (tests/test_env_gpu.py and
-// tools/rollexp.hip compare the two kernels on every output).
+// step is bound by its instruction count, and this file minimises it.  The single-step kernel
+// and the general k_rollout use the same functions; the oracle restates them (oracle2048.c) and
+// tests/test_fullsize_gpu.py + tools/rollexp.hip compare the kernels on every output.
 //
 // Direction handling without selects: a 4x4 byte board in four row words goes to the four LINE
 // words of the move (byte j = line j, word k = k-th cell along the move, see g2048_board.hpp) by
@@ -101,6 +101,70 @@ __device__ __forceinline__ uint32_t sel_lanes(uint64_t on, uint32_t a, uint32_t 
     uint32_t d;
     asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(d) : "v"(b), "v"(a), "s"(on));
     return d;
+}
+
+// The merge gain: sum over the bytes b of (f01_b << e01_b) + (f2_b << e2_b), f = 0x01 per merging
+// line -- eight SDWA shifts whose byte-select operands do the extractions, summed with three
+// v_add3.  One asm block: after an inline-asm result hipcc pads its consumer with an s_nop (it
+// cannot rule out a transcendental op, whose result needs a wait state); inside the block the
+// shifts (dst_sel DWORD) need none.
+__device__ __forceinline__ uint32_t merge_gain(uint32_t e01, uint32_t f01, uint32_t e2, uint32_t f2) {
+    uint32_t g, t0, t1, t2, t3, t4, t5, t6;
+    asm("v_lshlrev_b32_sdwa %1, %8, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_lshlrev_b32_sdwa %2, %8, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_lshlrev_b32_sdwa %3, %8, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2\n\t"
+        "v_lshlrev_b32_sdwa %4, %8, %9 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_lshlrev_b32_sdwa %5, %10, %11 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0\n\t"
+        "v_lshlrev_b32_sdwa %6, %10, %11 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:BYTE_1\n\t"
+        "v_lshlrev_b32_sdwa %7, %10, %11 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:BYTE_2\n\t"
+        "v_add3_u32 %1, %1, %2, %3\n\t"
+        "v_lshlrev_b32_sdwa %2, %10, %11 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:BYTE_3\n\t"
+        "v_add3_u32 %4, %4, %5, %6\n\t"
+        "v_add3_u32 %0, %1, %4, %7\n\t"
+        "v_add_u32 %0, %0, %2"
+        : "=&v"(g), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6)
+        : "v"(e01), "v"(f01), "v"(e2), "v"(f2));
+    return g;
+}
+
+// 0x80 flags of the equal non-empty neighbours along the compacted lines: ab (cells 0, 1), bc
+// (1, 2), cd (2, 3) -- the later cell non-empty implies the earlier one is.  v_xad: bit 7 of
+// (x ^ y) + 0x7F is set iff the bytes differ, of y + 0x7F iff y != 0; bitop3 0x08 = ~S0 & S1 & S2
+// (table index S0*4 + S1*2 + S2).  One asm block (see merge_gain).
+__device__ __forceinline__ void pair_flags(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           uint32_t& ab, uint32_t& bc, uint32_t& cd) {
+    uint32_t x0, x1, x2;
+    asm("v_xad_u32 %3, %6, %7, %10\n\t"
+        "v_xad_u32 %4, %7, %8, %10\n\t"
+        "v_xad_u32 %5, %8, %9, %10\n\t"
+        "v_add_u32 %0, %7, %10\n\t"
+        "v_add_u32 %1, %8, %10\n\t"
+        "v_add_u32 %2, %9, %10\n\t"
+        "v_bitop3_b32 %0, %3, %0, %11 bitop3:0x08\n\t"
+        "v_bitop3_b32 %1, %4, %1, %11 bitop3:0x08\n\t"
+        "v_bitop3_b32 %2, %5, %2, %11 bitop3:0x08"
+        : "=&v"(ab), "=&v"(bc), "=&v"(cd), "=&v"(x0), "=&v"(x1), "=&v"(x2)
+        : "v"(c0), "v"(c1), "v"(c2), "v"(c3), "v"(K7F), "v"(K80));
+}
+
+// Equal neighbours ACROSS the lines: 0x80 flags of the bytes j < 3 of any line word equal to byte
+// j + 1 (v_xad: bit 7 of (x ^ y) + 0x7F is set iff the bytes differ).  One asm block (see
+// merge_gain).
+__device__ __forceinline__ uint32_t across_pairs(uint32_t l0, uint32_t l1, uint32_t l2, uint32_t l3) {
+    uint32_t r, a0, a1, a2, a3;
+    asm("v_alignbit_b32 %1, %6, %5, 8\n\t"
+        "v_alignbit_b32 %2, %7, %6, 8\n\t"
+        "v_alignbit_b32 %3, %8, %7, 8\n\t"
+        "v_lshrrev_b32 %4, 8, %8\n\t"
+        "v_xad_u32 %1, %5, %1, %9\n\t"
+        "v_xad_u32 %2, %6, %2, %9\n\t"
+        "v_xad_u32 %3, %7, %3, %9\n\t"
+        "v_xad_u32 %4, %8, %4, %9\n\t"
+        "v_bitop3_b32 %1, %1, %2, %3 bitop3:0x80\n\t"
+        "v_bitop3_b32 %0, %1, %4, %10 bitop3:0x2a"  // ~(S0 & S1) & S2 (table index S0*4 + S1*2 + S2)
+        : "=v"(r), "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3)
+        : "v"(l0), "v"(l1), "v"(l2), "v"(l3), "v"(K7F), "v"(0x00808080u));
+    return r;
 }
 
 // bits [31:0] of {hi, lo} >> s
@@ -222,9 +286,8 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     G2048_MARK(merge, "+v"(C0), "+v"(C1), "+v"(C2), "+v"(C3));
     // 2) merges, front first (the later cell is non-empty => so is the earlier one)
     //    (v_xad: bit 7 of (x ^ y) + 0x7F set iff the bytes differ; of y + 0x7F iff y != 0)
-    const uint32_t ab = ~xad(C0, C1, K7F) & (C1 + K7F) & K80;
-    const uint32_t bc_raw = ~xad(C1, C2, K7F) & (C2 + K7F) & K80;
-    const uint32_t cd_raw = ~xad(C2, C3, K7F) & (C3 + K7F) & K80;
+    uint32_t ab, bc_raw, cd_raw;
+    pair_flags(C0, C1, C2, C3, ab, bc_raw, cd_raw);
     const uint32_t bc = bc_raw & ~ab;
     const uint32_t cd = cd_raw & (ab | ~bc_raw);
     const uint32_t AB = expand80(ab), BC = expand80(bc), CD = expand80(cd);
@@ -240,11 +303,11 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     //    c+d, so two words of candidates; shifting the 0x01 merge flag (not 1) by each byte makes
     //    a line without a merge contribute 0
     const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD, f01 = f_ab | f_bc;
-    uint32_t gain = shl_bytes(e01, f01) + shl_bytes(e2, f_cd);
+    uint32_t gain = merge_gain(e01, f01, e2, f_cd);
     G2048_MARK(moved_done, "+v"(gain));
     // 4) moved: a hole before a tile along a line, or a merge
     const uint32_t hb = ((D0 & ~D1) | (D1 & ~D2) | (D2 & ~D3)) & K80;
-    uint32_t mv = hb | or3_v(ab, bc_raw, cd_raw);
+    uint32_t mv = hb | ab | bc_raw | cd_raw;
     G2048_MARK(spawn, "+v"(mv));
     // 5) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
     //    line words (exponents < 32: no borrow; at most 4 * 0x20 per byte: no carry)
@@ -271,10 +334,7 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     //    always leaves one, so n == 0 iff nothing moved and the board is full) and no equal
     //    neighbours across the lines (adjacent bytes of a line word; v_xad: bit 7 of
     //    (x ^ y) + 0x7F is set iff the bytes differ) -- or the board is empty (n == 16)
-    const uint32_t Y0 = xad(L0, alignbit(L1, L0, 8u), K7F), Y1 = xad(L1, alignbit(L2, L1, 8u), K7F);
-    const uint32_t Y2 = xad(L2, alignbit(L3, L2, 8u), K7F), Y3 = xad(L3, L3 >> 8, K7F);
-    const uint32_t across = ~(Y0 & Y1 & Y2 & Y3) & 0x00808080u;
-    done = min(n | across, 16u - n) == 0u;
+    done = min(n | across_pairs(L0, L1, L2, L3), 16u - n) == 0u;
     // 7) back to rows
     G2048_MARK(net_inv, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
     dir_net(o0, o1, o2, o3, I, b.r0, b.r1, b.r2, b.r3);

@@ -35,16 +35,43 @@ class BoardBatch:
     """A batch of boards that are not an env's (sampled replay rows, the before / after boards
     of a step): the same `board` (u8 [n, 16] exponents), `n`, `device` and `encode()` as
     VecEnv2048, so every board_to_tensor_function -- the reference's two or a caller's own --
-    takes either."""
+    takes either.  The Board2048 accessors a reward_function may use (src/board.py:204-231)
+    answer for all n boards at once: `state` (tile values, int64 [n, 4, 4], 0 = empty),
+    `merge_score()` (int64 [n], when the batch carries the scores: play_one_step passes the
+    scores before / after the move), `simple_score()`, `log_scale()` (a batch whose `state` is
+    the exponents) and `number_of_empty_cells()`."""
 
-    def __init__(self, board: torch.Tensor):
+    def __init__(self, board: torch.Tensor, score: torch.Tensor | None = None, log: bool = False):
         self.board = board
         self.n = board.shape[0]
         self.device = board.device
+        self._score = score
+        self._log = log
 
     def encode(self, dtype=torch.float32, conv: bool = True):
         x = self.board.to(dtype)
         return x.view(self.n, 1, 4, 4) if conv else x
+
+    @property
+    def state(self) -> torch.Tensor:
+        e = self.board.to(torch.int64)
+        v = e if self._log else torch.where(e > 0, torch.ones_like(e) << e, torch.zeros_like(e))
+        return v.view(self.n, 4, 4)
+
+    def merge_score(self) -> torch.Tensor:
+        if self._score is None:
+            raise TypeError("merge_score(): this BoardBatch carries no scores (only the before / "
+                            "after boards that play_one_step hands a reward_function do)")
+        return self._score
+
+    def simple_score(self) -> torch.Tensor:
+        return BoardBatch(self.board).state.flatten(1).sum(1)
+
+    def log_scale(self) -> "BoardBatch":
+        return BoardBatch(self.board, self._score, log=True)
+
+    def number_of_empty_cells(self) -> torch.Tensor:
+        return (self.board == 0).sum(1)
 
 
 _FUSED_ENCODERS = (board_as_4d_tensor, board_as_flattened_tensor)
@@ -56,13 +83,16 @@ def reward_func_merge_score(board=None, next_board=None, action=None, done=None)
     raise RuntimeError("reward_func_merge_score is computed inside the env step kernel")
 
 
-def _custom_rewards(reward_function, s, s2, action, done, replay_buffer, row0):
+def _custom_rewards(reward_function, s, s2, action, done, replay_buffer, row0, score0, gain):
     """A caller's reward_function(board, next_board, action, done) (src/dqn_lib.py:97,104) over
     the whole batch -- BoardBatch views of the boards before / after the move (s' = s for
-    terminal and invalid moves, as the reference's peek_action), actions and done flags as
-    tensors -- written over the kernel's merge-score rewards in the ring rows just appended.
-    The ring stores rewards as int32 (the reference's merge-score rewards are ints)."""
-    r = reward_function(BoardBatch(s), BoardBatch(s2), action, done)
+    terminal and invalid moves, as the reference's peek_action) carrying the merge scores before
+    (score0) and after (score0 + the kernel's merge gain), so the reference's own
+    `next_board.merge_score() - board.merge_score()` works; actions and done flags as tensors --
+    written over the kernel's merge-score rewards in the ring rows just appended.  The ring
+    stores rewards as int32 (the reference's merge-score rewards are ints)."""
+    r = reward_function(BoardBatch(s, score0), BoardBatch(s2, score0 + gain.to(torch.int64)),
+                        action, done)
     r = torch.as_tensor(r, device=s.device)
     if r.shape != (s.shape[0],):
         raise ValueError(f"reward_function must return one reward per board ({s.shape[0]})")
@@ -104,8 +134,10 @@ def play_one_step(env: VecEnv2048, epsilon, model: torch.nn.Module, replay_buffe
     (s, a, 0, s, 1) and are re-dealt.  With epsilon >= 1 no Q-values are needed and `model`
     may be None (the random branch returns before the forward, :20-21).
     A reward_function other than reward_func_merge_score is called as the reference calls it
-    (board, next_board, action, done), batched (see _custom_rewards); it needs the replay
-    buffer, where the transition's s' lives after the auto-reset.
+    (board, next_board, action, done), batched: board / next_board are BoardBatch objects (the
+    Board2048 accessors over all boards, merge scores included), action / done tensors, and it
+    returns one reward per board (see _custom_rewards); it needs the replay buffer, where the
+    transition's s' lives after the auto-reset.
     Returns (env, actions, rewards, dones, max_q_values)."""
     custom = reward_function is not reward_func_merge_score
     if custom and replay_buffer is None:
@@ -115,11 +147,12 @@ def play_one_step(env: VecEnv2048, epsilon, model: torch.nn.Module, replay_buffe
     else:
         q = q_values(env, model, board_to_tensor_function)
     s = env.board.clone() if custom else None
+    score0 = (env.meta[:, 0].to(torch.int64) & 0xFFFFFFFF) if custom else None  # u32 in int32
     row0 = int(env.clock[0]) % (replay_buffer.capacity // env.n) * env.n if custom else 0
     action, reward, done = env.step_egreedy(q, epsilon, replay=replay_buffer)
     if custom:
         reward = _custom_rewards(reward_function, s, replay_buffer.s2[row0:row0 + env.n],
-                                 action, done, replay_buffer, row0)
+                                 action, done, replay_buffer, row0, score0, reward)
     return env, action, reward, done, q.amax(1)
 
 

@@ -24,6 +24,10 @@ from .nets import NETS, make_net
 from . import qnet
 from .optim import FusedAdam
 
+# Trainer.state_dict layout (experiment.py wraps it in its own file format tag).  1 (round 1): env meta [N, 4], no clock.  3: meta [N, 2] + a per-wave
+# clock, and the ABI-v3 random policy (include/g2048.h), whose draws differ from earlier builds'.
+TRAINER_STATE_VERSION = 3
+
 
 class DQNLearner:
     def __init__(self, replay: ReplayBuffer, net: str = "conv", dtype=torch.float32,
@@ -363,18 +367,6 @@ class Trainer:
             self.env.step_egreedy(q, None, replay=self.replay, reward=self._reward,
                                   done=self._done, action=self._action, eps_schedule=sched)
 
-    def _warm_forward(self) -> None:
-        """A rollout step whose Q comes from torch (the float64 learners) runs that forward once
-        outside the capture: hipBLASLt sets up a GEMM shape on its first call, which a stream
-        under capture does not permit.  Pure: nothing is stepped."""
-        L = self.learner
-        if L.f64 and L._fwd64 is None and L.kind != "dense64":
-            side = torch.cuda.Stream(self.env.device)
-            side.wait_stream(torch.cuda.current_stream(self.env.device))
-            with torch.cuda.stream(side):
-                L.q_values(self.env)
-            torch.cuda.current_stream(self.env.device).wait_stream(side)
-
     def _graphed_iteration(self) -> None:
         """One iteration (step + updates_per_step updates, target syncs included: the fused
         Adam performs them on the device update counter) as ONE hipGraph replay.  Capture
@@ -385,7 +377,6 @@ class Trainer:
         if L.world > 1:
             return self._graphed_iteration_dp()
         if self._loop_graph is None:
-            self._warm_forward()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._rollout_step()
@@ -402,7 +393,6 @@ class Trainer:
         updates of the iteration run the learner's own two-graph update."""
         L = self.learner
         if self._loop_graph is None:
-            self._warm_forward()
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self._rollout_step()
@@ -512,7 +502,8 @@ class Trainer:
     def state_dict(self) -> dict:
         cpu = lambda t: t.detach().cpu().clone()  # noqa: E731
         env, rb = self.env, self.replay
-        st = {"trainer": {"steps": self.steps, "updates_per_step": self.updates_per_step,
+        st = {"trainer_state_version": TRAINER_STATE_VERSION,
+              "trainer": {"steps": self.steps, "updates_per_step": self.updates_per_step,
                           "min_fill": self.min_fill, "eps_decay": self.eps_decay,
                           "min_eps": self.min_eps},
               "env": {"n": env.n, "seed": env.seed, "board_offset": env.board_offset,
@@ -530,6 +521,12 @@ class Trainer:
     @torch.no_grad()
     def load_state_dict(self, st: dict) -> None:
         self._loop_graph = None  # host-side env state (the reset epoch) is baked into a capture
+        fmt = st.get("trainer_state_version", 1)
+        if fmt != TRAINER_STATE_VERSION:
+            raise ValueError(
+                f"trainer state version {fmt} is not readable by this build (version "
+                f"{TRAINER_STATE_VERSION}: env meta [N, 2] + per-wave clock, ABI-v3 random-policy "
+                "draws); resume it with the build that wrote it")
         env, rb = self.env, self.replay
         e = st["env"]
         for k in ("n", "seed", "board_offset", "flags"):

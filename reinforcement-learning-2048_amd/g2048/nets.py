@@ -53,7 +53,8 @@ class _LinearSplitK(torch.autograd.Function):
                            x.reshape(s, m // s, -1)).sum(0)
         else:
             gw = gy.t() @ x
-        return gx, gw, gy.sum(0)
+        # b is None for a bias-free layer: autograd takes no gradient for a non-tensor input
+        return gx, gw, (gy.sum(0) if ctx.needs_input_grad[2] else None)
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:

@@ -38,6 +38,21 @@ def test_custom_reward_function(g2048):
     with pytest.raises(ValueError):
         dqn_lib.play_one_step(env, 1.0, None, None, reward_function=empties_after)
 
+    # the reference's own reward shape (src/dqn_lib.py:87-88) on the batch: merge scores after -
+    # before == the kernel's merge-score reward, and the Board2048 accessors answer per board
+    def ref_style(board, next_board, action, done):
+        assert board.state.shape == (board.n, 4, 4) and board.log_scale().state.max() < 32
+        return next_board.merge_score() - board.merge_score()
+
+    for t in range(5):
+        row0 = (6 + t) % 4 * n
+        before = env.meta[:, 0].clone().long()
+        _, a, r, d, _ = dqn_lib.play_one_step(env, 1.0, None, rb, reward_function=ref_style)
+        gain = rb.r[row0:row0 + n].long()
+        assert torch.equal(r.long(), gain) and int(gain.sum()) > 0, t
+        live = d == 0  # the env re-deals terminal boards (score 0), the ring keeps the transition
+        assert torch.equal((before + gain)[live], env.meta[:, 0].long()[live]), t
+
     def halves(board, next_board, action, done):
         return torch.full((board.n,), 0.5, device=board.device)
 

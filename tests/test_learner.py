@@ -181,3 +181,38 @@ def test_fused_f64_routing_on_cpu():
         qnet.Dense64Update64(conv64, conv64, 512)
     with pytest.raises(ValueError):  # float64 on the CPU: the fused kernels need CUDA tensors
         qnet.ConvUpdate64(conv64, conv64, 512)
+
+
+def test_board_batch_accessors():
+    """BoardBatch answers the Board2048 accessors a reward_function uses (src/board.py:204-231)
+    for every board: state (tile values), log_scale().state (exponents), simple_score,
+    number_of_empty_cells, merge_score (carried scores; a clear TypeError without them)."""
+    b = torch.zeros((3, 16), dtype=torch.uint8)
+    b[0, :3] = torch.tensor([1, 2, 17])
+    b[2, 15] = 31
+    bb = dqn_lib.BoardBatch(b, score=torch.tensor([4, 0, 8]))
+    st = bb.state
+    assert st.dtype == torch.int64 and st.shape == (3, 4, 4)
+    assert st[0, 0, :3].tolist() == [2, 4, 131072] and int(st[2, 3, 3]) == 2 ** 31
+    assert torch.equal(bb.log_scale().state.reshape(3, 16), b.long())
+    assert bb.simple_score().tolist() == [2 + 4 + 131072, 0, 2 ** 31]
+    assert bb.number_of_empty_cells().tolist() == [13, 16, 15]
+    assert bb.merge_score().tolist() == [4, 0, 8]
+    with pytest.raises(TypeError):
+        dqn_lib.BoardBatch(b).merge_score()
+
+
+def test_split_k_linear_without_bias():
+    """nets.Linear(bias=False) (the split-K weight-gradient layer) backpropagates: no gradient
+    is returned for the absent bias, and dW / dX match F.linear's."""
+    from g2048.nets import Linear
+
+    torch.manual_seed(0)
+    lin = Linear(16, 8, bias=False).double()
+    x = torch.randn(4096, 16, dtype=torch.float64, requires_grad=True)  # 4096 rows: split-K path
+    lin(x).square().sum().backward()
+    w2 = lin.weight.detach().clone().requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    torch.nn.functional.linear(x2, w2).square().sum().backward()
+    torch.testing.assert_close(lin.weight.grad, w2.grad, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(x.grad, x2.grad, rtol=1e-12, atol=1e-12)

@@ -78,6 +78,10 @@ def test_load_rejects_mismatch(G):
     c = _small(G, "conv", seed=4)
     with pytest.raises(ValueError):
         c.load_state_dict(st)
+    old = dict(st)
+    old.pop("trainer_state_version")  # a round-1 trainer state (env meta [N, 4], no clock)
+    with pytest.raises(ValueError, match="trainer state version 1"):
+        a.load_state_dict(old)
 
 
 def _move_ok(s, a, s2, r, letters=("u", "d", "l", "r")):

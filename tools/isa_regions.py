@@ -10,7 +10,7 @@ import re
 import sys
 from collections import Counter, defaultdict
 
-KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0EEEvNS_8StepArgsE"  # <kSum=false, kP410=false>
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0ELb1EEEvNS_8StepArgsE"  # <kSum=0, kP410=0, kQR=1>
 
 
 def kind(op):

@@ -22,7 +22,7 @@ void launch_lean(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
     make_args(e, rb, A);
     A.k_steps = K;
-    hipLaunchKernelGGL((k_rollout_lean<false, false>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+    hipLaunchKernelGGL((k_rollout_lean<false, false, true>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
 }
 
 struct Variant {
