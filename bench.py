@@ -72,8 +72,9 @@ def parse():
                    help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
     p.add_argument("--seed", type=int, default=0x2048)
-    p.add_argument("--train", default="dense64,conv,dense",
-                   help="learner nets to time (comma list of dense64,conv,dense; '' = none)")
+    p.add_argument("--train", default="dense64,conv,dense,dense@5000",
+                   help="learner legs to time: comma list of dense64 / conv / dense, each "
+                        "optionally @batch (default --batch); '' = none")
     p.add_argument("--train-dtypes", default="fp32,fp64")
     p.add_argument("--train-updates", type=int, default=200)
     p.add_argument("--batch", type=int, default=8192)
@@ -263,7 +264,7 @@ def bench_step(args, world, rank, dev):
 
 
 # ------------------------------------------------------------------ learner
-def bench_train(args, world, rank, dev, net, dtype):
+def bench_train(args, world, rank, dev, net, dtype, batch):
     """BASELINE configs[2]/[3] (configs[4] at --gpus 8): N boards + Double-DQN, replay 1M,
     B = 8192, gradient all-reduce over RCCL when world > 1.  (a) learner updates alone,
     (b) the training-loop iteration = Q of the greedy-branch boards + fused eps-greedy step /
@@ -276,7 +277,7 @@ def bench_train(args, world, rank, dev, net, dtype):
     env = g2048.VecEnv2048(n, seed=args.seed + 7, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(C, device=dev)
     tdt = torch.float32 if dtype == "fp32" else torch.float64
-    L = DQNLearner(rb, net=net, dtype=tdt, batch_size=args.batch, target_sync_every=100)
+    L = DQNLearner(rb, net=net, dtype=tdt, batch_size=batch, target_sync_every=100)
     T = Trainer(env, rb, L, updates_per_step=1, min_fill=0)
     T.prefill(C // n)  # replay pre-filled by random-policy rollout steps (one launch)
     for _ in range(5):
@@ -303,7 +304,7 @@ def bench_train(args, world, rank, dev, net, dtype):
         got = [torch.empty_like(flat) for _ in range(world)]
         dist.all_gather(got, flat)
         lockstep = all(torch.equal(got[0], g) for g in got[1:])
-    fl = flops_per_update(net, args.batch)
+    fl = flops_per_update(net, batch)
     peak = FP32_PEAK_TF if dtype == "fp32" else FP64_PEAK_TF
     tf = fl / (upd_ev / K) / 1e12
     return {"updates_per_s": K / upd_wall, "update_ms": upd_ev / K * 1e3,
@@ -316,7 +317,7 @@ def bench_train(args, world, rank, dev, net, dtype):
             "loop_late_iter_ms": late_wall / K2 * 1e3,
             "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
             "loop_late_epsilon_mean": eps_late,
-            "batch": args.batch, "replay": C, "dtype": dtype, "loss": loss,
+            "batch": batch, "replay": C, "dtype": dtype, "loss": loss,
             "params": L.n_params, "graphed_loop": T.graph, "ranks_lockstep": lockstep}
 
 
@@ -328,6 +329,8 @@ def cpu_baselines(args):
 
     env = CB.env_baseline(args.cpu_seconds)
     env["learner"] = [CB.learner_baseline("conv", b, updates=2) for b in (5000, 8192)]
+    # BASELINE configs[0]: the dense net at its own batch (src/configs/double_dqn_dense.py:17)
+    env["learner"].append(CB.learner_baseline("dense", 5000, updates=2))
     return env
 
 
@@ -351,9 +354,11 @@ def main():
                        "launch_us": lx * 1e6, "frac": ROLLOUT_BYTES * n * kx / lx / 1e9 / HBM_PEAK_GBS})
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
-    for net in [x for x in args.train.split(",") if x]:
+    for leg in [x for x in args.train.split(",") if x]:
+        net, _, b = leg.partition("@")  # "dense@5000": that net at that batch
         for dt in [x for x in args.train_dtypes.split(",") if x]:
-            train[f"{net}.{dt}"] = bench_train(args, world, rank, dev, net, dt)
+            train[f"{leg}.{dt}"] = bench_train(args, world, rank, dev, net, dt,
+                                               int(b) if b else args.batch)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args)

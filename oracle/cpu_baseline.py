@@ -157,7 +157,11 @@ def learner_baseline(net: str = "conv", batch: int = 8192, updates: int = 3,
             "dtype": "fp64", "batch": batch, "net": net,
             "sample": f"{updates} float64 train_steps of the reference {net} Sequential at "
                       f"B={batch} on torch CPU ({threads} threads), sampled from a "
-                      f"{cap}-row oracle-filled ring ({dt:.1f} s)"}
+                      f"{cap}-row oracle-filled ring ({dt:.1f} s); the batch is drawn and "
+                      f"encoded by the oracle's C sampler (o2048_replay_sample_f64), which "
+                      f"replaces the reference's Python extract_samples_* loops "
+                      f"(src/dqn_lib.py:33-84), so this leg is faster than the reference's "
+                      f"own train_step"}
 
 
 if __name__ == "__main__":
@@ -166,3 +170,4 @@ if __name__ == "__main__":
     else:
         print(json.dumps(env_baseline(2.0)))
         print(json.dumps(learner_baseline("conv", 5000, 1)))
+        print(json.dumps(learner_baseline("dense", 5000, 1)))

@@ -538,6 +538,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     // one transition of step t with its draws rw (g2048_roll.hpp)
     // lean (std::true_type): no episode log and auto-reset on -- the loop then carries neither
     // uniform test
+    const uint32_t k255 = opaque_255();
     auto one = [&](auto lean, const RandWords& rd, uint64_t t) {
         constexpr bool kLean = decltype(lean)::value;
         const uint32_t wa = rd.w;
@@ -547,7 +548,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
         const uint32_t r = lean_step(b, wa,
                                      p410 ? spawn_exp<true>(wa, rd.v, A.p4_thresh)
                                           : spawn_exp<false>(wa, rd.v, A.p4_thresh),
-                                     s_dir[a2], s_dir[a2 + 1u], done);
+                                     s_dir[a2], s_dir[a2 + 1u], done, k255);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
@@ -675,6 +676,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
     const uint32_t ep0 = ep.x;
     Board last = b;
+    const uint32_t k255 = opaque_255();
     // the ring offsets of one step: per-lane voffsets (section + lane) and the row's soffsets
     struct Off {
         uint32_t s, s2, a, r, d;  // VGPR
@@ -687,7 +689,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, o.s, o.o16, 0);
         bool done;
-        const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done);
+        const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done, k255);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;

@@ -33,6 +33,13 @@ namespace g2048 {
 #define G2048_MARK(x, ...)
 #endif
 
+// 255 in a register the compiler cannot see through (lean_step's k255), set once per kernel
+__device__ __forceinline__ uint32_t opaque_255() {
+    uint32_t k = 255u;
+    asm volatile("" : "+v"(k));
+    return k;
+}
+
 // [action][0] forward {SA, SC, S0, S2}, [action][1] inverse; actions 0 up, 1 down, 2 left, 3 right
 // (src/board.py:147-183).  Up, down and left are involutions (inverse == forward).
 __device__ __constant__ const uint32_t kDirNet[4][2][4] = {
@@ -167,6 +174,52 @@ __device__ __forceinline__ uint32_t across_pairs(uint32_t l0, uint32_t l1, uint3
     return r;
 }
 
+// The moved flags of a step: 0x80 per line with a hole before a tile along it -- bit 7 of
+// (D0 & ~D1) | (D1 & ~D2) | (D2 & N3), N3 = L3 + 0x7F (bit 7: cell 3 holds a tile) -- or with a
+// merge (P = ab | bc | cd, 0x80 flags).  Three bitop3 (table index S0*4 + S1*2 + S2): 0x74 =
+// (S0 & ~S1) | (S1 & ~S2), 0xF8 = S0 | (S1 & S2), 0xEA = (S0 & S1) | S2.  One asm block: written
+// in C, hipcc rewrites ~D as L + 0x7F per word (nine ops instead of four).
+__device__ __forceinline__ uint32_t moved_flags(uint32_t D0, uint32_t D1, uint32_t D2, uint32_t L3,
+                                                uint32_t P) {
+    uint32_t mv, n3, x;
+    asm("v_add_u32 %1, %5, %7\n\t"
+        "v_bitop3_b32 %2, %3, %4, %6 bitop3:0x74\n\t"
+        "v_bitop3_b32 %2, %2, %6, %1 bitop3:0xf8\n\t"
+        "v_bitop3_b32 %0, %2, %8, %9 bitop3:0xea"
+        : "=v"(mv), "=&v"(n3), "=&v"(x)
+        : "v"(D0), "v"(D1), "v"(L3), "v"(D2), "v"(K7F), "v"(K80), "v"(P));
+    return mv;
+}
+
+// 0xFF in every byte of a 0x01-flag word: f * 255 (bytes <= 1, so no carries) in one
+// v_mul_lo_u32.  k255 = 255 held opaque in a register: hipcc rewrites a multiply by the
+// constant as (f << 8) - f, two ops.
+__device__ __forceinline__ uint32_t expand01(uint32_t f, uint32_t k255) { return f * k255; }
+
+// The spawn slot from S (byte j: empties in lines 0..j; byte 3: their total):
+//   n  = total mod 16 -- 0 for the empty board as for a full one (neither moves, so neither spawns)
+//   k  = floor((w << 3) * n / 2^32), the rank of the chosen empty cell
+//   j8 = 8 j*, j* = the number of lines j < 3 with S_j <= k: bit 7 of byte j of
+//        X = 0x80 + k - S_j (the bytes stay in [0x70, 0x8F], no borrows)
+//   q  = k - S_j* = (position along line j*) - 4, in [-4, -1]: its two low bits are the position
+// One asm block: in C, hipcc re-derives n and X from the multiply that made S (two more ops).
+__device__ __forceinline__ void spawn_slot(uint32_t S, uint32_t w, uint32_t& n, uint32_t& j8,
+                                           uint32_t& q) {
+    uint32_t t, k;
+    asm("v_bfe_u32 %0, %5, 24, 4\n\t"
+        "v_lshlrev_b32 %3, 3, %6\n\t"
+        "v_mul_hi_u32 %4, %3, %0\n\t"
+        "v_mad_u32_u24 %3, %4, %7, %8\n\t"
+        "v_sub_u32 %3, %3, %5\n\t"
+        "v_and_b32 %3, 0x808080, %3\n\t"
+        "v_bcnt_u32_b32 %3, %3, 0\n\t"
+        "v_lshlrev_b32 %1, 3, %3\n\t"
+        "v_bfe_u32 %3, %5, %1, 8\n\t"
+        "v_sub_u32 %2, %4, %3"
+        : "=&v"(n), "=&v"(j8), "=&v"(q), "=&v"(t), "=&v"(k)
+        : "v"(S), "v"(w), "v"(0x010101u), "v"(0x808080u));
+}
+
 // bits [31:0] of {hi, lo} >> s
 __device__ __forceinline__ uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
     return __builtin_amdgcn_alignbit(hi, lo, s);
@@ -263,14 +316,15 @@ __device__ __forceinline__ void dir_sel_const(uint32_t a, uint4& F, uint4& I) {
 // the reference's uniform choice (src/board.py:41-51); this one needs no search.  Returns the merge
 // gain; done: the board as given was terminal (no legal move, src/dqn_lib.py:17-18).
 // Domain: exponents < 32 (the 0x20-flag sums below; a 4x4 game cannot pass 17).
+//   k255: 255, passed by the rollout kernels as an opaque loop-invariant register (expand01).
 __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, const uint4& F,
-                                              const uint4& I, bool& done) {
+                                              const uint4& I, bool& done, uint32_t k255 = 255u) {
     uint32_t L0, L1, L2, L3;
     G2048_MARK(net_fwd, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
     dir_net(b.r0, b.r1, b.r2, b.r3, F, L0, L1, L2, L3);
     G2048_MARK(compact, "+v"(L0), "+v"(L1), "+v"(L2), "+v"(L3));
     // bit 7 of byte j of D_k: cell k of line j is empty
-    const uint32_t D0 = K80 - L0, D1 = K80 - L1, D2 = K80 - L2, D3 = K80 - L3;
+    const uint32_t D0 = K80 - L0, D1 = K80 - L1, D2 = K80 - L2;
     // 1) stable compaction toward L0, back to front
     uint32_t M = zmask(D2);
     uint32_t C2 = bsel(M, L3, L2), C3 = L3 & ~M;
@@ -290,8 +344,8 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     pair_flags(C0, C1, C2, C3, ab, bc_raw, cd_raw);
     const uint32_t bc = bc_raw & ~ab;
     const uint32_t cd = cd_raw & (ab | ~bc_raw);
-    const uint32_t AB = expand80(ab), BC = expand80(bc), CD = expand80(cd);
     const uint32_t f_ab = ab >> 7, f_bc = bc >> 7, f_cd = cd >> 7;  // 0x01 per merging line
+    const uint32_t AB = expand01(f_ab, k255), BC = expand01(f_bc, k255), CD = expand01(f_cd, k255);
     const uint32_t c1 = C2 + f_cd;
     const uint32_t b1 = C1 + f_bc;
     uint32_t o0 = C0 + f_ab;
@@ -302,12 +356,12 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     // 3) score = sum of 2^e over the merged tiles: a line merges a+b or b+c (never both), and
     //    c+d, so two words of candidates; shifting the 0x01 merge flag (not 1) by each byte makes
     //    a line without a merge contribute 0
-    const uint32_t e01 = (o0 & AB) | (b1 & BC), e2 = c1 & CD, f01 = f_ab | f_bc;
-    uint32_t gain = merge_gain(e01, f01, e2, f_cd);
+    //    (a line's exponent bytes need no mask: where its flag byte is 0 the shift yields 0)
+    const uint32_t e01 = bsel(AB, o0, b1), f01 = f_ab | f_bc;
+    uint32_t gain = merge_gain(e01, f01, c1, f_cd);
     G2048_MARK(moved_done, "+v"(gain));
     // 4) moved: a hole before a tile along a line, or a merge
-    const uint32_t hb = ((D0 & ~D1) | (D1 & ~D2) | (D2 & ~D3)) & K80;
-    uint32_t mv = hb | ab | bc_raw | cd_raw;
+    const uint32_t mv = moved_flags(D0, D1, D2, L3, ab | bc_raw | cd_raw);
     G2048_MARK(spawn, "+v"(mv));
     // 5) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
     //    line words (exponents < 32: no borrow; at most 4 * 0x20 per byte: no carry)
@@ -315,15 +369,11 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     const uint32_t E20 = ((K20 - o0) & K20) + ((K20 - o1) & K20) + ((K20 - o2) & K20) +
                          ((K20 - o3) & K20);
     const uint32_t S = (E20 >> 5) * 0x01010101u;  // byte j: empties in lines 0..j; byte 3: n
-    const uint32_t n = S >> 24;
-    const uint32_t k = __umulhi(w << 3, n);
-    // bit 7 of byte j < 3: S_j > k; the target line j* = the number of lines with S_j <= k
-    const uint32_t T = (S | K80) - (k * 0x010101u + 0x010101u);
-    const uint32_t j8 = (uint32_t)__popc(~T & 0x00808080u) << 3;
-    const uint32_t q = k + 4u - __builtin_amdgcn_ubfe(S, j8, 8u);
+    uint32_t n, j8, q;
+    spawn_slot(S, w, n, j8, q);
     // the tile min(e, mv) (mv is 0 -- no move, no spawn -- or >= 0x80) at bit 8 j* + 32 (q & 1)
-    // of the half {o0, o1} (q < 2) or {o2, o3}: v_lshlrev_b64 reads 6 bits of the shift, and the
-    // half's mask is bit 1 of q sign-extended (q = 4 only without a move, when the tile is 0)
+    // of the half {o0, o1} (q & 2 clear) or {o2, o3}: v_lshlrev_b64 reads 6 bits of the shift,
+    // and the half's mask is bit 1 of q sign-extended (without a move the tile is 0)
     const uint64_t tile = (uint64_t)min(e, mv) << ((q << 5) + j8);
     const uint32_t qm = (uint32_t)__builtin_amdgcn_sbfe((int32_t)q, 1u, 1u);
     o0 |= (uint32_t)tile & ~qm;
@@ -333,8 +383,9 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     // 6) terminal (board as given, src/dqn_lib.py:17-18): no empty cell after a non-move (a move
     //    always leaves one, so n == 0 iff nothing moved and the board is full) and no equal
     //    neighbours across the lines (adjacent bytes of a line word; v_xad: bit 7 of
-    //    (x ^ y) + 0x7F is set iff the bytes differ) -- or the board is empty (n == 16)
-    done = min(n | across_pairs(L0, L1, L2, L3), 16u - n) == 0u;
+    //    (x ^ y) + 0x7F is set iff the bytes differ) -- or the board is empty (16 empties, n mod
+    //    16 = 0, and no tiles to pair)
+    done = (n | across_pairs(L0, L1, L2, L3)) == 0u;
     // 7) back to rows
     G2048_MARK(net_inv, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
     dir_net(o0, o1, o2, o3, I, b.r0, b.r1, b.r2, b.r3);
