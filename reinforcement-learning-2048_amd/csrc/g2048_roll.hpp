@@ -175,19 +175,18 @@ __device__ __forceinline__ uint32_t across_pairs(uint32_t l0, uint32_t l1, uint3
 }
 
 // The moved flags of a step: 0x80 per line with a hole before a tile along it -- bit 7 of
-// (D0 & ~D1) | (D1 & ~D2) | (D2 & N3), N3 = L3 + 0x7F (bit 7: cell 3 holds a tile) -- or with a
+// (D0 & ~D1) | (D1 & ~D2) | (D2 & N3), N3 = L3 + 0x7F7F7F7F (bit 7: cell 3 holds a tile) -- or with a
 // merge (P = ab | bc | cd, 0x80 flags).  Three bitop3 (table index S0*4 + S1*2 + S2): 0x74 =
 // (S0 & ~S1) | (S1 & ~S2), 0xF8 = S0 | (S1 & S2), 0xEA = (S0 & S1) | S2.  One asm block: written
-// in C, hipcc rewrites ~D as L + 0x7F per word (nine ops instead of four).
-__device__ __forceinline__ uint32_t moved_flags(uint32_t D0, uint32_t D1, uint32_t D2, uint32_t L3,
+// in C, hipcc rewrites ~D as L + 0x7F per word (nine ops instead of three).
+__device__ __forceinline__ uint32_t moved_flags(uint32_t D0, uint32_t D1, uint32_t D2, uint32_t N3,
                                                 uint32_t P) {
-    uint32_t mv, n3, x;
-    asm("v_add_u32 %1, %5, %7\n\t"
-        "v_bitop3_b32 %2, %3, %4, %6 bitop3:0x74\n\t"
-        "v_bitop3_b32 %2, %2, %6, %1 bitop3:0xf8\n\t"
-        "v_bitop3_b32 %0, %2, %8, %9 bitop3:0xea"
-        : "=v"(mv), "=&v"(n3), "=&v"(x)
-        : "v"(D0), "v"(D1), "v"(L3), "v"(D2), "v"(K7F), "v"(K80), "v"(P));
+    uint32_t mv, x;
+    asm("v_bitop3_b32 %1, %2, %3, %4 bitop3:0x74\n\t"
+        "v_bitop3_b32 %1, %1, %4, %5 bitop3:0xf8\n\t"
+        "v_bitop3_b32 %0, %1, %6, %7 bitop3:0xea"
+        : "=v"(mv), "=&v"(x)
+        : "v"(D0), "v"(D1), "v"(D2), "v"(N3), "v"(K80), "v"(P));
     return mv;
 }
 
@@ -196,28 +195,81 @@ __device__ __forceinline__ uint32_t moved_flags(uint32_t D0, uint32_t D1, uint32
 // constant as (f << 8) - f, two ops.
 __device__ __forceinline__ uint32_t expand01(uint32_t f, uint32_t k255) { return f * k255; }
 
-// The spawn slot from S (byte j: empties in lines 0..j; byte 3: their total):
+// The spawn slot of a step.  E_j = line j's empty cells after the move = its empty cells before
+// (the compaction masks M0..M2: 0xFF per empty byte; cell 3 from N3 = L3 + 0x7F7F7F7F, bit 7 set
+// for a tile) + its merges (f01 + f_cd, each frees a cell) -- at most 4 per byte, no carries --
+// and S = E * 0x01010101 (byte j: empties in lines 0..j; byte 3: their total).  Then
 //   n  = total mod 16 -- 0 for the empty board as for a full one (neither moves, so neither spawns)
 //   k  = floor((w << 3) * n / 2^32), the rank of the chosen empty cell
 //   j8 = 8 j*, j* = the number of lines j < 3 with S_j <= k: bit 7 of byte j of
 //        X = 0x80 + k - S_j (the bytes stay in [0x70, 0x8F], no borrows)
 //   q  = k - S_j* = (position along line j*) - 4, in [-4, -1]: its two low bits are the position
-// One asm block: in C, hipcc re-derives n and X from the multiply that made S (two more ops).
-__device__ __forceinline__ void spawn_slot(uint32_t S, uint32_t w, uint32_t& n, uint32_t& j8,
-                                           uint32_t& q) {
-    uint32_t t, k;
-    asm("v_bfe_u32 %0, %5, 24, 4\n\t"
-        "v_lshlrev_b32 %3, 3, %6\n\t"
-        "v_mul_hi_u32 %4, %3, %0\n\t"
-        "v_mad_u32_u24 %3, %4, %7, %8\n\t"
-        "v_sub_u32 %3, %3, %5\n\t"
-        "v_and_b32 %3, 0x808080, %3\n\t"
-        "v_bcnt_u32_b32 %3, %3, 0\n\t"
-        "v_lshlrev_b32 %1, 3, %3\n\t"
-        "v_bfe_u32 %3, %5, %1, 8\n\t"
-        "v_sub_u32 %2, %4, %3"
-        : "=&v"(n), "=&v"(j8), "=&v"(q), "=&v"(t), "=&v"(k)
-        : "v"(S), "v"(w), "v"(0x010101u), "v"(0x808080u));
+// One asm block: in C, hipcc re-derives n and X from the multiply that made S (more ops).
+__device__ __forceinline__ void spawn_slot(uint32_t M0, uint32_t M1, uint32_t M2, uint32_t N3,
+                                           uint32_t f01, uint32_t f_cd, uint32_t w, uint32_t& n,
+                                           uint32_t& j8, uint32_t& q) {
+    uint32_t e, t, u, k;
+    asm("v_and_b32 %3, 0x1010101, %7\n\t"
+        "v_and_b32 %4, 0x1010101, %8\n\t"
+        "v_and_b32 %5, 0x1010101, %9\n\t"
+        "v_add3_u32 %3, %3, %4, %5\n\t"
+        "v_lshrrev_b32 %4, 7, %10\n\t"
+        "v_bfi_b32 %4, %4, 0, %14\n\t"
+        "v_add3_u32 %4, %4, %11, %12\n\t"
+        "v_add_u32 %3, %3, %4\n\t"
+        "v_mul_lo_u32 %3, %3, %14\n\t"
+        "v_bfe_u32 %0, %3, 24, 4\n\t"
+        "v_lshlrev_b32 %4, 3, %13\n\t"
+        "v_mul_hi_u32 %6, %4, %0\n\t"
+        "v_mad_u32_u24 %4, %6, %15, %16\n\t"
+        "v_sub_u32 %4, %4, %3\n\t"
+        "v_and_b32 %4, 0x808080, %4\n\t"
+        "v_bcnt_u32_b32 %4, %4, 0\n\t"
+        "v_lshlrev_b32 %1, 3, %4\n\t"
+        "v_bfe_u32 %4, %3, %1, 8\n\t"
+        "v_sub_u32 %2, %6, %4"
+        : "=&v"(n), "=&v"(j8), "=&v"(q), "=&v"(e), "=&v"(t), "=&v"(u), "=&v"(k)
+        : "v"(M0), "v"(M1), "v"(M2), "v"(N3), "v"(f01), "v"(f_cd), "v"(w), "v"(0x01010101u),
+          "v"(0x010101u), "v"(0x808080u));
+}
+
+// The merges of the compacted line words C0..C3 from the pair flags (0x80: ab = cells 0, 1 equal,
+// bc_raw / cd_raw = cells 1, 2 / 2, 3 equal; see pair_flags):
+//   bc = bc_raw & ~ab              (bitop3 0x30: S0 & ~S1)
+//   cd = cd_raw & (ab | ~bc_raw)   (bitop3 0xD0: S0 & (S1 | ~S2))
+//   f_* = flag >> 7 (0x01 per merging line), AB / BC / CD = f_* * 255 (byte masks, expand01)
+//   b1 = C1 + f_bc, c1 = C2 + f_cd, o0 = C0 + f_ab
+//   o1 = AB ? c1 : b1,  o2 = AB ? C3 & ~CD : (BC ? C3 : c1),  o3 = C3 & ~(AB | BC | CD)
+//   e01 = AB ? o0 : b1 (the merged exponent of an a+b or b+c merge), f01 = f_ab | f_bc
+// (bitop3 table index S0*4 + S1*2 + S2; v_bfi_b32 d = S0 ? S1 : S2 per bit.)  One asm block, so
+// the selects stay v_bfi (hipcc splits them into and/or pairs once the masks have other users).
+__device__ __forceinline__ void merge_lines(uint32_t C0, uint32_t C1, uint32_t C2, uint32_t C3,
+                                            uint32_t ab, uint32_t bc_raw, uint32_t cd_raw,
+                                            uint32_t k255, uint32_t& o0, uint32_t& o1,
+                                            uint32_t& o2, uint32_t& o3, uint32_t& e01,
+                                            uint32_t& c1, uint32_t& f01, uint32_t& f_cd) {
+    uint32_t fab, fbc, AB, BC, CD, b1;
+    asm("v_bitop3_b32 %9, %17, %16, %16 bitop3:0x30\n\t"   // bc
+        "v_bitop3_b32 %7, %18, %16, %17 bitop3:0xd0\n\t"   // cd
+        "v_lshrrev_b32 %8, 7, %16\n\t"                     // f_ab
+        "v_lshrrev_b32 %9, 7, %9\n\t"                      // f_bc
+        "v_lshrrev_b32 %7, 7, %7\n\t"                      // f_cd
+        "v_mul_lo_u32 %10, %8, %19\n\t"                    // AB
+        "v_mul_lo_u32 %11, %9, %19\n\t"                    // BC
+        "v_mul_lo_u32 %12, %7, %19\n\t"                    // CD
+        "v_add_u32 %13, %21, %9\n\t"                       // b1 = C1 + f_bc
+        "v_add_u32 %5, %14, %7\n\t"                        // c1 = C2 + f_cd
+        "v_add_u32 %0, %8, %15\n\t"                        // o0 = C0 + f_ab
+        "v_or_b32 %6, %8, %9\n\t"                          // f01
+        "v_bfi_b32 %1, %10, %5, %13\n\t"                   // o1
+        "v_bfi_b32 %2, %11, %20, %5\n\t"                   // BC ? C3 : c1
+        "v_bitop3_b32 %3, %20, %12, %12 bitop3:0x30\n\t"   // C3 & ~CD
+        "v_bfi_b32 %4, %10, %0, %13\n\t"                   // e01
+        "v_bfi_b32 %2, %10, %3, %2\n\t"                    // o2
+        "v_bitop3_b32 %3, %3, %10, %11 bitop3:0x10"          // o3 = (C3 & ~CD) & ~AB & ~BC
+        : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3), "=&v"(e01), "=&v"(c1), "=&v"(f01),
+          "=&v"(f_cd), "=&v"(fab), "=&v"(fbc), "=&v"(AB), "=&v"(BC), "=&v"(CD), "=&v"(b1)
+        : "v"(C2), "v"(C0), "v"(ab), "v"(bc_raw), "v"(cd_raw), "v"(k255), "v"(C3), "v"(C1));
 }
 
 // bits [31:0] of {hi, lo} >> s
@@ -326,51 +378,41 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     // bit 7 of byte j of D_k: cell k of line j is empty
     const uint32_t D0 = K80 - L0, D1 = K80 - L1, D2 = K80 - L2;
     // 1) stable compaction toward L0, back to front
-    uint32_t M = zmask(D2);
-    uint32_t C2 = bsel(M, L3, L2), C3 = L3 & ~M;
-    M = zmask(D1);
-    uint32_t C1 = bsel(M, C2, L1);
-    C2 = bsel(M, C3, C2);
-    C3 &= ~M;
-    M = zmask(D0);
-    uint32_t C0 = bsel(M, C1, L0);
-    C1 = bsel(M, C2, C1);
-    C2 = bsel(M, C3, C2);
-    C3 &= ~M;
+    const uint32_t M2 = zmask(D2);
+    uint32_t C2 = bsel(M2, L3, L2), C3 = L3 & ~M2;
+    const uint32_t M1 = zmask(D1);
+    uint32_t C1 = bsel(M1, C2, L1);
+    C2 = bsel(M1, C3, C2);
+    C3 &= ~M1;
+    const uint32_t M0 = zmask(D0);
+    uint32_t C0 = bsel(M0, C1, L0);
+    C1 = bsel(M0, C2, C1);
+    C2 = bsel(M0, C3, C2);
+    C3 &= ~M0;
     G2048_MARK(merge, "+v"(C0), "+v"(C1), "+v"(C2), "+v"(C3));
     // 2) merges, front first (the later cell is non-empty => so is the earlier one)
     //    (v_xad: bit 7 of (x ^ y) + 0x7F set iff the bytes differ; of y + 0x7F iff y != 0)
     uint32_t ab, bc_raw, cd_raw;
     pair_flags(C0, C1, C2, C3, ab, bc_raw, cd_raw);
-    const uint32_t bc = bc_raw & ~ab;
-    const uint32_t cd = cd_raw & (ab | ~bc_raw);
-    const uint32_t f_ab = ab >> 7, f_bc = bc >> 7, f_cd = cd >> 7;  // 0x01 per merging line
-    const uint32_t AB = expand01(f_ab, k255), BC = expand01(f_bc, k255), CD = expand01(f_cd, k255);
-    const uint32_t c1 = C2 + f_cd;
-    const uint32_t b1 = C1 + f_bc;
-    uint32_t o0 = C0 + f_ab;
-    uint32_t o1 = bsel(AB, c1, b1);
-    uint32_t o2 = bsel(AB, C3 & ~CD, bsel(BC, C3, c1));
-    uint32_t o3 = C3 & ~(AB | BC | CD);
+    //    bc = bc_raw & ~ab (a+b taken first), cd = cd_raw & (ab | ~bc_raw) (c not used by b+c);
+    //    then the merged line words o0..o3, and for the score (3): e01 = the exponents of the
+    //    a+b or b+c merges (a line merges one or neither), c1 = of the c+d merges, and their 0x01
+    //    flags f01, f_cd
+    uint32_t o0, o1, o2, o3, e01, c1, f01, f_cd;
+    merge_lines(C0, C1, C2, C3, ab, bc_raw, cd_raw, k255, o0, o1, o2, o3, e01, c1, f01, f_cd);
     G2048_MARK(score, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
-    // 3) score = sum of 2^e over the merged tiles: a line merges a+b or b+c (never both), and
-    //    c+d, so two words of candidates; shifting the 0x01 merge flag (not 1) by each byte makes
-    //    a line without a merge contribute 0
-    //    (a line's exponent bytes need no mask: where its flag byte is 0 the shift yields 0)
-    const uint32_t e01 = bsel(AB, o0, b1), f01 = f_ab | f_bc;
+    // 3) score = sum of 2^e over the merged tiles: two words of candidates; shifting the 0x01
+    //    merge flag (not 1) by each byte makes a line without a merge contribute 0 (so the
+    //    exponent bytes need no mask)
     uint32_t gain = merge_gain(e01, f01, c1, f_cd);
     G2048_MARK(moved_done, "+v"(gain));
     // 4) moved: a hole before a tile along a line, or a merge
-    const uint32_t mv = moved_flags(D0, D1, D2, L3, ab | bc_raw | cd_raw);
+    const uint32_t N3 = L3 + K7F;  // bit 7: cell 3 holds a tile
+    const uint32_t mv = moved_flags(D0, D1, D2, N3, ab | bc_raw | cd_raw);
     G2048_MARK(spawn, "+v"(mv));
-    // 5) spawn in line space (see above).  E_j * 0x20 = sum of the 0x20 empty-flags of the four
-    //    line words (exponents < 32: no borrow; at most 4 * 0x20 per byte: no carry)
-    constexpr uint32_t K20 = 0x20202020u;
-    const uint32_t E20 = ((K20 - o0) & K20) + ((K20 - o1) & K20) + ((K20 - o2) & K20) +
-                         ((K20 - o3) & K20);
-    const uint32_t S = (E20 >> 5) * 0x01010101u;  // byte j: empties in lines 0..j; byte 3: n
+    // 5) spawn in line space (see above)
     uint32_t n, j8, q;
-    spawn_slot(S, w, n, j8, q);
+    spawn_slot(M0, M1, M2, N3, f01, f_cd, w, n, j8, q);
     // the tile min(e, mv) (mv is 0 -- no move, no spawn -- or >= 0x80) at bit 8 j* + 32 (q & 1)
     // of the half {o0, o1} (q & 2 clear) or {o2, o3}: v_lshlrev_b64 reads 6 bits of the shift,
     // and the half's mask is bit 1 of q sign-extended (without a move the tile is 0)
