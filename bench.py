@@ -45,7 +45,7 @@ ROLLOUT_BYTES = 38
 #   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
 STEP_BYTES = 37
 STEP_BYTES_BOOKKEEPING = 54
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r02")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
 
 
@@ -387,7 +387,7 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": rec["hbm_bytes_per_launch"] if rec else None,
                          "traffic_source": os.path.relpath(PMC_FILE, ROOT) if rec else None,
-                         "kernel": "k_rollout (g2048_env_rollout, ring + buffer stores)",
+                         "kernel": "k_rollout_lean (g2048_env_rollout: ring in one buffer window, auto-reset, no episode log)",
                          "bytes_per_step": ROLLOUT_BYTES,
                          "bytes_per_launch": ROLLOUT_BYTES * n * k,
                          "launch_us": launch_s * 1e6,

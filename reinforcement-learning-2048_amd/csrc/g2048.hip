@@ -484,6 +484,20 @@ __global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const 
 // step spends no VALU on addresses.  Used when every section of the ring is below 4 GiB.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// A board's 16-byte buffer store whose data registers stay untouched for two wait states after
+// it.  gfx950 reads a store's data VGPRs after issue when the store queue backs up, and a store of
+// more than 8 bytes needs two wait states before a VALU rewrites them; hipcc does not always
+// leave them (it scheduled the rollout's next v_perm into the board registers right behind the
+// store: at 1M+ boards about one board in 1 600 of some ring rows was stored with the first word
+// already overwritten).  The nop reads the four registers, so they stay live -- nothing is
+// written into them -- until it has issued, two wait states after the store (both volatile:
+// their order is kept).  tools/store_hazard_audit.py checks the compiled kernels.
+__device__ __forceinline__ void store_board(const Board& b, __amdgpu_buffer_rsrc_t rw,
+                                            uint32_t voff, uint32_t soff) {
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, voff, soff, 0);
+    asm volatile("s_nop 1" ::"v"(b.r0), "v"(b.r1), "v"(b.r2), "v"(b.r3));
+}
+
 // tools/prof_roll.hip: per-pair s_memtime ticks of a few waves (no-op in the library)
 #ifndef G2048_ROLL_TICK
 #define G2048_ROLL_TICK(np)
@@ -554,10 +568,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
         if constexpr (kSum) rsum += r;
         if constexpr (kRing) {
             if constexpr (kBuf) {
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{so.r0, so.r1, so.r2, so.r3}, rw,
-                                                       v_s, soff * 16u, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, v_s2,
-                                                       soff * 16u, 0);
+                store_board(so, rw, v_s, soff * 16u);
+                store_board(b, rw, v_s2, soff * 16u);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(wa >> 30), rw, v_a, soff, 0);
                 __builtin_amdgcn_raw_buffer_store_b32(r, rw, v_r, soff * 4u, 0);
                 __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, v_d, soff, 0);
@@ -637,7 +649,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 //   steps take their row offsets from loop-invariant VGPRs (section offset + j * size * n) and
 //   the quad's base from three SGPRs updated once per quad -- 1.25 SALU per step instead of 5
 //   (at one wave per SIMD an SALU op costs an issue turn like a VALU op).
-template <bool kSum, bool kP410, bool kQR>
+//   kStores: ring sections written (bits s, s2, a, r, d) -- all in the library; tools/rollexp.hip
+//   times subsets to price the stores.
+template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_lean(StepArgs A) {
     __shared__ uint4 s_dir[16];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -687,16 +701,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     auto one = [&](uint32_t w, uint32_t v, uint32_t v2, const uint4& F, const uint4& I,
                    const Off& o) {
         G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, o.s, o.o16, 0);
+        if constexpr (kStores & 1)
+            store_board(b, rw, o.s, o.o16);
         bool done;
         const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done, k255);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, o.s2, o.o16, 0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, o.a, o.o1, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(r, rw, o.r, o.o4, 0);
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, o.d, o.o1, 0);
+        if constexpr ((kStores & 2) != 0)
+            store_board(b, rw, o.s2, o.o16);
+        if constexpr ((kStores & 4) != 0)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, o.a, o.o1, 0);
+        if constexpr ((kStores & 8) != 0) __builtin_amdgcn_raw_buffer_store_b32(r, rw, o.r, o.o4, 0);
+        if constexpr ((kStores & 16) != 0)
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, o.d, o.o1, 0);
         // a wave-uniform branch whose body is selects: every value keeps its registers (a
         // lane-masked `if (done)` made hipcc copy the board and counters through phi moves, and
         // a v_mov costs a full issue turn)

@@ -408,7 +408,7 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     G2048_MARK(moved_done, "+v"(gain));
     // 4) moved: a hole before a tile along a line, or a merge
     const uint32_t N3 = L3 + K7F;  // bit 7: cell 3 holds a tile
-    const uint32_t mv = moved_flags(D0, D1, D2, N3, ab | bc_raw | cd_raw);
+    uint32_t mv = moved_flags(D0, D1, D2, N3, ab | bc_raw | cd_raw);
     G2048_MARK(spawn, "+v"(mv));
     // 5) spawn in line space (see above)
     uint32_t n, j8, q;

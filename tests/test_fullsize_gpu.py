@@ -61,6 +61,32 @@ def test_bench_rollout_full_size_vs_oracle(g2048):
         assert ref.ep[:, 0].sum() > 0  # episodes ended and auto-reset inside the launch
 
 
+def test_rollout_large_n_vs_oracle(g2048):
+    """1 M boards, ring of N*16 rows (the headline kernel's quad-row path), one launch of 3 steps
+    and four of 16 -- every clock phase -- against the oracle on four 1 000-board slices.  At this
+    size the store queue backs up: the first version of k_rollout_lean stored some boards with the
+    first word already rewritten by the next instruction (store_board in g2048.hip)."""
+    n_all, k, seed = 1 << 20, 16, 7
+    env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
+    rb = g2048.ReplayBuffer(n_all * k, device=DEV)
+    env.rollout(3, replay=rb)
+    for _ in range(4):
+        env.rollout(k, replay=rb)
+    torch.cuda.synchronize()
+    board = _np(env.board)
+    ring = {name: _np(getattr(rb, name)) for name in ["s", "s2", "a", "r", "d"]}
+    for i0 in (0, 68000, 500000, n_all - 1000):
+        n = 1000
+        ref = O.OracleEnv(n, seed=seed, board_offset=i0)
+        ref_rb = O.OracleReplay(n * k)
+        for _ in range(3 + 4 * k):
+            ref.step(O.MODE_RANDOM, replay=ref_rb)
+        assert np.array_equal(board[i0:i0 + n], ref.board), i0
+        rows = (np.arange(k)[:, None] * n_all + np.arange(i0, i0 + n)[None, :]).reshape(-1)
+        for name in ["s", "s2", "a", "r", "d"]:
+            assert np.array_equal(ring[name][rows], getattr(ref_rb, name)), (i0, name)
+
+
 @pytest.mark.parametrize("qdtype", [np.float32, np.float64])
 def test_egreedy_step_full_size_vs_oracle(g2048, qdtype):
     """One fused epsilon-greedy step (g2048_env_step_egreedy, src/dqn_lib.py:16-30,91-107) at

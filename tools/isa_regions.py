@@ -2,15 +2,16 @@
     hipcc --offload-arch=gfx950 -O3 -std=c++17 --cuda-device-only -S -DG2048_ISA_MARKS \\
           tools/rollexp.hip -o /tmp/roll_marks.s
     python tools/isa_regions.py /tmp/roll_marks.s
-Counts every instruction between consecutive ';; region X' markers inside the pair loop (both
-steps of a pair are summed, so the per-step figures are half), split into VALU / SALU / VMEM / LDS
-/ other.  The markers fix the instruction order, so the counts describe the marker build; the
+Counts every instruction between consecutive ';; region X' markers inside the main loop (two
+4-step quads per iteration: the figures are summed over 8 steps, and over both quads' Philox
+blocks), split into VALU / SALU / VMEM / LDS / other.  The auto-reset block is counted as if taken
+every step; the wave takes it on the steps where one of its 64 boards ends an episode.  The markers fix the instruction order, so the counts describe the marker build; the
 timed library is built without them."""
 import re
 import sys
 from collections import Counter, defaultdict
 
-KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0ELb1EEEvNS_8StepArgsE"  # <kSum=0, kP410=0, kQR=1>
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0ELb1ELi31EEEvNS_8StepArgsE"  # <kSum=0, kP410=0, kQR=1, all stores>
 
 
 def kind(op):
@@ -60,7 +61,7 @@ def main(path, dump=None):
     for r, c in per.items():
         tot.update(c)
         print(f"{r:14s} {sum(c.values()):5d}  " + "  ".join(f"{c[k]:8d}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
-    print(f"{'pair total':14s} {sum(tot.values()):5d}  " + "  ".join(f"{tot[k]:8d}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
+    print(f"{'loop total':14s} {sum(tot.values()):5d}  " + "  ".join(f"{tot[k]:8d}" for k in ("VALU", "SALU", "VMEM", "LDS", "wait/nop", "branch")))
 
 
 if __name__ == "__main__":

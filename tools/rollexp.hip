@@ -7,6 +7,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 namespace {
@@ -25,6 +26,50 @@ void launch_lean(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     hipLaunchKernelGGL((k_rollout_lean<false, false, true>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
 }
 
+template <int kStores>
+void launch_part(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_rollout_lean<false, false, true, kStores>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+}
+
+// The ring stores alone (no board arithmetic): the rollout's store pattern with a cheap per-step
+// value, to price the store stream at large N.  kAux: the buffer stores' cache-policy bits
+// (2 = nt).
+template <int kStores, int kAux>
+__global__ __launch_bounds__(kBlock) void k_store_only(StepArgs A) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= A.n) return;
+    const uint32_t n32 = (uint32_t)A.n, cap32 = (uint32_t)A.rb.capacity, lane = (uint32_t)i;
+    const uint64_t t0 = load_clock(A.clock, i);
+    uint32_t soff = (uint32_t)ring_row(t0, A.rb.rows) * n32;
+    __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(A.rb.win, 0, (int)A.rb.win_bytes, 0x00020000);
+    const uint32_t v_s = A.rb.o_s + 16u * lane, v_s2 = A.rb.o_s2 + 16u * lane;
+    const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
+    uint32_t x = lane * 2654435761u;
+    for (int s = 0; s < A.k_steps; ++s) {
+        x = x * 1664525u + 1013904223u;
+        if constexpr (kStores & 1)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{x, x + 1u, x + 2u, x + 3u}, rw, v_s, soff * 16u, kAux);
+        if constexpr ((kStores & 2) != 0)
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{x ^ 1u, x ^ 2u, x ^ 3u, x}, rw, v_s2, soff * 16u, kAux);
+        if constexpr ((kStores & 4) != 0) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)x, rw, v_a, soff, kAux);
+        if constexpr ((kStores & 8) != 0) __builtin_amdgcn_raw_buffer_store_b32(x, rw, v_r, soff * 4u, kAux);
+        if constexpr ((kStores & 16) != 0) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(x >> 8), rw, v_d, soff, kAux);
+        soff = soff + n32 == cap32 ? 0u : soff + n32;
+    }
+}
+
+template <int kStores, int kAux>
+void launch_store(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_store_only<kStores, kAux>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+}
+
 struct Variant {
     const char* name;
     void (*fn)(g2048_env*, g2048_replay*, int, hipStream_t);
@@ -33,7 +78,15 @@ struct Variant {
 const Variant kVariants[] = {
     {"k_rollout (general path)", launch_old},
     {"k_rollout_lean", launch_lean},
+    // timing only (parity MISMATCH expected: sections left unwritten)
+    {"lean, no byte stores (a, d)", launch_part<0x0B>},
+    {"lean, s + s2 only", launch_part<0x03>},
+    {"lean, no ring stores", launch_part<0x00>},
+    {"stores only (all five)", launch_store<0x1F, 0>},
+    {"stores only (s + s2)", launch_store<0x03, 0>},
+    {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
+constexpr int kParityVariants = 2;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
@@ -79,7 +132,7 @@ int main(int argc, char** argv) {
     auto r0 = fetch(rbs[0]->r, C);
     auto d0 = fetch(rbs[0]->d, C);
     int bad = 0;
-    for (int v = 1; v < nv; ++v) {
+    for (int v = 1; v < kParityVariants; ++v) {
         const bool ok = fetch(envs[v]->board, n * 16) == b0 && fetch(envs[v]->meta, n * 2) == m0 &&
                         fetch(envs[v]->ep, n * 4) == e0 &&
                         fetch(envs[v]->clock, (n + 63) / 64) == c0 &&
@@ -87,6 +140,61 @@ int main(int argc, char** argv) {
                         fetch(rbs[v]->a, C) == a0 && fetch(rbs[v]->r, C) == r0 &&
                         fetch(rbs[v]->d, C) == d0;
         printf("parity %-34s %s\n", kVariants[v].name, ok ? "bitwise equal" : "MISMATCH");
+        if (!ok) {  // which outputs, and the first differing index of each
+            auto first = [](const auto& x, const auto& y) -> long long {
+                for (size_t k = 0; k < x.size(); ++k)
+                    if (x[k] != y[k]) return (long long)k;
+                return -1;
+            };
+            printf("  board %lld meta %lld ep %lld clock %lld s %lld s2 %lld a %lld r %lld d %lld\n",
+                   first(fetch(envs[v]->board, n * 16), b0), first(fetch(envs[v]->meta, n * 2), m0),
+                   first(fetch(envs[v]->ep, n * 4), e0), first(fetch(envs[v]->clock, (n + 63) / 64), c0),
+                   first(fetch(rbs[v]->s, C * 16), s0), first(fetch(rbs[v]->s2, C * 16), t0),
+                   first(fetch(rbs[v]->a, C), a0), first(fetch(rbs[v]->r, C), r0),
+                   first(fetch(rbs[v]->d, C), d0));
+            const auto sv = fetch(rbs[v]->s, C * 16);
+            long long k = first(sv, s0), cnt = 0;
+            for (size_t q = 0; q < sv.size(); q += 16)
+                cnt += memcmp(&sv[q], &s0[q], 16) != 0;
+            printf("  %lld ring rows of s differ\n", cnt);
+            std::vector<long long> rowhist(C / n, 0);
+            for (size_t q = 0; q < sv.size(); q += 16)
+                if (memcmp(&sv[q], &s0[q], 16) != 0) rowhist[(q / 16) / n]++;
+            printf("  differing s per row:");
+            for (size_t q = 0; q < rowhist.size(); ++q) printf(" %lld", rowhist[q]);
+            printf("\n");
+            const auto tv = fetch(rbs[v]->s2, C * 16);
+            const auto dv = fetch(rbs[v]->d, C);
+            int shown = 0;
+            for (size_t q = 0; q < sv.size() && shown < 6; q += 16) {
+                if (memcmp(&sv[q], &s0[q], 16) == 0) continue;
+                ++shown;
+                const long long slot = q / 16, row = slot / n, bi = slot % n;
+                const long long prev = ((row + (long long)(C / n) - 1) % (C / n)) * n + bi;
+                printf("  row %lld board %lld (wave lane %lld)\n   s ref ", row, bi, bi & 63);
+                for (int c = 0; c < 16; ++c) printf("%02x", s0[slot * 16 + c]);
+                printf("\n   s var ");
+                for (int c = 0; c < 16; ++c) printf("%02x", sv[slot * 16 + c]);
+                printf("\n   s2prv ");
+                for (int c = 0; c < 16; ++c) printf("%02x", tv[prev * 16 + c]);
+                printf("  d(prev) ref %d var %d; wave's d(prev) sum %d\n", (int)d0[prev], (int)dv[prev],
+                       [&] { int z = 0; for (int c = 0; c < 64; ++c) z += d0[prev - (bi & 63) + c]; return z; }());
+            }
+            if (false) {
+                const long long slot = k / 16, row = slot / n, bi = slot % n;
+                const long long prev = ((row + (long long)(C / n) - 1) % (C / n)) * n + bi;
+                auto hex = [](const uint8_t* p) {
+                    for (int q = 0; q < 16; ++q) printf("%x", p[q]);
+                };
+                printf("  row %lld board %lld\n  s  (variant 0) ", row, bi);
+                hex(&s0[slot * 16]);
+                printf("\n  s  (variant)   ");
+                hex(&sv[slot * 16]);
+                printf("\n  s2 of the previous row ");
+                hex(&t0[prev * 16]);
+                printf("  d %d\n", (int)d0[prev]);
+            }
+        }
         bad += !ok;
     }
     // timing: graphs of 20 launches, each replayed once untimed, then 10 timed replays
