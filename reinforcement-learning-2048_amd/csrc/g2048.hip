@@ -651,8 +651,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 //   (at one wave per SIMD an SALU op costs an issue turn like a VALU op).
 //   kStores: ring sections written (bits s, s2, a, r, d) -- all in the library; tools/rollexp.hip
 //   times subsets to price the stores.
-template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_rollout_lean(StepArgs A) {
+//   kWaves: the occupancy hint (the library uses 4; tools/rollexp.hip times others at large N).
+template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F, int kWaves = 4>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void k_rollout_lean(StepArgs A) {
     __shared__ uint4 s_dir[16];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const bool live = i < A.n;

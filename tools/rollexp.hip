@@ -62,6 +62,14 @@ __global__ __launch_bounds__(kBlock) void k_store_only(StepArgs A) {
     }
 }
 
+template <bool kQR, int kWaves>
+void launch_occ(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_rollout_lean<false, false, kQR, 0x1F, kWaves>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+}
+
 template <int kStores, int kAux>
 void launch_store(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
@@ -78,6 +86,8 @@ struct Variant {
 const Variant kVariants[] = {
     {"k_rollout (general path)", launch_old},
     {"k_rollout_lean", launch_lean},
+    {"lean, 5 waves/SIMD", launch_occ<true, 5>},
+    {"lean no-QR, 4 waves/SIMD", launch_occ<false, 4>},
     // timing only (parity MISMATCH expected: sections left unwritten)
     {"lean, no byte stores (a, d)", launch_part<0x0B>},
     {"lean, s + s2 only", launch_part<0x03>},
@@ -86,7 +96,7 @@ const Variant kVariants[] = {
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
-constexpr int kParityVariants = 2;  // the others skip sections of the ring
+constexpr int kParityVariants = 4;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
