@@ -71,6 +71,9 @@ def parse():
     p.add_argument("--step-steps", type=int, default=2000,
                    help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
+    p.add_argument("--settle-ms", type=float, default=60.0,
+                   help="untimed back-to-back replays of the timed graph before each timed region "
+                        "(the clock ramps over the first ~10 ms of load; see DESIGN 6)")
     p.add_argument("--seed", type=int, default=0x2048)
     p.add_argument("--train", default="dense64,conv,dense,dense@5000",
                    help="learner legs to time: comma list of dense64 / conv / dense, each "
@@ -163,6 +166,23 @@ def timed(world, dev, fn, reps: int):
     return max_over_ranks(wall, world, dev), e0.elapsed_time(e1) / 1e3
 
 
+def settle(replay, ms: float, max_calls: int = 4000) -> float:
+    """Keep the GPU busy with `replay` (untimed) for at least `ms` of wall time, so the timed
+    region starts at the clock a sustained run holds: gfx950 ramps its clock over the first
+    ~10 ms of load (64k-board rollout: 30.3 us per launch right after a short warm-up, 27.4 us
+    after ~10 ms).  Returns the wall milliseconds spent."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    calls = 0
+    while (time.perf_counter() - t0) * 1e3 < ms and calls < max_calls:
+        replay()
+        calls += 1
+        if calls % 8 == 0:
+            torch.cuda.synchronize()  # pace the host: the queue stays short
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3
+
+
 def capture(fn, n_steps: int):
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
@@ -201,7 +221,7 @@ def bench_rollout(args, world, rank, dev, k_override=None):
         g.replay()
     for _ in range(max(args.warmup, 1)):
         launch()
-    torch.cuda.synchronize()
+    settle_ms = settle(graphs[0][0].replay, args.settle_ms)
 
     def run_all():
         for g, reps in graphs:
@@ -211,7 +231,7 @@ def bench_rollout(args, world, rank, dev, k_override=None):
     wall, ev = timed(world, dev, run_all, 1)
     env.check_errors()
     assert int(rb.count) == n * k
-    return dict(wall=wall, ev_s=ev, n=n, k=k)
+    return dict(wall=wall, ev_s=ev, n=n, k=k, settle_ms=settle_ms)
 
 
 # ------------------------------------------------------------------ one launch per step
@@ -237,7 +257,7 @@ def bench_step(args, world, rank, dev):
         g.replay()
     for _ in range(3):
         graphs[0][0].replay()
-    torch.cuda.synchronize()
+    settle(graphs[0][0].replay, args.settle_ms)
 
     def run_all():
         for g, reps in graphs:
@@ -391,6 +411,7 @@ def main():
                          "bytes_per_step": ROLLOUT_BYTES,
                          "bytes_per_launch": ROLLOUT_BYTES * n * k,
                          "launch_us": launch_s * 1e6,
+                         "settle_ms": ro["settle_ms"],
                          "issue": rec.get("issue") if rec else None},
             "cpu_baseline": cpu,
         }
