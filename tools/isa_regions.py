@@ -11,7 +11,7 @@ import re
 import sys
 from collections import Counter, defaultdict
 
-KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0ELb1ELi31EEEvNS_8StepArgsE"  # <kSum=0, kP410=0, kQR=1, all stores>
+KERNEL = "_ZN12_GLOBAL__N_114k_rollout_leanILb0ELb0ELb1ELi31ELi4EEEvNS_8StepArgsE"  # <kSum=0, kP410=0, kQR=1, all stores>
 
 
 def kind(op):
