@@ -62,6 +62,140 @@ __global__ __launch_bounds__(kBlock) void k_store_only(StepArgs A) {
     }
 }
 
+// A warp-specialised large-N rollout, measured and not kept: workgroups of 512
+// threads.  Past ~256k boards the ring streams to HBM and the launch is
+// store-bound, and in k_rollout_lean every wave both computes and stores: with the store queue
+// full, all waves of a SIMD end up waiting at their stores together, so compute and stores
+// barely overlap (4M boards x 16: 261 us of compute + 480 us of stores -> 700-745 us).  Here
+// waves 0-3 step the workgroup's 256 boards and write each transition into an LDS double
+// buffer; waves 4-7 copy the previous step's buffer to the ring.  One barrier per step, so a
+// step would cost max(compute, store issue) instead of their sum -- but it measured the sum all
+// the same (4M x 16: 738 us).  Bitwise the same transitions as k_rollout_lean.
+struct WsBuf {
+    uint4 s[kBlock];
+    uint4 s2[kBlock];
+    uint32_t r[kBlock];
+    uint8_t a[kBlock];
+    uint8_t d[kBlock];
+};
+
+template <bool kSum, bool kP410>
+__global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
+    __shared__ uint4 s_dir[8];
+    __shared__ WsBuf buf[2];
+    const bool storer = threadIdx.x >= kBlock;
+    const int j = storer ? (int)threadIdx.x - kBlock : (int)threadIdx.x;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + j;
+    const bool live = i < A.n;
+    uint64_t c0 = 0;
+    if (live) c0 = A.clock[i >> 6];
+    if (threadIdx.x < 8) s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
+    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    const int K = A.k_steps > 0 ? A.k_steps : 0;
+    __syncthreads();
+    if (storer) {
+        // the ring side: step s's transition of board i from buf[s & 1] to ring row (t0 + s) mod rows
+        const uint32_t cap32 = (uint32_t)A.rb.capacity, n32 = (uint32_t)A.n;
+        uint32_t soff = (uint32_t)ring_row(t0, A.rb.rows) * n32;
+        __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc(A.rb.win, 0, (int)A.rb.win_bytes, 0x00020000);
+        const uint32_t lane = (uint32_t)i;
+        const uint32_t v_s = A.rb.o_s + 16u * lane, v_s2 = A.rb.o_s2 + 16u * lane;
+        const uint32_t v_a = A.rb.o_a + lane, v_r = A.rb.o_r + 4u * lane, v_d = A.rb.o_d + lane;
+        for (int s = 0; s < K; ++s) {
+            __syncthreads();  // buf[s & 1] holds step s
+            const WsBuf& B = buf[s & 1];
+            if (live) {
+                const uint4 sv = B.s[j], s2v = B.s2[j];
+                const uint32_t rv = B.r[j];
+                const uint8_t av = B.a[j], dv = B.d[j];
+                store_board(Board{sv.x, sv.y, sv.z, sv.w}, rw, v_s, soff * 16u);
+                store_board(Board{s2v.x, s2v.y, s2v.z, s2v.w}, rw, v_s2, soff * 16u);
+                __builtin_amdgcn_raw_buffer_store_b8(av, rw, v_a, soff, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(rv, rw, v_r, soff * 4u, 0);
+                __builtin_amdgcn_raw_buffer_store_b8(dv, rw, v_d, soff, 0);
+            }
+            soff = soff + n32 == cap32 ? 0u : soff + n32;
+        }
+        return;
+    }
+    // the board side
+    Board b{0u, 0u, 0u, 0u};
+    uint2 m = make_uint2(0, 0);
+    uint4 ep = make_uint4(0, 0, 0, 0);
+    if (live) {
+        b = load_board(A.board[i]);
+        m = A.meta[i];
+        ep = A.ep[i];
+    }
+    const uint64_t gid = A.board_offset + (uint64_t)i;
+    const uint32_t p4 = A.p4_thresh;
+    long long rsum = 0;
+    const uint32_t ep0 = ep.x;
+    Board last = b;
+    const uint32_t k255 = opaque_255();
+    uint4 blk = make_uint4(0, 0, 0, 0), vb = blk, vb2 = blk;
+    for (int s = 0; s < K; ++s) {
+        const uint64_t t = t0 + (uint64_t)s;
+        if (s == 0 || (t & 3u) == 0u) {
+            blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, t >> 2);
+            value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, t >> 2, vb, vb2);
+        }
+        const uint32_t k = (uint32_t)t & 3u;
+        const uint32_t w = word_of(blk, k), v = word_of(vb, k), v2 = word_of(vb2, k);
+        const uint32_t a2 = (w >> 30) * 2u;
+        WsBuf& B = buf[s & 1];
+        B.s[j] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+        bool done;
+        const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), s_dir[a2], s_dir[a2 + 1u], done, k255);
+        m.x += r;
+        m.y += 1u;
+        if constexpr (kSum) rsum += r;
+        B.s2[j] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+        B.a[j] = (uint8_t)(w >> 30);
+        B.r[j] = r;
+        B.d[j] = (uint8_t)done;
+        const uint64_t dl = __builtin_amdgcn_ballot_w64(done);
+        if (dl != 0u) {
+            const Board f = fresh_board_w<kP410>(w, v, v2, p4);
+            last.r0 = sel_lanes(dl, b.r0, last.r0);
+            last.r1 = sel_lanes(dl, b.r1, last.r1);
+            last.r2 = sel_lanes(dl, b.r2, last.r2);
+            last.r3 = sel_lanes(dl, b.r3, last.r3);
+            ep.x = sel_lanes(dl, ep.x + 1u, ep.x);
+            ep.y = sel_lanes(dl, m.x, ep.y);
+            ep.z = sel_lanes(dl, m.y, ep.z);
+            b.r0 = sel_lanes(dl, f.r0, b.r0);
+            b.r1 = sel_lanes(dl, f.r1, b.r1);
+            b.r2 = sel_lanes(dl, f.r2, b.r2);
+            b.r3 = sel_lanes(dl, f.r3, b.r3);
+            m.x = sel_lanes(dl, 0u, m.x);
+            m.y = sel_lanes(dl, 0u, m.y);
+        }
+        __syncthreads();  // step s is in buf[s & 1]; the ring side copies it during step s + 1
+    }
+    if (!live) return;
+    const uint64_t t1 = t0 + (uint64_t)K;
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (ep.x != ep0) {
+        ep.w = max_exp(last);
+        A.ep[i] = ep;
+        if (A.qsum) A.qsum[i] = 0.0;
+    }
+    if ((i & 63) == 0) A.clock[i >> 6] = t1;
+    if constexpr (kSum) A.reward_sum[i] += rsum;
+    if (i == 0) bump_count(A, t1);
+}
+
+void launch_ws(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_rollout_ws<false, false>), dim3(grid_for(e->n)), dim3(2 * kBlock), 0, st, A);
+}
+
 template <bool kQR, int kWaves>
 void launch_occ(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
@@ -86,6 +220,7 @@ struct Variant {
 const Variant kVariants[] = {
     {"k_rollout (general path)", launch_old},
     {"k_rollout_lean", launch_lean},
+    {"warp-specialised (k_rollout_ws)", launch_ws},
     {"lean, 5 waves/SIMD", launch_occ<true, 5>},
     {"lean no-QR, 4 waves/SIMD", launch_occ<false, 4>},
     // timing only (parity MISMATCH expected: sections left unwritten)
@@ -96,7 +231,7 @@ const Variant kVariants[] = {
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
-constexpr int kParityVariants = 4;  // the others skip sections of the ring
+constexpr int kParityVariants = 5;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
