@@ -1425,14 +1425,22 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
     } else if (A.rb.win_bytes && !A.log && !(A.flags & G2048_NO_AUTORESET)) {
         // the headline case
         const bool p410 = (A.flags & G2048_P4_10) != 0u, qr = A.rb.rows % 4 == 0;
+        // past 1M boards the launch is store-bound: five waves per SIMD (a few
+        // spilled registers) beat four there in every measurement (4M x 16: 604-681 us against
+        // 700-748), and lose below (1M x 64: +3 %; 64k: +70 %)
+        const bool big = A.n > (1 << 20);
 #define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q>), grid, block, 0, st, A)
+#define G2048_LEAN5(S, Q) hipLaunchKernelGGL((k_rollout_lean<S, false, Q, 0x1F, 5>), grid, block, 0, st, A)
         if (reward_sum) {
             if (p410) { if (qr) G2048_LEAN(true, true, true); else G2048_LEAN(true, true, false); }
+            else if (big) { if (qr) G2048_LEAN5(true, true); else G2048_LEAN5(true, false); }
             else { if (qr) G2048_LEAN(true, false, true); else G2048_LEAN(true, false, false); }
         } else {
             if (p410) { if (qr) G2048_LEAN(false, true, true); else G2048_LEAN(false, true, false); }
+            else if (big) { if (qr) G2048_LEAN5(false, true); else G2048_LEAN5(false, false); }
             else { if (qr) G2048_LEAN(false, false, true); else G2048_LEAN(false, false, false); }
         }
+#undef G2048_LEAN5
 #undef G2048_LEAN
     } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);

@@ -61,12 +61,14 @@ def test_bench_rollout_full_size_vs_oracle(g2048):
         assert ref.ep[:, 0].sum() > 0  # episodes ended and auto-reset inside the launch
 
 
-def test_rollout_large_n_vs_oracle(g2048):
+@pytest.mark.parametrize("n_all", [1 << 20, (1 << 20) + 4160])
+def test_rollout_large_n_vs_oracle(g2048, n_all):
     """1 M boards, ring of N*16 rows (the headline kernel's quad-row path), one launch of 3 steps
     and four of 16 -- every clock phase -- against the oracle on four 1 000-board slices.  At this
     size the store queue backs up: the first version of k_rollout_lean stored some boards with the
-    first word already rewritten by the next instruction (store_board in g2048.hip)."""
-    n_all, k, seed = 1 << 20, 16, 7
+    first word already rewritten by the next instruction (store_board in g2048.hip).  Past 1 M
+    boards (the second case, ragged) the five-waves-per-SIMD instance runs."""
+    k, seed = 16, 7
     env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
     rb = g2048.ReplayBuffer(n_all * k, device=DEV)
     env.rollout(3, replay=rb)
