@@ -196,6 +196,16 @@ __device__ __forceinline__ int pos_of(int p, int tap) {
 __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
+    // conv2's B fragments: the first two k-steps are requested before conv1, so their L2 round
+    // trip overlaps conv1 + V and its barrier instead of stalling conv2's first MFMAs
+    const gdouble* bp = opaque(pk.u) + (size_t)w * 9 * 16 * 64 + l;  // [w][xi][s][lane]
+    auto ld9 = [&](double(&b)[9], int s) {
+#pragma unroll
+        for (int x = 0; x < 9; ++x) b[x] = bp[(x * 16 + s) * 64];
+    };
+    double bb[3][9];
+    ld9(bb[0], 0);
+    ld9(bb[1], 1);
     __syncthreads();  // x and the small weights visible
     conv1_mfma<true>(M.x, M.d, W);
     __syncthreads();
@@ -203,16 +213,18 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
     // conv2 in the Winograd domain, F(2x2, 2x2): M_xi = V_xi U_xi ([16 b x 64 c] x [64 c x 64 o],
     // nine independent GEMMs, 144 MFMAs per wave instead of the direct form's 256); wave w ->
     // output channels 16w .. 16w+15.  Then Y = A^T M A (A^T = [[1,1,0],[0,1,1]]), lane-local.
+    // fc1's first two chunks of B fragments are requested after conv2's last MFMA, before its
+    // output transform and barrier.
+    const gdouble* bpf = opaque(pk.pf1) + (size_t)w * 64 * 64 + l;
+    auto ld8 = [&](double(&b)[8], int k) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = bpf[(8 * k + u) * 64];
+    };
+    double bf[3][8];
     {
         d4 acc[9];
 #pragma unroll
         for (int x = 0; x < 9; ++x) acc[x] = d4{0.0, 0.0, 0.0, 0.0};
-        const gdouble* bp = opaque(pk.u) + (size_t)w * 9 * 16 * 64 + l;  // [w][xi][s][lane]
-        // B fragments two k-steps ahead in three rotating buffers
-        auto ld9 = [&](double(&b)[9], int s) {
-#pragma unroll
-            for (int x = 0; x < 9; ++x) b[x] = bp[(x * 16 + s) * 64];
-        };
         auto la9 = [&](double(&a)[9], int s) {
             const double* vr = M.d + lr * DSB + 4 * s + lk;
 #pragma unroll
@@ -221,9 +233,7 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
         // fully unrolled (a rolled loop keeps the accumulators in VGPRs and copies them to
         // AGPRs and back every iteration); a scheduling barrier per step keeps each step's
         // prefetches (A one step, B two steps ahead) where they are written
-        double bb[3][9], aa[2][9];
-        ld9(bb[0], 0);
-        ld9(bb[1], 1);
+        double aa[2][9];
         la9(aa[0], 0);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -233,6 +243,9 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
             for (int x = 0; x < 9; ++x) acc[x] = mfma(aa[s & 1][x], bb[s % 3][x], acc[x]);
             __builtin_amdgcn_sched_barrier(0);
         }
+        ld8(bf[0], 0);
+        ld8(bf[1], 1);
+        __builtin_amdgcn_sched_barrier(0);
         const int o = 16 * w + lr;
         const double bo = W.b2[o];
 #pragma unroll
@@ -260,26 +273,20 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
         d4 acc[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) acc[c] = d4{0.0, 0.0, 0.0, 0.0};
-        const gdouble* bp = opaque(pk.pf1) + (size_t)w * 64 * 64 + l;
-        // B fragments two chunks of 8 k-steps ahead (rotating buffers, fully unrolled)
-        auto ld8 = [&](double(&b)[8], int k) {
-#pragma unroll
-            for (int u = 0; u < 8; ++u) b[u] = bp[(8 * k + u) * 64];
-        };
+        // B fragments two chunks of 8 k-steps ahead (rotating buffers, fully unrolled; the first
+        // two were requested before conv2's output transform)
         auto la8 = [&](double(&a)[8], int k) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) a[u] = M.h2[lr * HS + 4 * (8 * k + u) + lk];
         };
-        double bb[3][8], aa[2][8];
-        ld8(bb[0], 0);
-        ld8(bb[1], 1);
+        double aa[2][8];
         la8(aa[0], 0);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             if (k + 1 < 8) la8(aa[(k + 1) & 1], k + 1);
-            if (k + 2 < 8) ld8(bb[(k + 2) % 3], k + 2);
+            if (k + 2 < 8) ld8(bf[(k + 2) % 3], k + 2);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc[u & 3] = mfma(aa[k & 1][u], bb[k % 3][u], acc[u & 3]);
+            for (int u = 0; u < 8; ++u) acc[u & 3] = mfma(aa[k & 1][u], bf[k % 3][u], acc[u & 3]);
             __builtin_amdgcn_sched_barrier(0);
         }
         const int j = 16 * w + lr;
