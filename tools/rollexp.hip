@@ -257,6 +257,14 @@ int main(int argc, char** argv) {
             return 1;
         }
     }
+    {
+        StepArgs A;
+        make_args(envs[0], rbs[0], A);
+        if (!A.rb.win_bytes) {  // the buffer-store kernels need the ring in one < 4 GiB window
+            printf("ring of %lld rows exceeds the 4 GiB buffer window: not timed\n", (long long)(n * K));
+            return 1;
+        }
+    }
     // parity: 5 launches from the same start (an odd K first moves every clock to an odd step)
     for (int v = 0; v < nv; ++v) {
         kVariants[v].fn(envs[v], rbs[v], 3, st);
