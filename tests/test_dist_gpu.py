@@ -39,7 +39,8 @@ def _worker(rank, world, port, net, out_dir, dtype="fp32"):
     L = DQNLearner(rb, net=net, dtype=torch.float64 if dtype == "fp64" else torch.float32,
                    batch_size=1024, target_sync_every=2,
                    seed=100 + rank)  # different seeds: the broadcast must equalise the init
-    assert L.world == world and L.fused and L.f64 == (dtype == "fp64")
+    fused = net != "dense"  # dense: the torch-ROCm path
+    assert L.world == world and L.fused == fused and L.f64 == (fused and dtype == "fp64")
     init = torch.cat([p.detach().reshape(-1).clone() for p in L.model.parameters()])
     for _ in range(3):
         L.update()
@@ -61,10 +62,11 @@ def _worker(rank, world, port, net, out_dir, dtype="fp32"):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "fp64"])
-@pytest.mark.parametrize("net", ["conv", "dense64"])
+@pytest.mark.parametrize("net", ["conv", "dense64", "dense"])
 def test_two_ranks_stay_in_lockstep(tmp_path, net, dtype):
     """fp64: the fused float64 update writes the gradient, the flat bucket is all-reduced and
-    g2048_adam_step_sync_f64 applies Adam (+ target sync)."""
+    g2048_adam_step_sync_f64 applies Adam (+ target sync).  dense: the torch-ROCm path (autograd
+    gradients in the flat bucket, torch Adam)."""
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need an MI355X")
     mp.spawn(_worker, args=(2, _free_port(), net, str(tmp_path), dtype), nprocs=2, join=True)
@@ -134,7 +136,8 @@ def test_bench_two_ranks():
     env = dict(os.environ, G2048_BENCH_BACKEND="gloo")
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
                           "--steps", "20", "--warmup", "5", "--step-steps", "200",
-                          "--train", "dense64", "--train-dtypes", "fp32,fp64", "--train-updates", "20",
+                          "--train", "dense64,dense@512", "--train-dtypes", "fp32,fp64",
+                          "--train-updates", "20",
                           "--no-cpu-baseline"], capture_output=True, text=True, env=env,
                          timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -144,3 +147,6 @@ def test_bench_two_ranks():
     assert line["value"] > 0 and line["step_kernel"]["env_steps_per_s"] > 0
     assert line["learner"]["dense64.fp32"]["graphed_loop"] is True
     assert line["learner"]["dense64.fp64"]["path"] == "fused HIP kernels"
+    for leg in ("dense64.fp32", "dense64.fp64", "dense@512.fp32", "dense@512.fp64"):
+        assert line["learner"][leg]["ranks_lockstep"] is True, leg
+    assert line["learner"]["dense@512.fp64"]["batch"] == 512
