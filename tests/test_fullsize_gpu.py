@@ -72,11 +72,15 @@ def test_rollout_large_n_vs_oracle(g2048, n_all):
     env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
     rb = g2048.ReplayBuffer(n_all * k, device=DEV)
     env.rollout(3, replay=rb)
-    for _ in range(4):
+    for _ in range(3):
         env.rollout(k, replay=rb)
+    rs = torch.zeros(n_all, dtype=torch.int64, device=DEV)
+    env.rollout(k, replay=rb, reward_sum=rs)  # the reward-sum instance for the last launch
     torch.cuda.synchronize()
     board = _np(env.board)
     ring = {name: _np(getattr(rb, name)) for name in ["s", "s2", "a", "r", "d"]}
+    # the last launch wrote all k rows: its reward sums are the rows' rewards per board
+    assert np.array_equal(_np(rs), ring["r"].reshape(k, n_all).astype(np.int64).sum(0))
     for i0 in (0, 68000, 500000, n_all - 1000):
         n = 1000
         ref = O.OracleEnv(n, seed=seed, board_offset=i0)
