@@ -1429,7 +1429,10 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
         // spilled registers) beat four there in every measurement (4M x 16: 604-681 us against
         // 700-748), and lose below (1M x 64: +3 %; 64k: +70 %)
         const bool big = A.n > (1 << 20);
-#define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q>), grid, block, 0, st, A)
+        // (the p(4) = 0.1 instances carry two more Philox blocks per quad: under the four-wave
+        // register cap they spilled, so they take a three-wave cap -- at 64k boards the kernel
+        // runs one wave per SIMD anyway)
+#define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q, 0x1F, (P) ? 3 : 4>), grid, block, 0, st, A)
 #define G2048_LEAN5(S, Q) hipLaunchKernelGGL((k_rollout_lean<S, false, Q, 0x1F, 5>), grid, block, 0, st, A)
         if (reward_sum) {
             if (p410) { if (qr) G2048_LEAN(true, true, true); else G2048_LEAN(true, true, false); }
