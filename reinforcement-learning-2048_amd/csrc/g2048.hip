@@ -1001,6 +1001,163 @@ inline uint32_t p4_thresh(uint32_t flags) {
     return (flags & G2048_P4_10) ? 429496730u : 2147483648u;  // round(p * 2^32)
 }
 
+// The large-N instance of g2048_env_rollout: past ~1M boards the ring streams to HBM
+// and the launch is store-bound; a kernel whose waves each compute AND store overlaps the two
+// badly (with the store queue full, a SIMD's waves wait at their stores together: compute +
+// stores ~ their sum).  Decoupled warp specialisation: workgroups of 512 threads, compute wave p
+// (0-3) and store wave p + 4 own the same 64 boards and share a kD-step LDS ring of transitions.  No workgroup barrier
+// inside the loop: the pair hands slots over through two LDS counters (produced / consumed steps,
+// release / acquire at workgroup scope), so the compute wave runs up to kD steps ahead of its
+// store wave and a store wave waiting on a full store queue stalls only itself.  Every wait is
+// capped: a broken hand-over ends the loop and bumps the env's error counter (env.check_errors()
+// raises) instead of hanging the GPU.
+// kAux: the ring stores' cache-policy bits (2 = nt: the ring is not re-read by this launch).
+// kD = 8: 78 KB of LDS, two workgroups per CU (4M x 16: 445 us against 694 for the five-wave
+// k_rollout_lean; 4 or 12 steps: 622 / 652 us).  The same transitions, bit for bit.
+struct alignas(16) PairSlot {
+    uint4 s[64];
+    uint4 s2[64];
+    uint32_t r[64];
+    uint8_t a[64];
+    uint8_t d[64];
+};
+
+__device__ __forceinline__ bool wait_until(const uint32_t* c, uint32_t want) {
+    // wave-uniform: every lane reads the same LDS word
+    for (int spin = 0; spin < (1 << 20); ++spin) {
+        if (__hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= want) return true;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+template <bool kSum, bool kP410, int kD = 8, int kAux = 2>
+__global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
+    __shared__ uint4 s_dir[8];
+    __shared__ PairSlot ring[4][kD];
+    __shared__ uint32_t prod[4], cons[4];
+    const bool storer = threadIdx.x >= kBlock;
+    const int j = storer ? (int)threadIdx.x - kBlock : (int)threadIdx.x;
+    const int pair = j >> 6, lane = j & 63;
+    const int64_t i = (int64_t)blockIdx.x * kBlock + j;
+    const bool live = i < A.n;
+    uint64_t c0 = 0;
+    if (live) c0 = A.clock[i >> 6];
+    if (threadIdx.x < 8) s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
+    if (threadIdx.x < 4) {
+        prod[threadIdx.x] = 0u;
+        cons[threadIdx.x] = 0u;
+    }
+    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    const int K = A.k_steps > 0 ? A.k_steps : 0;
+    __syncthreads();
+    if (storer) {
+        const uint32_t cap32 = (uint32_t)A.rb.capacity, n32 = (uint32_t)A.n;
+        uint32_t soff = (uint32_t)ring_row(t0, A.rb.rows) * n32;
+        __amdgpu_buffer_rsrc_t rw =
+            __builtin_amdgcn_make_buffer_rsrc(A.rb.win, 0, (int)A.rb.win_bytes, 0x00020000);
+        const uint32_t bl = (uint32_t)i;
+        const uint32_t v_s = A.rb.o_s + 16u * bl, v_s2 = A.rb.o_s2 + 16u * bl;
+        const uint32_t v_a = A.rb.o_a + bl, v_r = A.rb.o_r + 4u * bl, v_d = A.rb.o_d + bl;
+        for (int s = 0; s < K; ++s) {
+            if (!wait_until(&prod[pair], (uint32_t)s + 1u)) {
+                if (lane == 0) atomicAdd(A.err, 1ull);  // never expected: surfaces as an env error
+                break;
+            }
+            const PairSlot& B = ring[pair][s % kD];
+            const uint4 sv = B.s[lane], s2v = B.s2[lane];
+            const uint32_t rv = B.r[lane];
+            const uint8_t av = B.a[lane], dv = B.d[lane];
+            // the slot's reads are complete (the release below orders them) before it is freed
+            if (lane == 0)
+                __hip_atomic_store(&cons[pair], (uint32_t)s + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (live) {
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{sv.x, sv.y, sv.z, sv.w}, rw, v_s, soff * 16u, kAux);
+                __builtin_amdgcn_raw_buffer_store_b128(u32x4{s2v.x, s2v.y, s2v.z, s2v.w}, rw, v_s2, soff * 16u, kAux);
+                asm volatile("s_nop 1" ::"v"(sv.x), "v"(sv.y), "v"(sv.z), "v"(sv.w), "v"(s2v.x), "v"(s2v.y), "v"(s2v.z), "v"(s2v.w));
+                __builtin_amdgcn_raw_buffer_store_b8(av, rw, v_a, soff, kAux);
+                __builtin_amdgcn_raw_buffer_store_b32(rv, rw, v_r, soff * 4u, kAux);
+                __builtin_amdgcn_raw_buffer_store_b8(dv, rw, v_d, soff, kAux);
+            }
+            soff = soff + n32 == cap32 ? 0u : soff + n32;
+        }
+        return;
+    }
+    Board b{0u, 0u, 0u, 0u};
+    uint2 m = make_uint2(0, 0);
+    uint4 ep = make_uint4(0, 0, 0, 0);
+    if (live) {
+        b = load_board(A.board[i]);
+        m = A.meta[i];
+        ep = A.ep[i];
+    }
+    const uint64_t gid = A.board_offset + (uint64_t)i;
+    const uint32_t p4 = A.p4_thresh;
+    long long rsum = 0;
+    const uint32_t ep0 = ep.x;
+    Board last = b;
+    const uint32_t k255 = opaque_255();
+    uint4 blk = make_uint4(0, 0, 0, 0), vb = blk, vb2 = blk;
+    for (int s = 0; s < K; ++s) {
+        const uint64_t t = t0 + (uint64_t)s;
+        if (s == 0 || (t & 3u) == 0u) {
+            blk = draw(A.seed_lo, A.seed_hi, gid, DOMAIN_RANDOM, t >> 2);
+            value_blocks<kP410>(A.seed_lo, A.seed_hi, gid, t >> 2, vb, vb2);
+        }
+        const uint32_t k = (uint32_t)t & 3u;
+        const uint32_t w = word_of(blk, k), v = word_of(vb, k), v2 = word_of(vb2, k);
+        const uint32_t a2 = (w >> 30) * 2u;
+        // slot s % kD is free once the store wave has taken step s - kD
+        if (s >= kD && !wait_until(&cons[pair], (uint32_t)(s - kD) + 1u)) {
+            if (lane == 0) atomicAdd(A.err, 1ull);
+            break;
+        }
+        PairSlot& B = ring[pair][s % kD];
+        B.s[lane] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+        bool done;
+        const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), s_dir[a2], s_dir[a2 + 1u], done, k255);
+        m.x += r;
+        m.y += 1u;
+        if constexpr (kSum) rsum += r;
+        B.s2[lane] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+        B.a[lane] = (uint8_t)(w >> 30);
+        B.r[lane] = r;
+        B.d[lane] = (uint8_t)done;
+        if (lane == 0)
+            __hip_atomic_store(&prod[pair], (uint32_t)s + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint64_t dl = __builtin_amdgcn_ballot_w64(done);
+        if (dl != 0u) {
+            const Board f = fresh_board_w<kP410>(w, v, v2, p4);
+            last.r0 = sel_lanes(dl, b.r0, last.r0);
+            last.r1 = sel_lanes(dl, b.r1, last.r1);
+            last.r2 = sel_lanes(dl, b.r2, last.r2);
+            last.r3 = sel_lanes(dl, b.r3, last.r3);
+            ep.x = sel_lanes(dl, ep.x + 1u, ep.x);
+            ep.y = sel_lanes(dl, m.x, ep.y);
+            ep.z = sel_lanes(dl, m.y, ep.z);
+            b.r0 = sel_lanes(dl, f.r0, b.r0);
+            b.r1 = sel_lanes(dl, f.r1, b.r1);
+            b.r2 = sel_lanes(dl, f.r2, b.r2);
+            b.r3 = sel_lanes(dl, f.r3, b.r3);
+            m.x = sel_lanes(dl, 0u, m.x);
+            m.y = sel_lanes(dl, 0u, m.y);
+        }
+    }
+    if (!live) return;
+    const uint64_t t1 = t0 + (uint64_t)K;
+    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    A.meta[i] = m;
+    if (ep.x != ep0) {
+        ep.w = max_exp(last);
+        A.ep[i] = ep;
+        if (A.qsum) A.qsum[i] = 0.0;
+    }
+    if ((i & 63) == 0) A.clock[i >> 6] = t1;
+    if constexpr (kSum) A.reward_sum[i] += rsum;
+    if (i == 0) bump_count(A, t1);
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
@@ -1425,25 +1582,27 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
     } else if (A.rb.win_bytes && !A.log && !(A.flags & G2048_NO_AUTORESET)) {
         // the headline case
         const bool p410 = (A.flags & G2048_P4_10) != 0u, qr = A.rb.rows % 4 == 0;
-        // past 1M boards the launch is store-bound: five waves per SIMD (a few
-        // spilled registers) beat four there in every measurement (4M x 16: 604-681 us against
-        // 700-748), and lose below (1M x 64: +3 %; 64k: +70 %)
-        const bool big = A.n > (1 << 20);
+        // from 256k boards on the launch is store-bound: the warp-specialised
+        // k_rollout_ws (compute and store waves decoupled by an LDS ring) runs 4M x 16 in 445 us
+        // against 694 for the five-wave k_rollout_lean, 1M x 64 in 524 against 674, 256k x 64 in
+        // 124 against 147; at 64k it loses (42 us against 28: one compute wave per SIMD there)
+        const bool big = A.n >= (1 << 18);
         // (the p(4) = 0.1 instances carry two more Philox blocks per quad: under the four-wave
         // register cap they spilled, so they take a three-wave cap -- at 64k boards the kernel
         // runs one wave per SIMD anyway)
 #define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q, 0x1F, (P) ? 3 : 4>), grid, block, 0, st, A)
-#define G2048_LEAN5(S, Q) hipLaunchKernelGGL((k_rollout_lean<S, false, Q, 0x1F, 5>), grid, block, 0, st, A)
-        if (reward_sum) {
+#define G2048_WS(S, P) hipLaunchKernelGGL((k_rollout_ws<S, P>), grid, dim3(2 * kBlock), 0, st, A)
+        if (big) {
+            if (reward_sum) { if (p410) G2048_WS(true, true); else G2048_WS(true, false); }
+            else { if (p410) G2048_WS(false, true); else G2048_WS(false, false); }
+        } else if (reward_sum) {
             if (p410) { if (qr) G2048_LEAN(true, true, true); else G2048_LEAN(true, true, false); }
-            else if (big) { if (qr) G2048_LEAN5(true, true); else G2048_LEAN5(true, false); }
             else { if (qr) G2048_LEAN(true, false, true); else G2048_LEAN(true, false, false); }
         } else {
             if (p410) { if (qr) G2048_LEAN(false, true, true); else G2048_LEAN(false, true, false); }
-            else if (big) { if (qr) G2048_LEAN5(false, true); else G2048_LEAN5(false, false); }
             else { if (qr) G2048_LEAN(false, false, true); else G2048_LEAN(false, false, false); }
         }
-#undef G2048_LEAN5
+#undef G2048_WS
 #undef G2048_LEAN
     } else if (A.rb.win_bytes) {
         if (reward_sum) hipLaunchKernelGGL((k_rollout<true, true, true>), grid, block, 0, st, A);

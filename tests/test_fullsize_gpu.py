@@ -61,13 +61,14 @@ def test_bench_rollout_full_size_vs_oracle(g2048):
         assert ref.ep[:, 0].sum() > 0  # episodes ended and auto-reset inside the launch
 
 
-@pytest.mark.parametrize("n_all", [1 << 20, (1 << 20) + 4160])
+@pytest.mark.parametrize("n_all", [(1 << 18) - 64, (1 << 20) + 4160])
 def test_rollout_large_n_vs_oracle(g2048, n_all):
-    """1 M boards, ring of N*16 rows (the headline kernel's quad-row path), one launch of 3 steps
-    and four of 16 -- every clock phase -- against the oracle on four 1 000-board slices.  At this
-    size the store queue backs up: the first version of k_rollout_lean stored some boards with the
-    first word already rewritten by the next instruction (store_board in g2048.hip).  Past 1 M
-    boards (the second case, ragged) the five-waves-per-SIMD instance runs."""
+    """256k / 1 M boards, ring of N*16 rows, one launch of 3 steps and four of 16 -- every clock
+    phase -- against the oracle on four 1 000-board slices.  Just below 256k boards
+    k_rollout_lean runs (its quad-row path; its first version, under store-queue back-pressure,
+    stored some boards with the first word already rewritten by the next instruction: store_board
+    in g2048.hip).  From 256k boards on (the second case, ragged: a partly live last workgroup)
+    the warp-specialised k_rollout_ws runs."""
     k, seed = 16, 7
     env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
     rb = g2048.ReplayBuffer(n_all * k, device=DEV)
@@ -81,7 +82,7 @@ def test_rollout_large_n_vs_oracle(g2048, n_all):
     ring = {name: _np(getattr(rb, name)) for name in ["s", "s2", "a", "r", "d"]}
     # the last launch wrote all k rows: its reward sums are the rows' rewards per board
     assert np.array_equal(_np(rs), ring["r"].reshape(k, n_all).astype(np.int64).sum(0))
-    for i0 in (0, 68000, 500000, n_all - 1000):
+    for i0 in (0, 68000, n_all // 2, n_all - 1000):
         n = 1000
         ref = O.OracleEnv(n, seed=seed, board_offset=i0)
         ref_rb = O.OracleReplay(n * k)
@@ -91,6 +92,33 @@ def test_rollout_large_n_vs_oracle(g2048, n_all):
         rows = (np.arange(k)[:, None] * n_all + np.arange(i0, i0 + n)[None, :]).reshape(-1)
         for name in ["s", "s2", "a", "r", "d"]:
             assert np.array_equal(ring[name][rows], getattr(ref_rb, name)), (i0, name)
+
+
+@pytest.mark.parametrize("p4", [0.5, 0.1])
+def test_ws_rollout_equals_single_steps(g2048, p4):
+    """The large-N kernel (k_rollout_ws: compute and store waves handing transitions over through
+    an LDS ring, nt stores) == single steps at 1 M + 64 boards, both p(4) modes, reward sums on
+    and off, launches of 5 / 16 / 11 steps (every clock phase, a ring that wraps inside a launch),
+    and no hand-over timeouts (the env's error counter stays 0)."""
+    n, seed = (1 << 20) + 64, 99
+    e1 = g2048.VecEnv2048(n, seed=seed, device=DEV, p4=p4)
+    e2 = g2048.VecEnv2048(n, seed=seed, device=DEV, p4=p4)
+    r1, r2 = g2048.ReplayBuffer(24 * n, device=DEV), g2048.ReplayBuffer(24 * n, device=DEV)
+    rs = torch.zeros(n, dtype=torch.int64, device=DEV)
+    acc = torch.zeros(n, dtype=torch.int64, device=DEV)
+    for j, k in enumerate((5, 16, 11)):
+        e1.rollout(k, replay=r1, reward_sum=rs if j % 2 else None)
+        for _ in range(k):
+            r, _, _ = e2.step(None, replay=r2)
+            if j % 2:
+                acc += r
+        assert torch.equal(e1.board, e2.board) and torch.equal(e1.meta, e2.meta), k
+        assert torch.equal(e1.clock, e2.clock) and torch.equal(e1.ep, e2.ep), k
+    assert torch.equal(rs, acc)
+    for name in ["s", "s2", "a", "r", "d", "count"]:
+        assert torch.equal(getattr(r1, name), getattr(r2, name)), name
+    assert int(e1.ep[:, 0].sum()) > 0
+    e1.check_errors()
 
 
 @pytest.mark.parametrize("qdtype", [np.float32, np.float64])

@@ -80,7 +80,7 @@ struct WsBuf {
 };
 
 template <bool kSum, bool kP410>
-__global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
+__global__ __launch_bounds__(2 * kBlock) void k_rollout_ws_barrier(StepArgs A) {
     __shared__ uint4 s_dir[8];
     __shared__ WsBuf buf[2];
     const bool storer = threadIdx.x >= kBlock;
@@ -189,11 +189,19 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
     if (i == 0) bump_count(A, t1);
 }
 
+template <int kD, int kAux>
+void launch_ws2(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_rollout_ws<false, false, kD, kAux>), dim3(grid_for(e->n)), dim3(2 * kBlock), 0, st, A);
+}
+
 void launch_ws(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
     make_args(e, rb, A);
     A.k_steps = K;
-    hipLaunchKernelGGL((k_rollout_ws<false, false>), dim3(grid_for(e->n)), dim3(2 * kBlock), 0, st, A);
+    hipLaunchKernelGGL((k_rollout_ws_barrier<false, false>), dim3(grid_for(e->n)), dim3(2 * kBlock), 0, st, A);
 }
 
 template <bool kQR, int kWaves>
@@ -220,9 +228,13 @@ struct Variant {
 const Variant kVariants[] = {
     {"k_rollout (general path)", launch_old},
     {"k_rollout_lean", launch_lean},
-    {"warp-specialised (k_rollout_ws)", launch_ws},
+    {"warp-specialised, barrier per step", launch_ws},
     {"lean, 5 waves/SIMD", launch_occ<true, 5>},
     {"lean no-QR, 4 waves/SIMD", launch_occ<false, 4>},
+    {"ws2: pair ring 4 steps", launch_ws2<4, 0>},
+    {"ws2: pair ring 8 steps", launch_ws2<8, 0>},
+    {"ws2: pair ring 8 steps, nt", launch_ws2<8, 2>},
+    {"ws2: pair ring 12 steps, nt", launch_ws2<12, 2>},
     // timing only (parity MISMATCH expected: sections left unwritten)
     {"lean, no byte stores (a, d)", launch_part<0x0B>},
     {"lean, s + s2 only", launch_part<0x03>},
@@ -231,7 +243,7 @@ const Variant kVariants[] = {
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
-constexpr int kParityVariants = 5;  // the others skip sections of the ring
+constexpr int kParityVariants = 9;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
