@@ -68,6 +68,9 @@ def parse():
     p.add_argument("--rollout-k", type=int, default=64, help="env steps per rollout launch")
     p.add_argument("--rollout-k-extra", default="256",
                    help="further K values timed beside the headline (rollout_k_sweep field)")
+    p.add_argument("--large-n", default="4194304x16",
+                   help="boards x K of a large-N rollout timed beside the headline "
+                        "(rollout_large_n field; '' skips it)")
     p.add_argument("--step-steps", type=int, default=2000,
                    help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
@@ -197,7 +200,7 @@ def capture(fn, n_steps: int):
 
 
 # ------------------------------------------------------------------ headline: the rollout kernel
-def bench_rollout(args, world, rank, dev, k_override=None):
+def bench_rollout(args, world, rank, dev, k_override=None, n_override=None):
     """W untimed + `steps` timed k_rollout launches (K env steps of every board each, replay
     append into an N*K-row ring), replayed from hipGraphs of --graph-steps launches (the kernel
     reads its step clock and ring row from device memory, so a replay is a fresh rollout): back
@@ -205,7 +208,8 @@ def bench_rollout(args, world, rank, dev, k_override=None):
     rocprofv3 --kernel-trace reports), not kernel + host enqueue gap."""
     import g2048
 
-    n, k = args.boards, (args.rollout_k if k_override is None else k_override)
+    n = args.boards if n_override is None else n_override
+    k = args.rollout_k if k_override is None else k_override
     env = g2048.VecEnv2048(n, seed=args.seed, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(n * k, device=dev)
 
@@ -372,6 +376,19 @@ def main():
         lx = rx["ev_s"] / args.steps
         ksweep.append({"k": kx, "env_steps_per_s": n * kx * world * args.steps / rx["wall"],
                        "launch_us": lx * 1e6, "frac": ROLLOUT_BYTES * n * kx / lx / 1e9 / HBM_PEAK_GBS})
+    # the same launch at large N (boards x K): past 256k boards the ring streams to HBM and
+    # g2048_env_rollout dispatches the warp-specialised k_rollout_ws
+    large = None
+    if args.large_n:
+        nl, _, kl = args.large_n.partition("x")
+        nl, kl = int(nl), int(kl or 16)
+        rl = bench_rollout(args, world, rank, dev, k_override=kl, n_override=nl)
+        ll = rl["ev_s"] / args.steps
+        large = {"boards_per_gpu": nl, "k": kl, "kernel": "k_rollout_ws" if nl >= (1 << 18)
+                 else "k_rollout_lean", "env_steps_per_s": nl * kl * world * args.steps / rl["wall"],
+                 "launch_us": ll * 1e6, "achieved_GBs": ROLLOUT_BYTES * nl * kl / ll / 1e9,
+                 "frac": ROLLOUT_BYTES * nl * kl / ll / 1e9 / HBM_PEAK_GBS}
+        torch.cuda.empty_cache()
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
     for leg in [x for x in args.train.split(",") if x]:
@@ -417,6 +434,8 @@ def main():
         }
         if ksweep:
             line["rollout_k_sweep"] = ksweep
+        if large:
+            line["rollout_large_n"] = large
         if step:
             line["step_kernel"] = step
         if train:

@@ -22,7 +22,7 @@ def test_bench_configs4_eight_ranks_on_one_gpu():
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--boards", "65536",
            "--train", "conv", "--train-dtypes", "fp64,fp32", "--train-updates", "10",
            "--step-steps", "0", "--steps", "20", "--warmup", "5", "--rollout-k-extra", "",
-           "--no-cpu-baseline"]
+           "--large-n", "", "--no-cpu-baseline"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]

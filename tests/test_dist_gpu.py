@@ -137,7 +137,7 @@ def test_bench_two_ranks():
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
                           "--steps", "20", "--warmup", "5", "--step-steps", "200",
                           "--train", "dense64,dense@512", "--train-dtypes", "fp32,fp64",
-                          "--train-updates", "20",
+                          "--train-updates", "20", "--large-n", "524288x16",
                           "--no-cpu-baseline"], capture_output=True, text=True, env=env,
                          timeout=300, cwd=root)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -145,6 +145,8 @@ def test_bench_two_ranks():
     assert line["n_gpus"] == 2
     assert line["config"]["global_boards"] == 2 * 65536
     assert line["value"] > 0 and line["step_kernel"]["env_steps_per_s"] > 0
+    big = line["rollout_large_n"]  # each rank's 512k boards through k_rollout_ws
+    assert big["kernel"] == "k_rollout_ws" and big["boards_per_gpu"] == 524288 and big["frac"] > 0
     assert line["learner"]["dense64.fp32"]["graphed_loop"] is True
     assert line["learner"]["dense64.fp64"]["path"] == "fused HIP kernels"
     for leg in ("dense64.fp32", "dense64.fp64", "dense@512.fp32", "dense@512.fp64"):
