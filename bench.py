@@ -388,6 +388,9 @@ def main():
                  else "k_rollout_lean", "env_steps_per_s": nl * kl * world * args.steps / rl["wall"],
                  "launch_us": ll * 1e6, "achieved_GBs": ROLLOUT_BYTES * nl * kl / ll / 1e9,
                  "frac": ROLLOUT_BYTES * nl * kl / ll / 1e9 / HBM_PEAK_GBS}
+        recl = pmc_record(f"{large['kernel']}@{nl}x{kl}")
+        large["traffic"] = recl["hbm_bytes_per_launch"] if recl and "hbm_bytes_per_launch" in recl else None
+        large["bytes_per_launch"] = ROLLOUT_BYTES * nl * kl
         torch.cuda.empty_cache()
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}

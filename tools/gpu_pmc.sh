@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 run_pass() {  # name, counters...
     local name=$1; shift
     timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-trace --output-format csv \
-        -d gpurun_out/pmc_$name -o $name -- python tools/pmc_step.py > gpurun_out/pmc_$name.log 2>&1 \
+        -d /tmp/pmc_$name -o $name -- python tools/pmc_step.py > gpurun_out/pmc_$name.log 2>&1 \
         || { tail -30 gpurun_out/pmc_$name.log; return 1; }
 }
 run_pass fetch FETCH_SIZE && run_pass write WRITE_SIZE && \
 run_pass sq SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA && \
-python tools/pmc_summary.py gpurun_out/pmc.json gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq
+python tools/pmc_summary.py gpurun_out/pmc.json /tmp/pmc_fetch /tmp/pmc_write /tmp/pmc_sq

@@ -20,6 +20,8 @@ SHAPES = {65536: 64, 1 << 22: 16}  # tools/pmc_step.py: boards -> rollout K
 
 
 def kernel_key(name: str, grid: int):
+    if "k_rollout_ws" in name:  # 512-thread workgroups of 256 boards: two work-items per board
+        return f"k_rollout_ws@{grid // 2}x{SHAPES.get(grid // 2, 0)}"
     if "k_rollout" in name:
         return f"k_rollout@{grid}x{SHAPES.get(grid, 0)}"
     if "k_step" in name:
@@ -57,6 +59,7 @@ def main(out_path, *dirs):
                        hbm_bytes_per_launch=(2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
         if "SQ_WAVES" in c and c["SQ_WAVES"] > 0:
             steps = int(key.split("x")[1]) if key.startswith("k_rollout") else 1
+            # (k_rollout_ws: SQ_WAVES counts the compute and the store waves)
             per = lambda n: c.get(n, 0.0) / c["SQ_WAVES"] / steps  # noqa: E731
             rec["issue"] = {
                 "valu_insts_per_wave_step": per("SQ_INSTS_VALU"),
