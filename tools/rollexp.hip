@@ -277,8 +277,10 @@ int main(int argc, char** argv) {
             return 1;
         }
     }
-    // parity: 5 launches from the same start (an odd K first moves every clock to an odd step)
-    for (int v = 0; v < nv; ++v) {
+    // parity: 5 launches from the same start (an odd K first moves every clock to an odd step);
+    // ROLLEXP_PHASE0=1 skips them (timing then starts from step 0, as bench.py's legs do)
+    const bool phase0 = getenv("ROLLEXP_PHASE0") != nullptr;
+    for (int v = 0; v < nv && !phase0; ++v) {
         kVariants[v].fn(envs[v], rbs[v], 3, st);
         for (int it = 0; it < 4; ++it) kVariants[v].fn(envs[v], rbs[v], K, st);
     }
@@ -297,7 +299,7 @@ int main(int argc, char** argv) {
     auto r0 = fetch(rbs[0]->r, C);
     auto d0 = fetch(rbs[0]->d, C);
     int bad = 0;
-    for (int v = 1; v < kParityVariants; ++v) {
+    for (int v = 1; v < kParityVariants && !phase0; ++v) {
         const bool ok = fetch(envs[v]->board, n * 16) == b0 && fetch(envs[v]->meta, n * 2) == m0 &&
                         fetch(envs[v]->ep, n * 4) == e0 &&
                         fetch(envs[v]->clock, (n + 63) / 64) == c0 &&
