@@ -492,9 +492,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // already overwritten).  The nop reads the four registers, so they stay live -- nothing is
 // written into them -- until it has issued, two wait states after the store (both volatile:
 // their order is kept).  tools/store_hazard_audit.py checks the compiled kernels.
+template <int kAux = 0>
 __device__ __forceinline__ void store_board(const Board& b, __amdgpu_buffer_rsrc_t rw,
                                             uint32_t voff, uint32_t soff) {
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, voff, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{b.r0, b.r1, b.r2, b.r3}, rw, voff, soff, kAux);
     asm volatile("s_nop 1" ::"v"(b.r0), "v"(b.r1), "v"(b.r2), "v"(b.r3));
 }
 
@@ -652,7 +653,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 //   kStores: ring sections written (bits s, s2, a, r, d) -- all in the library; tools/rollexp.hip
 //   times subsets to price the stores.
 //   kWaves: the occupancy hint (the library uses 4; tools/rollexp.hip times others at large N).
-template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F, int kWaves = 4>
+//   kAux: the ring stores' cache-policy bits (the library uses 0; tools/rollexp.hip times nt).
+template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F, int kWaves = 4, int kAux = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void k_rollout_lean(StepArgs A) {
     __shared__ uint4 s_dir[16];
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -703,19 +705,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
                    const Off& o) {
         G2048_MARK(store_s, "+v"(b.r0), "+v"(b.r1), "+v"(b.r2), "+v"(b.r3));
         if constexpr (kStores & 1)
-            store_board(b, rw, o.s, o.o16);
+            store_board<kAux>(b, rw, o.s, o.o16);
         bool done;
         const uint32_t r = lean_step(b, w, spawn_exp<kP410>(w, v, p4), F, I, done, k255);
         m.x += r;
         m.y += 1u;
         if constexpr (kSum) rsum += r;
         if constexpr ((kStores & 2) != 0)
-            store_board(b, rw, o.s2, o.o16);
+            store_board<kAux>(b, rw, o.s2, o.o16);
         if constexpr ((kStores & 4) != 0)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, o.a, o.o1, 0);
-        if constexpr ((kStores & 8) != 0) __builtin_amdgcn_raw_buffer_store_b32(r, rw, o.r, o.o4, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(w >> 30), rw, o.a, o.o1, kAux);
+        if constexpr ((kStores & 8) != 0) __builtin_amdgcn_raw_buffer_store_b32(r, rw, o.r, o.o4, kAux);
         if constexpr ((kStores & 16) != 0)
-            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, o.d, o.o1, 0);
+            __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done, rw, o.d, o.o1, kAux);
         // a wave-uniform branch whose body is selects: every value keeps its registers (a
         // lane-masked `if (done)` made hipcc copy the board and counters through phi moves, and
         // a v_mov costs a full issue turn)

@@ -189,6 +189,14 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws_barrier(StepArgs A) {
     if (i == 0) bump_count(A, t1);
 }
 
+template <int kAux>
+void launch_lean_aux(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
+    StepArgs A;
+    make_args(e, rb, A);
+    A.k_steps = K;
+    hipLaunchKernelGGL((k_rollout_lean<false, false, true, 0x1F, 4, kAux>), dim3(grid_for(e->n)), dim3(kBlock), 0, st, A);
+}
+
 template <int kD, int kAux>
 void launch_ws2(g2048_env* e, g2048_replay* rb, int K, hipStream_t st) {
     StepArgs A;
@@ -231,6 +239,13 @@ const Variant kVariants[] = {
     {"warp-specialised, barrier per step", launch_ws},
     {"lean, 5 waves/SIMD", launch_occ<true, 5>},
     {"lean no-QR, 4 waves/SIMD", launch_occ<false, 4>},
+    {"lean, nt stores", launch_lean_aux<2>},
+    {"lean, aux 1 (glc)", launch_lean_aux<1>},
+    {"lean, aux 16 (sc1)", launch_lean_aux<16>},
+    {"lean, aux 17 (sc0 sc1)", launch_lean_aux<17>},
+    {"lean, aux 3 (sc0 nt)", launch_lean_aux<3>},
+    {"ws, aux 1", launch_ws2<8, 1>},
+    {"ws, aux 3", launch_ws2<8, 3>},
     {"ws2: pair ring 4 steps", launch_ws2<4, 0>},
     {"ws2: pair ring 8 steps", launch_ws2<8, 0>},
     {"ws2: pair ring 8 steps, nt", launch_ws2<8, 2>},
@@ -243,7 +258,7 @@ const Variant kVariants[] = {
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
-constexpr int kParityVariants = 9;  // the others skip sections of the ring
+constexpr int kParityVariants = 16;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
