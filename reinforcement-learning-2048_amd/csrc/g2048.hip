@@ -641,6 +641,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     G2048_ROLL_MARK(3);
 }
 
+constexpr int kRingSc1 = 16;  // the sc1 bit of a gfx950 buffer store's cache policy
+
 // The headline instance of g2048_env_rollout -- ring in one buffer window, auto-reset on, no
 // episode log: four steps per iteration from one Philox block (one word per step), the next
 // quad's block drawn at the top of a quad, and each step's direction selectors read from LDS one
@@ -653,7 +655,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
 //   kStores: ring sections written (bits s, s2, a, r, d) -- all in the library; tools/rollexp.hip
 //   times subsets to price the stores.
 //   kWaves: the occupancy hint (the library uses 4; tools/rollexp.hip times others at large N).
-//   kAux: the ring stores' cache-policy bits (the library uses 0; tools/rollexp.hip times nt).
+//   kAux: the ring stores' cache-policy bits (the library uses kRingSc1; tools/rollexp.hip
+//   times the others).
 template <bool kSum, bool kP410, bool kQR, int kStores = 0x1F, int kWaves = 4, int kAux = 0>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))) void k_rollout_lean(StepArgs A) {
     __shared__ uint4 s_dir[16];
@@ -1013,7 +1016,8 @@ inline uint32_t p4_thresh(uint32_t flags) {
 // store wave and a store wave waiting on a full store queue stalls only itself.  Every wait is
 // capped: a broken hand-over ends the loop and bumps the env's error counter (env.check_errors()
 // raises) instead of hanging the GPU.
-// kAux: the ring stores' cache-policy bits (2 = nt: the ring is not re-read by this launch).
+// kAux: the ring stores' cache-policy bits: 3 = sc0 | nt (4M x 16: 461 us against 478 with nt
+// alone, 593 with sc0 alone).
 // kD = 8: 78 KB of LDS, two workgroups per CU (4M x 16: 445 us against 694 for the five-wave
 // k_rollout_lean; 4 or 12 steps: 622 / 652 us).  The same transitions, bit for bit.
 struct alignas(16) PairSlot {
@@ -1033,7 +1037,7 @@ __device__ __forceinline__ bool wait_until(const uint32_t* c, uint32_t want) {
     return false;
 }
 
-template <bool kSum, bool kP410, int kD = 8, int kAux = 2>
+template <bool kSum, bool kP410, int kD = 8, int kAux = 3>
 __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
     __shared__ uint4 s_dir[8];
     __shared__ PairSlot ring[4][kD];
@@ -1592,7 +1596,9 @@ int g2048_env_rollout(g2048_env* e, int32_t k_steps, g2048_replay* rb, int64_t* 
         // (the p(4) = 0.1 instances carry two more Philox blocks per quad: under the four-wave
         // register cap they spilled, so they take a three-wave cap -- at 64k boards the kernel
         // runs one wave per SIMD anyway)
-#define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q, 0x1F, (P) ? 3 : 4>), grid, block, 0, st, A)
+// (ring stores with the sc1 cache-policy bit: 64k x 64 25.1 us against 28.1 with none, 27.5
+// with sc0, 28.3-30.0 with nt; tools/rollexp.hip, profiles/r03/rollexp_cachepolicy_*)
+#define G2048_LEAN(S, P, Q) hipLaunchKernelGGL((k_rollout_lean<S, P, Q, 0x1F, (P) ? 3 : 4, kRingSc1>), grid, block, 0, st, A)
 #define G2048_WS(S, P) hipLaunchKernelGGL((k_rollout_ws<S, P>), grid, dim3(2 * kBlock), 0, st, A)
         if (big) {
             if (reward_sum) { if (p410) G2048_WS(true, true); else G2048_WS(true, false); }
