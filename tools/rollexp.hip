@@ -246,6 +246,9 @@ const Variant kVariants[] = {
     {"lean, aux 3 (sc0 nt)", launch_lean_aux<3>},
     {"ws, aux 1", launch_ws2<8, 1>},
     {"ws, aux 3", launch_ws2<8, 3>},
+    {"ws, aux 16 (sc1)", launch_ws2<8, 16>},
+    {"ws, aux 18 (sc1 nt)", launch_ws2<8, 18>},
+    {"ws, aux 19 (sc0 sc1 nt)", launch_ws2<8, 19>},
     {"ws2: pair ring 4 steps", launch_ws2<4, 0>},
     {"ws2: pair ring 8 steps", launch_ws2<8, 0>},
     {"ws2: pair ring 8 steps, nt", launch_ws2<8, 2>},
@@ -258,7 +261,7 @@ const Variant kVariants[] = {
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
 };
-constexpr int kParityVariants = 16;  // the others skip sections of the ring
+constexpr int kParityVariants = 19;  // the others skip sections of the ring
 
 template <typename T>
 std::vector<T> fetch(const T* d, size_t n) {
