@@ -260,6 +260,8 @@ const Variant kVariants[] = {
     {"stores only (all five)", launch_store<0x1F, 0>},
     {"stores only (s + s2)", launch_store<0x03, 0>},
     {"stores only (all five, nt)", launch_store<0x1F, 2>},
+    {"stores only (all five, sc1)", launch_store<0x1F, 16>},
+    {"lean, no ring stores (sc1 build)", launch_part<0x00>},
 };
 constexpr int kParityVariants = 19;  // the others skip sections of the ring
 
