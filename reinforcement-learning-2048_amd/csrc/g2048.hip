@@ -1105,6 +1105,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
     Board last = b;
     const uint32_t k255 = opaque_255();
     uint4 blk = make_uint4(0, 0, 0, 0), vb = blk, vb2 = blk;
+    bool ok = true;  // wave-uniform: false once a hand-over timed out
     for (int s = 0; s < K; ++s) {
         const uint64_t t = t0 + (uint64_t)s;
         if (s == 0 || (t & 3u) == 0u) {
@@ -1117,6 +1118,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
         // slot s % kD is free once the store wave has taken step s - kD
         if (s >= kD && !wait_until(&cons[pair], (uint32_t)(s - kD) + 1u)) {
             if (lane == 0) atomicAdd(A.err, 1ull);
+            ok = false;
             break;
         }
         PairSlot& B = ring[pair][s % kD];
@@ -1150,7 +1152,10 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
             m.y = sel_lanes(dl, 0u, m.y);
         }
     }
-    if (!live) return;
+    // After a timed-out hand-over the wave leaves its boards, meta, episode counters and clock
+    // at t0 (ring rows it handed over may be written; the env's error counter is set, so
+    // check_errors() raises and the caller must reset the env).
+    if (!live || !ok) return;
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     A.meta[i] = m;

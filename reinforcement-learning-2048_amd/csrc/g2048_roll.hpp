@@ -426,8 +426,10 @@ __device__ __forceinline__ uint32_t lean_step(Board& b, uint32_t w, uint32_t e, 
     //    always leaves one, so n == 0 iff nothing moved and the board is full) and no equal
     //    neighbours across the lines (adjacent bytes of a line word; v_xad: bit 7 of
     //    (x ^ y) + 0x7F is set iff the bytes differ) -- or the board is empty (16 empties, n mod
-    //    16 = 0, and no tiles to pair)
-    done = (n | across_pairs(L0, L1, L2, L3)) == 0u;
+    //    16 = 0).  The empty board's zero bytes compare equal in across_pairs, so its flags are
+    //    masked with N3 (bit 7 of byte j: cell 3 of line j holds a tile), which is all ones on a
+    //    full board -- the only other board with n == 0 -- and zero on the empty one.
+    done = (n | (across_pairs(L0, L1, L2, L3) & N3)) == 0u;
     // 7) back to rows
     G2048_MARK(net_inv, "+v"(o0), "+v"(o1), "+v"(o2), "+v"(o3));
     dir_net(o0, o1, o2, o3, I, b.r0, b.r1, b.r2, b.r3);

@@ -65,7 +65,8 @@ class BoardBatch:
         return self._score
 
     def simple_score(self) -> torch.Tensor:
-        return BoardBatch(self.board).state.flatten(1).sum(1)
+        # sum of `state` (src/board.py:204-205): tile values, or exponents after log_scale()
+        return self.state.flatten(1).sum(1)
 
     def log_scale(self) -> "BoardBatch":
         return BoardBatch(self.board, self._score, log=True)

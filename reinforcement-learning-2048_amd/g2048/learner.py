@@ -24,9 +24,22 @@ from .nets import NETS, make_net
 from . import qnet
 from .optim import FusedAdam
 
-# Trainer.state_dict layout (experiment.py wraps it in its own file format tag).  1 (round 1): env meta [N, 4], no clock.  3: meta [N, 2] + a per-wave
-# clock, and the ABI-v3 random policy (include/g2048.h), whose draws differ from earlier builds'.
+# Trainer.state_dict layout (experiment.py wraps it in its own file format tag).  Versions:
+#   1 (round 1): env meta [N, 4], no clock;
+#   2 (round 2): meta [N, 2] + a per-wave clock, ABI-v2 random-policy draws (no version key was
+#                written then; load_state_dict infers 1 / 2 from the meta shape);
+#   3: the layout of 2 with the ABI-v3 random policy (include/g2048.h), whose draws differ.
 TRAINER_STATE_VERSION = 3
+_STATE_LAYOUTS = {1: "env meta [N, 4], no step clock", 2: "env meta [N, 2] + per-wave clock, ABI-v2 "
+                  "random-policy draws", 3: "env meta [N, 2] + per-wave clock, ABI-v3 random-policy "
+                  "draws"}
+
+
+def _state_version(st: dict) -> int:
+    if "trainer_state_version" in st:
+        return int(st["trainer_state_version"])
+    meta = st.get("env", {}).get("meta")
+    return 1 if meta is not None and meta.shape[-1] == 4 else 2
 
 
 class DQNLearner:
@@ -521,12 +534,12 @@ class Trainer:
     @torch.no_grad()
     def load_state_dict(self, st: dict) -> None:
         self._loop_graph = None  # host-side env state (the reset epoch) is baked into a capture
-        fmt = st.get("trainer_state_version", 1)
+        fmt = _state_version(st)
         if fmt != TRAINER_STATE_VERSION:
             raise ValueError(
-                f"trainer state version {fmt} is not readable by this build (version "
-                f"{TRAINER_STATE_VERSION}: env meta [N, 2] + per-wave clock, ABI-v3 random-policy "
-                "draws); resume it with the build that wrote it")
+                f"trainer state version {fmt} ({_STATE_LAYOUTS.get(fmt, 'unknown layout')}) is not "
+                f"readable by this build (version {TRAINER_STATE_VERSION}: "
+                f"{_STATE_LAYOUTS[TRAINER_STATE_VERSION]}); resume it with the build that wrote it")
         env, rb = self.env, self.replay
         e = st["env"]
         for k in ("n", "seed", "board_offset", "flags"):

@@ -358,6 +358,43 @@ def test_rollout_ring_layouts(g2048):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("autoreset", [True, False])
+def test_empty_board_is_terminal(g2048, autoreset):
+    """An all-empty board has no legal move, so the random-policy step (lean_step) must report
+    done (the oracle: legal == 0 -> done, src/dqn_lib.py:17-18) and, with auto-reset, deal a
+    fresh board -- through the single step and the rollout, ring rows included."""
+    n, seed = 777, 2024
+    b = _random_boards(n, 9)
+    b[::3] = 0  # every third board empty (b[:4] are empty already)
+    flags = 0 if autoreset else O.NO_AUTORESET
+    for use_rollout in (False, True):
+        env = g2048.VecEnv2048(n, seed=seed, device=DEV, reset=False, autoreset=autoreset)
+        env.board.copy_(torch.from_numpy(b))
+        rb = g2048.ReplayBuffer(8 * n, device=DEV)
+        ref = O.OracleEnv(n, seed=seed, flags=flags, reset=False)
+        ref.board[:] = b
+        ref_rb = O.OracleReplay(8 * n)
+        if use_rollout:
+            env.rollout(5, replay=rb)
+        else:
+            for _ in range(5):
+                env.step(None, replay=rb)
+        outs = [ref.step(O.MODE_RANDOM, replay=ref_rb) for _ in range(5)]
+        assert outs[0]["done"][::3].all() and outs[0]["legal"][::3].max() == 0
+        assert np.array_equal(_np(env.board), ref.board), use_rollout
+        assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta), use_rollout
+        assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep), use_rollout
+        for name in ["s", "s2", "a", "r", "d", "count"]:
+            assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), (name, use_rollout)
+        if not autoreset:
+            assert not ref.board[::3].any()  # finished boards stay as they are
+    # the single step's outputs agree with each other: done == (legal == 0)
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV, reset=False, autoreset=autoreset)
+    env.board.copy_(torch.from_numpy(b))
+    _, d, lg = env.step(None)
+    assert np.array_equal(_np(d), (_np(lg) == 0).astype(np.uint8))
+
+
 def test_rollout_vs_oracle(g2048):
     """The rollout against the CPU oracle directly (random-policy draws: half a Philox block per
     step), starting from an odd clock."""

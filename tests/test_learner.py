@@ -183,6 +183,15 @@ def test_fused_f64_routing_on_cpu():
         qnet.ConvUpdate64(conv64, conv64, 512)
 
 
+def test_trainer_state_version_inference():
+    """States written before the version key existed: round 1 (meta [N, 4]) and round 2
+    (meta [N, 2] + clock) are told apart by the meta shape."""
+    from g2048.learner import _state_version, TRAINER_STATE_VERSION
+    assert _state_version({"trainer_state_version": 3}) == TRAINER_STATE_VERSION == 3
+    assert _state_version({"env": {"meta": torch.zeros((5, 4))}}) == 1
+    assert _state_version({"env": {"meta": torch.zeros((5, 2))}}) == 2
+
+
 def test_board_batch_accessors():
     """BoardBatch answers the Board2048 accessors a reward_function uses (src/board.py:204-231)
     for every board: state (tile values), log_scale().state (exponents), simple_score,
@@ -196,6 +205,8 @@ def test_board_batch_accessors():
     assert st[0, 0, :3].tolist() == [2, 4, 131072] and int(st[2, 3, 3]) == 2 ** 31
     assert torch.equal(bb.log_scale().state.reshape(3, 16), b.long())
     assert bb.simple_score().tolist() == [2 + 4 + 131072, 0, 2 ** 31]
+    # Board2048.log_scale().simple_score() sums the exponents (src/board.py:204-205,224-231)
+    assert bb.log_scale().simple_score().tolist() == [1 + 2 + 17, 0, 31]
     assert bb.number_of_empty_cells().tolist() == [13, 16, 15]
     assert bb.merge_score().tolist() == [4, 0, 8]
     with pytest.raises(TypeError):

@@ -29,3 +29,33 @@ def test_no_store_data_hazard(tmp_path):
                         "-S", os.path.join(CSRC, f), "-o", s], check=True, capture_output=True)
         out.append(s)
     assert sum(store_hazard_audit.audit(s) for s in out) == 0
+
+
+def test_audit_sees_loads_and_branches(tmp_path):
+    """The audit sees every VGPR writer and follows branches: VALU writers count as hazards, LDS /
+    VMEM load writers are notes."""
+    import store_hazard_audit
+
+    cases = {
+        "valu": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                 "v_mov_b32 v5, 0\n", 1),
+        "lds": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                "ds_read_b128 v[6:9], v2\n", 0),
+        "vmem": ("global_store_dwordx4 v[0:1], v[4:7], off\n"
+                 "global_load_dword v7, v[0:1], off\n", 0),
+        "nop": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                "s_nop 1\nv_mov_b32 v5, 0\n", 0),
+        "branch": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                   "s_branch .LBB0_2\nv_mov_b32 v5, 0\n.LBB0_2:\nv_mov_b32 v4, 0\n", 1),
+        "cbranch": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                    "s_cbranch_scc1 .LBB0_3\nv_mov_b32 v1, 0\ns_endpgm\n.LBB0_3:\n"
+                    "v_add_u32 v6, v6, v6\n", 1),
+        "other": ("buffer_store_dwordx4 v[4:7], v1, s[0:3], 0 offen\n"
+                  "v_mov_b32 v8, 0\nds_read_b32 v3, v2\n", 0),
+    }
+    for name, (asm, want) in cases.items():
+        p = tmp_path / (name + ".s")
+        p.write_text("_Z1kv:\n" + asm)
+        notes = []
+        assert store_hazard_audit.audit(str(p), notes) == want, name
+        assert len(notes) == (name in ("lds", "vmem")), name

@@ -79,9 +79,12 @@ def test_load_rejects_mismatch(G):
     with pytest.raises(ValueError):
         c.load_state_dict(st)
     old = dict(st)
-    old.pop("trainer_state_version")  # a round-1 trainer state (env meta [N, 4], no clock)
-    with pytest.raises(ValueError, match="trainer state version 1"):
+    old.pop("trainer_state_version")  # a round-2 trainer state (no key, env meta [N, 2] + clock)
+    with pytest.raises(ValueError, match="trainer state version 2 .env meta \\[N, 2\\]"):
         a.load_state_dict(old)
+    old["env"] = dict(st["env"], meta=torch.zeros((a.env.n, 4), dtype=torch.int32))
+    with pytest.raises(ValueError, match="trainer state version 1 .env meta \\[N, 4\\]"):
+        a.load_state_dict(old)  # a round-1 trainer state (env meta [N, 4], no clock)
 
 
 def _move_ok(s, a, s2, r, letters=("u", "d", "l", "r")):
