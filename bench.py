@@ -45,18 +45,36 @@ ROLLOUT_BYTES = 38
 #   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
 STEP_BYTES = 37
 STEP_BYTES_BOOKKEEPING = 54
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r03")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
+INFINITY_CACHE_BYTES = 256 << 20  # MI355X_MICROARCH.md: die-level L3, 256 MiB
+RESIDENCY_RULE = ("MI355X_MICROARCH.md, Infinity Cache: a line stays resident while everything "
+                  "loaded or stored between two uses of it fits in about 256 MiB")
 
 
 def pmc_record(key: str):
-    """HBM bytes per launch (+ issue counters) of one kernel@shape from the committed rocprofv3
-    PMC passes (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE / SQ passes), or None."""
+    """Memory-side bytes per launch (+ issue counters) of one kernel@shape from the committed
+    rocprofv3 PMC passes (tools/gpu_pmc.sh: separate FETCH_SIZE / WRITE_SIZE / SQ passes, run as
+    their own rocprofv3 commands -- NOT measured by this process), with the file's provenance."""
     try:
         with open(PMC_FILE) as f:
-            return json.load(f).get(key)
+            d = json.load(f)
     except (OSError, ValueError):
         return None
+    r = d.get(key)
+    if r is not None:
+        r = dict(r, source=f"{os.path.relpath(PMC_FILE, ROOT)} ({d.get('_provenance', 'rocprofv3 --pmc passes, tools/gpu_pmc.sh')})")
+    return r
+
+
+def traffic_fields(rec, algorithmic: float) -> dict:
+    """`traffic` (bytes per launch from the committed PMC passes) and where it came from."""
+    if not rec or "hbm_bytes_per_launch" not in rec:
+        return {"traffic": None, "traffic_source": None}
+    t = rec["hbm_bytes_per_launch"]
+    return {"traffic": t, "traffic_over_algorithmic": t / algorithmic,
+            "traffic_source": rec["source"] + "; FETCH_SIZE + WRITE_SIZE at the memory side of "
+                              "L2 (Infinity-Cache hits included), per launch"}
 
 
 def parse():
@@ -71,6 +89,9 @@ def parse():
     p.add_argument("--large-n", default="4194304x16",
                    help="boards x K of a large-N rollout timed beside the headline "
                         "(rollout_large_n field; '' skips it)")
+    p.add_argument("--hbm-ring-launches", type=int, default=8,
+                   help="rollout_64k_hbm leg: the headline launch into a ring of this many "
+                        "launches' rows (> 256 MiB: streamed to HBM); 0 or 1 skips it")
     p.add_argument("--step-steps", type=int, default=2000,
                    help="timed one-launch-per-step env steps (0 = skip that leg)")
     p.add_argument("--graph-steps", type=int, default=100)
@@ -110,13 +131,28 @@ def launch_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
+def pick_device(local: int, world: int, backend: str, n_dev: int) -> int:
+    """The GPU index of local rank `local`.  Under RCCL ("nccl") every rank needs its own GPU:
+    more ranks than visible devices is refused (RCCL cannot put two ranks on one device, and
+    stacking them would silently measure a different workload).  The gloo rehearsal
+    (G2048_BENCH_BACKEND=gloo) may share devices round-robin."""
+    if world == 1:
+        return 0
+    if backend == "nccl":
+        if local >= n_dev or world > n_dev:
+            raise SystemExit(f"bench.py: WORLD_SIZE={world} ranks under RCCL but only {n_dev} "
+                             "visible GPU(s): one rank per GPU is required")
+        return local
+    return local % max(n_dev, 1)
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1) if world > 1 else 0)
+    dev = torch.device("cuda", pick_device(local, world, BACKEND, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
         if BACKEND == "nccl":
@@ -200,18 +236,19 @@ def capture(fn, n_steps: int):
 
 
 # ------------------------------------------------------------------ headline: the rollout kernel
-def bench_rollout(args, world, rank, dev, k_override=None, n_override=None):
+def bench_rollout(args, world, rank, dev, k_override=None, n_override=None, ring_launches=1):
     """W untimed + `steps` timed k_rollout launches (K env steps of every board each, replay
-    append into an N*K-row ring), replayed from hipGraphs of --graph-steps launches (the kernel
-    reads its step clock and ring row from device memory, so a replay is a fresh rollout): back
-    to back on the GPU, so the events' time per launch is the kernel's own duration (what
-    rocprofv3 --kernel-trace reports), not kernel + host enqueue gap."""
+    append into an N*K*ring_launches-row ring), replayed from hipGraphs of --graph-steps launches
+    (the kernel reads its step clock and ring row from device memory, so a replay is a fresh
+    rollout): back to back on the GPU, so the events' time per launch is the kernel's own duration
+    (what rocprofv3 --kernel-trace reports), not kernel + host enqueue gap.  With ring_launches R
+    > 1 each launch writes ring rows the previous R - 1 launches did not touch."""
     import g2048
 
     n = args.boards if n_override is None else n_override
     k = args.rollout_k if k_override is None else k_override
     env = g2048.VecEnv2048(n, seed=args.seed, device=dev, board_offset=rank * n)
-    rb = g2048.ReplayBuffer(n * k, device=dev)
+    rb = g2048.ReplayBuffer(n * k * ring_launches, device=dev)
 
     def launch():
         env.rollout(k, replay=rb)
@@ -234,8 +271,35 @@ def bench_rollout(args, world, rank, dev, k_override=None, n_override=None):
 
     wall, ev = timed(world, dev, run_all, 1)
     env.check_errors()
-    assert int(rb.count) == n * k
-    return dict(wall=wall, ev_s=ev, n=n, k=k, settle_ms=settle_ms)
+    assert int(rb.count) == n * k * ring_launches
+    # the bytes a launch's lines see between two uses: the ring (rows of R launches) + env state
+    ws = ROLLOUT_BYTES * n * k * ring_launches + n * (16 + 8 + 16) + 8 * ((n + 63) // 64)
+    return dict(wall=wall, ev_s=ev, n=n, k=k, settle_ms=settle_ms, board_offset=rank * n,
+                working_set=ws)
+
+
+def rollout_roofline(r, steps, rec):
+    """The roofline object of one rollout leg: algorithmic 38 B per env step over the HIP-event
+    launch time.  bound "hbm" only when the working set exceeds the Infinity Cache (else the
+    bytes need never reach HBM and the launch is bound by instruction issue)."""
+    launch_s = r["ev_s"] / steps
+    algo = ROLLOUT_BYTES * r["n"] * r["k"]
+    achieved = algo / launch_s / 1e9
+    hbm = r["working_set"] > INFINITY_CACHE_BYTES
+    out = {"bound": "hbm" if hbm else "issue",
+           "resident": "hbm-streamed" if hbm else "infinity-cache",
+           "working_set_bytes": r["working_set"], "residency_rule": RESIDENCY_RULE,
+           "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS,
+           "frac_note": ("of the HBM spec; the bytes stream to HBM" if hbm else
+                         "algorithmic bytes over the HBM spec, but the working set stays in the "
+                         "Infinity Cache: not an HBM-bandwidth claim (see `issue`)"),
+           "bytes_per_step": ROLLOUT_BYTES, "bytes_per_launch": algo,
+           "launch_us": launch_s * 1e6, "settle_ms": r["settle_ms"]}
+    out.update(traffic_fields(rec, algo))
+    if rec and rec.get("issue"):
+        out["issue"] = rec["issue"]
+    return out
 
 
 # ------------------------------------------------------------------ one launch per step
@@ -366,8 +430,11 @@ def main():
     ro = bench_rollout(args, world, rank, dev)
     n, k = ro["n"], ro["k"]
     value = n * k * world * args.steps / ro["wall"]
-    launch_s = ro["ev_s"] / args.steps
-    achieved = ROLLOUT_BYTES * n * k / launch_s / 1e9
+    ranges = [[ro["board_offset"], n]]
+    if world > 1:  # every rank's global board range: disjoint Philox subsequences
+        got = [None] * world
+        dist.all_gather_object(got, ranges[0])
+        ranges = got
     # the same launch at further K: a launch's first steps run slower than its steady state
     # (DESIGN.md 4.2), so the per-step time falls with K
     ksweep = []
@@ -375,7 +442,20 @@ def main():
         rx = bench_rollout(args, world, rank, dev, k_override=kx)
         lx = rx["ev_s"] / args.steps
         ksweep.append({"k": kx, "env_steps_per_s": n * kx * world * args.steps / rx["wall"],
-                       "launch_us": lx * 1e6, "frac": ROLLOUT_BYTES * n * kx / lx / 1e9 / HBM_PEAK_GBS})
+                       "launch_us": lx * 1e6, "frac": ROLLOUT_BYTES * n * kx / lx / 1e9 / HBM_PEAK_GBS,
+                       "resident": "infinity-cache" if rx["working_set"] <= INFINITY_CACHE_BYTES
+                       else "hbm-streamed"})
+    # the headline launch (64k boards x K) into a ring of --hbm-ring-launches launches' rows:
+    # every launch writes rows the previous ones did not, so the ring streams to HBM
+    hbm64 = None
+    if args.hbm_ring_launches > 1:
+        rh = bench_rollout(args, world, rank, dev, ring_launches=args.hbm_ring_launches)
+        hbm64 = {"boards_per_gpu": n, "k": k, "ring_rows": n * k * args.hbm_ring_launches,
+                 "kernel": "k_rollout_lean",
+                 "env_steps_per_s": n * k * world * args.steps / rh["wall"],
+                 "roofline": rollout_roofline(rh, args.steps, pmc_record(
+                     f"k_rollout@{n}x{k}r{args.hbm_ring_launches}"))}
+        torch.cuda.empty_cache()
     # the same launch at large N (boards x K): past 256k boards the ring streams to HBM and
     # g2048_env_rollout dispatches the warp-specialised k_rollout_ws
     large = None
@@ -383,14 +463,12 @@ def main():
         nl, _, kl = args.large_n.partition("x")
         nl, kl = int(nl), int(kl or 16)
         rl = bench_rollout(args, world, rank, dev, k_override=kl, n_override=nl)
-        ll = rl["ev_s"] / args.steps
-        large = {"boards_per_gpu": nl, "k": kl, "kernel": "k_rollout_ws" if nl >= (1 << 18)
-                 else "k_rollout_lean", "env_steps_per_s": nl * kl * world * args.steps / rl["wall"],
-                 "launch_us": ll * 1e6, "achieved_GBs": ROLLOUT_BYTES * nl * kl / ll / 1e9,
-                 "frac": ROLLOUT_BYTES * nl * kl / ll / 1e9 / HBM_PEAK_GBS}
-        recl = pmc_record(f"{large['kernel']}@{nl}x{kl}")
-        large["traffic"] = recl["hbm_bytes_per_launch"] if recl and "hbm_bytes_per_launch" in recl else None
-        large["bytes_per_launch"] = ROLLOUT_BYTES * nl * kl
+        kern = "k_rollout_ws" if nl >= (1 << 18) else "k_rollout_lean"
+        roof = rollout_roofline(rl, args.steps, pmc_record(f"{kern}@{nl}x{kl}"))
+        large = {"boards_per_gpu": nl, "k": kl, "kernel": kern,
+                 "env_steps_per_s": nl * kl * world * args.steps / rl["wall"],
+                 "launch_us": roof["launch_us"], "achieved_GBs": roof["achieved"],
+                 "frac": roof["frac"], "roofline": roof}
         torch.cuda.empty_cache()
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
@@ -402,7 +480,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args)
-    rec = pmc_record(f"k_rollout@{n}x{k}")
+    roof = rollout_roofline(ro, args.steps, pmc_record(f"k_rollout@{n}x{k}"))
+    roof["kernel"] = ("k_rollout_lean (g2048_env_rollout: ring in one buffer window, auto-reset, "
+                      "no episode log)")
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -422,19 +502,13 @@ def main():
                                    f"launch moving every board {k} times with replay append",
                        "boards_per_gpu": n, "global_boards": n * world,
                        "env_steps_per_launch": n * k, "replay_rows": n * k,
+                       "rank_boards": ranges,
                        "parallelism": f"dp{world} (boards sharded, no collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": rec["hbm_bytes_per_launch"] if rec else None,
-                         "traffic_source": os.path.relpath(PMC_FILE, ROOT) if rec else None,
-                         "kernel": "k_rollout_lean (g2048_env_rollout: ring in one buffer window, auto-reset, no episode log)",
-                         "bytes_per_step": ROLLOUT_BYTES,
-                         "bytes_per_launch": ROLLOUT_BYTES * n * k,
-                         "launch_us": launch_s * 1e6,
-                         "settle_ms": ro["settle_ms"],
-                         "issue": rec.get("issue") if rec else None},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
+        if hbm64:
+            line["rollout_64k_hbm"] = hbm64
         if ksweep:
             line["rollout_k_sweep"] = ksweep
         if large:

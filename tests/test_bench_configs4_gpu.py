@@ -31,6 +31,11 @@ def test_bench_configs4_eight_ranks_on_one_gpu():
     assert rec["n_gpus"] == 8
     assert rec["config"]["global_boards"] == 8 * 65536 == 524288
     assert rec["value"] > 0 and rec["scaling"] == "weak"
+    # the ranks' global board ranges tile [0, 8 * 65536) without overlap: board g owns Philox
+    # subsequence g, so no two ranks share one
+    ranges = sorted(tuple(r) for r in rec["config"]["rank_boards"])
+    assert len(ranges) == 8 and all(n == 65536 for _, n in ranges)
+    assert [o for o, _ in ranges] == [r * 65536 for r in range(8)]
     for dt in ("fp64", "fp32"):
         L = rec["learner"][f"conv.{dt}"]
         assert L["path"] == "fused HIP kernels", L

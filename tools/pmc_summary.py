@@ -7,7 +7,8 @@ Units: KB.  Infinity-Cache hits are counted, so at 64k boards (the working set f
 256 MiB cache) the numbers are memory-side traffic, not HBM-only; the 4M-board rows are past it.
 Issue counters (one SQ pass): per wave and env step, VALU / SALU instructions and the wave's
 cycles (quad-cycles, as SQ reports them); issue_util = (VALU + SALU active) / wave cycles.
-Usage: pmc_summary.py <out.json> <pass-dir> [<pass-dir> ...]"""
+Usage: pmc_summary.py <out.json> <pass-dir>[:suffix] [...]  (a suffix is appended to the keys of
+that pass, e.g. k_rollout@65536x64 + "r8" for the ring of 8 launches' rows)."""
 import csv
 import glob
 import json
@@ -31,7 +32,8 @@ def kernel_key(name: str, grid: int):
 
 def load(dirs):
     vals = defaultdict(lambda: defaultdict(list))  # key -> counter -> [per dispatch]
-    for d in dirs:
+    for spec in dirs:
+        d, _, suffix = spec.partition(":")
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             per = defaultdict(float)  # (dispatch, counter) -> summed over dimensions
             meta = {}
@@ -40,6 +42,7 @@ def load(dirs):
                 key = kernel_key(r["Kernel_Name"], grid)
                 if key is None:
                     continue
+                key += suffix
                 did = r.get("Dispatch_Id") or r.get("Correlation_Id")
                 per[(did, r["Counter_Name"])] += float(r["Counter_Value"])
                 meta[did] = key
@@ -48,9 +51,24 @@ def load(dirs):
     return vals
 
 
+def provenance() -> str:
+    import socket
+    import subprocess
+    import time
+    gpu = ""
+    try:
+        out = subprocess.run(["rocm-smi", "--showproductname"], capture_output=True, text=True,
+                             timeout=30).stdout
+        gpu = next((l.split(":")[-1].strip() for l in out.splitlines() if "Card Series" in l), "")
+    except Exception:
+        pass
+    return (f"rocprofv3 --pmc passes (tools/gpu_pmc.sh) on {socket.gethostname()} {gpu}, "
+            f"{time.strftime('%Y-%m-%d %H:%M UTC', time.gmtime())}")
+
+
 def main(out_path, *dirs):
     vals = load(dirs)
-    res = {}
+    res = {"_provenance": provenance()}
     for key in sorted(vals):
         c = {cn: statistics.median(v) for cn, v in vals[key].items()}
         rec = {"dispatches": max(len(v) for v in vals[key].values())}
@@ -58,7 +76,7 @@ def main(out_path, *dirs):
             rec.update(fetch_kb_raw=c["FETCH_SIZE"], write_kb=c["WRITE_SIZE"],
                        hbm_bytes_per_launch=(2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
         if "SQ_WAVES" in c and c["SQ_WAVES"] > 0:
-            steps = int(key.split("x")[1]) if key.startswith("k_rollout") else 1
+            steps = int(key.split("x")[1].rstrip("r0123456789") or 1) if key.startswith("k_rollout") else 1
             # (k_rollout_ws: SQ_WAVES counts the compute and the store waves)
             per = lambda n: c.get(n, 0.0) / c["SQ_WAVES"] / steps  # noqa: E731
             rec["issue"] = {
