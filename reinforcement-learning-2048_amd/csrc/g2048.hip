@@ -1668,8 +1668,10 @@ int g2048_replay_wrap(g2048_replay** out, int64_t capacity, int device_id, uint8
 int g2048_replay_create(g2048_replay** out, int64_t capacity, int device_id, void* stream) {
     if (!out || capacity <= 0) return fail(G2048_EINVAL, "replay_create: need capacity > 0");
     DeviceGuard g(device_id);
-    // one allocation, 256-byte aligned sections: s | s2 | r | a | d | count
-    auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
+    // one allocation, 256-byte aligned sections: s | s2 | r | a | d | count, each one
+    // G2048_REPLAY_SECTION_PAD bytes further (include/g2048.h: the HBM channel spread of the
+    // five store streams)
+    auto up = [](int64_t x) { return ((x + 255) & ~(int64_t)255) + G2048_REPLAY_SECTION_PAD; };
     const int64_t o_s2 = up(16 * capacity), o_r = o_s2 + up(16 * capacity);
     const int64_t o_a = o_r + up(4 * capacity), o_d = o_a + up(capacity);
     const int64_t o_c = o_d + up(capacity), total = o_c + 256;

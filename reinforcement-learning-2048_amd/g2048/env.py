@@ -351,11 +351,13 @@ class ReplayBuffer:
         self.capacity = int(capacity)
         c = self.capacity
         if sections is None:
-            # one allocation, 256-byte aligned sections s | s2 | r | a | d | count (as
-            # g2048_replay_create lays them out): the rollout's ring stores then always take the
-            # one-descriptor buffer path (sections within 4 GiB), whereas separately allocated
-            # tensors land wherever the allocator puts them
-            up = lambda x: (x + 255) // 256 * 256  # noqa: E731
+            # one allocation, 256-byte aligned sections s | s2 | r | a | d | count, each
+            # G2048_REPLAY_SECTION_PAD bytes further (as g2048_replay_create lays them out): the
+            # rollout's ring stores then always take the one-descriptor buffer path (sections
+            # within 4 GiB), whereas separately allocated tensors land wherever the allocator
+            # puts them; the pad keeps power-of-two capacities from putting the five store
+            # streams on the same HBM channels (include/g2048.h)
+            up = lambda x: (x + 255) // 256 * 256 + N.REPLAY_SECTION_PAD  # noqa: E731
             o_s2 = up(16 * c)
             o_r = o_s2 + up(16 * c)
             o_a = o_r + up(4 * c)

@@ -35,6 +35,16 @@ def test_library_exports_every_declared_symbol():
     assert exported == _declared()
 
 
+def test_python_mirror_constants_match_header():
+    """The Python host side lays out ReplayBuffer like g2048_replay_create: same section pad."""
+    import g2048._native as N
+
+    src = open(HEADER).read()
+    pad = int(re.search(r"#define G2048_REPLAY_SECTION_PAD (\d+)", src).group(1))
+    assert N.REPLAY_SECTION_PAD == pad and pad % 256 == 0 and pad % 4096 != 0
+    assert int(re.search(r"#define G2048_ABI_VERSION (\d+)", src).group(1)) == N.ABI_VERSION
+
+
 def test_no_cpu_fallback():
     """The product path fails loudly without a GPU instead of falling back."""
     import torch

@@ -57,11 +57,12 @@ class LibReplay:
         N.load().g2048_replay_destroy(self.handle)
 
 
-def offset_replay(capacity, dev, offset):
+def offset_replay(capacity, dev, offset, pad=0):
     """ReplayBuffer sections carved from one torch allocation starting `offset` bytes past a
-    2 MiB boundary (the default layout otherwise)."""
+    2 MiB boundary (the default layout otherwise); `pad` extra bytes after each section (breaks
+    the power-of-two distances between the sections at power-of-two capacities)."""
     c = capacity
-    up = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    up = lambda x: (x + 255) // 256 * 256 + pad  # noqa: E731
     o_s2 = up(16 * c)
     o_r = o_s2 + up(16 * c)
     o_a = o_r + up(4 * c)
@@ -113,10 +114,32 @@ def main():
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--launches", type=int, default=200)
     p.add_argument("--variants", default="torch/torch,torch/lib,lib/lib,torch/torch+,torch/fresh")
+    p.add_argument("--rings", type=int, default=0,
+                   help="mode 2: this many rings allocated up front (default layout, then padded "
+                        "layouts), one env, each ring timed once per round: is the time a property "
+                        "of the allocation?")
+    p.add_argument("--ring-mult", type=int, default=1, help="mode 2: ring of this many launches' rows")
+    p.add_argument("--pads", default="", help="mode 2 with these section pads (comma list)")
     a = p.parse_args()
     dev = torch.device("cuda", 0)
     n, k = a.boards, a.k
     algo = 38.0 * n * k
+    if a.rings or a.pads:
+        env = g2048.VecEnv2048(n, seed=0x2048, device=dev)
+        pads = ([int(x) for x in a.pads.split(",")] if a.pads else
+                [0] * (a.rings // 2) + [4096 * (j + 1) + 256 * j for j in range(a.rings - a.rings // 2)])
+        rings = [offset_replay(n * k * a.ring_mult, dev, 0, pad) for pad in pads]
+        for rnd in range(a.rounds):
+            for j, rb in enumerate(rings):
+                fn = lambda: env.rollout(k, replay=rb)  # noqa: E731
+                g = capture(fn, 20)
+                g.replay()
+                t = time_graph(g, 10, 20.0) / 200
+                env.check_errors()
+                print(f"round {rnd} ring {j} pad {pads[j]:6d} base {rb.s.data_ptr():#x} "
+                      f"{t * 1e6:8.1f} us ({algo / t / 8e12:.3f})", flush=True)
+                del g
+        return
     for rnd in range(a.rounds):
         for v in a.variants.split(","):
             ev, rv = v.split("/")
