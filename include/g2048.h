@@ -405,9 +405,15 @@ G2048_API int g2048_dense64_update_f64(const g2048_dense64_params_f64* online,
  * in float64, the reference's precision (`.double()`, :28): the arguments, step_dev protocol,
  * sampler, Bellman target (gamma the float32 torch uses), MSELoss(sum), gradient order and
  * Adam / target-sync semantics of g2048_dense64_update_f64, for Conv2d(1,64,2) -> ReLU ->
- * Conv2d(64,64,2) -> ReLU -> Flatten -> Linear(256,64) -> ReLU -> Linear(64,4).  Five launches:
- * operand packing, targets, two train launches, reduction + Adam.  grad_out: f64[33476] in
- * torch parameter order.  workspace: f64[g2048_convnet_update_f64_workspace(B)]. */
+ * Conv2d(64,64,2) -> ReLU -> Flatten -> Linear(256,64) -> ReLU -> Linear(64,4).  Four launches:
+ * targets, two train launches, reduction + Adam.  grad_out: f64[33476] in torch parameter order.
+ * workspace: f64[g2048_convnet_update_f64_workspace(B)]; it starts with both nets' weights packed
+ * in f64-MFMA operand order.  With Adam folded in (exp_avg and exp_avg_sq given) the update reads
+ * those packed operands and re-packs the weights it writes (the online net every update, the
+ * target net on a sync), so the caller packs them with g2048_convnet_pack_f64 once after
+ * allocating the workspace and again after changing either net's weights any other way.  A
+ * gradient-only update (no Adam state: a data-parallel learner applies Adam after the
+ * all-reduce) packs at its start. */
 typedef struct {
     double *w1, *b1;       /* Conv2d(1, 64, 2)  */
     double *w2, *b2;       /* Conv2d(64, 64, 2) */
@@ -416,6 +422,10 @@ typedef struct {
 } g2048_convnet_params_f64;
 
 G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch);
+/* Pack both nets' conv2 / fc1 weights into the head of an update workspace (one launch). */
+G2048_API int g2048_convnet_pack_f64(const g2048_convnet_params_f64* online,
+                                     const g2048_convnet_params_f64* target,
+                                     double* workspace_dev, void* stream);
 G2048_API int g2048_convnet_update_f64(const g2048_convnet_params_f64* online,
                                        const g2048_convnet_params_f64* target, g2048_replay* rb,
                                        const int64_t* idx_in_dev, int64_t batch, uint64_t seed,

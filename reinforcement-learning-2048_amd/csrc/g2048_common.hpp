@@ -59,15 +59,30 @@ __device__ __forceinline__ float adam_apply(const AdamCoef& c, float g, float* m
 // scalars as torch forms them in double: m.lerp_(g, 1 - b1); v.mul_(b2).addcmul_(g, g, 1 - b2);
 // denom = v.sqrt() / sqrt(1 - b2^t) + eps; p.addcdiv_(m, denom, -lr / (1 - b1^t)).  Shared by the
 // float64 reductions (g2048_learn64.hip, g2048_conv64.hip) and g2048_adam_step_sync_f64.
-__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
-                                         double g, double& m, double& v, double p) {
+// The step's two scalars (lr / (1 - b1^t), sqrt(1 - b2^t)): two f64 pow calls, so a kernel that
+// updates many elements per lane forms them once, off its critical path.
+struct Adam64Coef {
+    double step_size, bc2_sqrt;
+};
+
+__device__ __forceinline__ Adam64Coef adam64_coef(double t, double lr, double b1, double b2) {
 #pragma clang fp contract(off)
-    const double step_size = lr / (1.0 - pow(b1, t));
-    const double bc2_sqrt = sqrt(1.0 - pow(b2, t));
+    return Adam64Coef{lr / (1.0 - pow(b1, t)), sqrt(1.0 - pow(b2, t))};
+}
+
+__device__ __forceinline__ double adam64_apply(const Adam64Coef& c, double b1, double b2,
+                                               double eps, double g, double& m, double& v,
+                                               double p) {
+#pragma clang fp contract(off)
     m = m + (1.0 - b1) * (g - m);
     v = v * b2 + (1.0 - b2) * g * g;
-    const double denom = sqrt(v) / bc2_sqrt + eps;
-    return p + (-step_size) * (m / denom);
+    const double denom = sqrt(v) / c.bc2_sqrt + eps;
+    return p + (-c.step_size) * (m / denom);
+}
+
+__device__ __forceinline__ double adam64(double t, double lr, double b1, double b2, double eps,
+                                         double g, double& m, double& v, double p) {
+    return adam64_apply(adam64_coef(t, lr, b1, b2), b1, b2, eps, g, m, v, p);
 }
 
 }  // namespace g2048

@@ -1,12 +1,16 @@
 // g2048_conv64.hip -- the Double-DQN update of the reference conv Q-net in float64, the
 // reference's precision (src/configs/double_dqn_conv.py:19-28 `.double()`; BASELINE configs[3]):
-// train_step (src/dqn_lib.py:119-164) + the target sync (:227-228) as five launches:
-//   1. pack      the big weight matrices of both nets into f64-MFMA operand order (B fragments);
-//   2. targets   per 16-row tile: sampler, Q_online(s') and Q_target(s') -> y (Double or vanilla)
-//   3. train A   per tile: Q_online(s) -> MSE(sum) -> fc2 / fc1 gradients, dH2 -> dZ2 (workspace)
-//   4. train B   per tile: conv1 recomputed, conv2 / conv1 gradients from dZ2
-//   5. reduce    fixed-order sum of the per-workgroup gradient slabs + torch's Adam in float64
-//                (+ the target sync on the device update counter)
+// train_step (src/dqn_lib.py:119-164) + the target sync (:227-228) as four launches:
+//   1. targets   per 16-row tile: sampler, Q_online(s') and Q_target(s') -> y (Double or vanilla)
+//   2. train A   per tile: Q_online(s) -> MSE(sum) -> fc2 / fc1 gradients, dH2 -> dZ2 (workspace)
+//   3. train B   per tile: conv1 recomputed, conv2 / conv1 gradients from dZ2
+//   4. reduce    fixed-order sum of the per-workgroup gradient slabs + torch's Adam in float64
+//                (+ the target sync on the device update counter), and the updated weights
+//                re-packed into f64-MFMA operand order (B fragments) for the next update: the
+//                online net's every update, the target net's when the sync fires
+// The packed operands live at the start of the workspace; g2048_convnet_pack_f64 (k_pack) writes
+// them from the weights as given.  Without Adam (grad_out only: a data-parallel learner applies
+// Adam after the all-reduce) the update packs at its start instead.
 // The GEMM-shaped layers (conv2 as im2col [rows = 16 boards x 4 positions] x [256 = tap x c] x
 // [64 o], fc1, and their backward products) run on v_mfma_f64_16x16x4_f64; conv1, fc2 and the
 // element-wise work on VALU.  Every sum has a fixed order, so an update is run-to-run bitwise
@@ -49,6 +53,8 @@ constexpr int O_U_ON = 0, O_F1_ON = PACKU, O_U_TG = PACKU + PACK, O_F1_TG = 2 * 
               O_F1B = 2 * PACKU + 2 * PACK, O_UB = 2 * PACKU + 3 * PACK,
               PACK_ALL = 3 * PACKU + 3 * PACK, PACK_FWD = PACKU + PACK;
 static_assert(PACK_ALL % 256 == 0 && PACK_FWD % 256 == 0, "pack grid");
+// workspace: packed operands | the next-step word (+ pad to 256 B) | slabs | dZ2 rows
+constexpr int WS_STEP = PACK_ALL, WS_SLAB = PACK_ALL + 32;
 
 // Phase ticks (s_memtime deltas of thread 0 of workgroup 0, charged to the phase that ENDS at the
 // marker), compiled in only for kernel tuning (tools/prof_conv64.hip).
@@ -352,18 +358,35 @@ struct PackArgs {
 
 // (G g G^T)[xi] of g = W2[o][c][.][.] for lane l of k-step s of wave w:
 //   forward  (U):  o = 16w + lr, c = 4s + lk     backward (UB): c = 16w + lr, o = 4s + lk
+// (G g G^T)[xi] of the 2x2 kernel g (g[ty * 2 + tx]); k_pack and the reduce's re-pack share it
+__device__ __forceinline__ double wino_u(double g0, double g1, double g2, double g3, int xi) {
+    const int xy = xi / 3, xx = xi % 3;
+    const double r0 = xy == 0 ? g0 : xy == 1 ? g0 + g2 : g2;
+    const double r1 = xy == 0 ? g1 : xy == 1 ? g1 + g3 : g3;
+    return xx == 0 ? r0 : xx == 1 ? r0 + r1 : r1;
+}
+
+// packed indices of the operands of one weight element (the inverse maps of k_pack's)
+__device__ __forceinline__ int idx_u(int o, int c, int xi) {  // U: o = 16w + lr, c = 4s + lk
+    return (((o >> 4) * 9 + xi) * 16 + (c >> 2)) * 64 + (c & 3) * 16 + (o & 15);
+}
+__device__ __forceinline__ int idx_ub(int o, int c, int xi) {  // UB: c = 16w + lr, o = 4s + lk
+    return (((c >> 4) * 9 + xi) * 16 + (o >> 2)) * 64 + (o & 3) * 16 + (c & 15);
+}
+__device__ __forceinline__ int idx_pf1(int j, int k) {  // Pf1: j = 16w + lr, k = 4s + lk
+    return ((j >> 4) * 64 + (k >> 2)) * 64 + (k & 3) * 16 + (j & 15);
+}
+__device__ __forceinline__ int idx_f1b(int j, int k) {  // F1B: k = 64w + 16cb + lr, j = 4s + lk
+    return (((k >> 6) * 4 + ((k >> 4) & 3)) * 16 + (j >> 2)) * 64 + (j & 3) * 16 + (k & 15);
+}
+
 template <bool BWD>
 __device__ __forceinline__ double pack_u(const double* w2, int i) {
     const int l = i & 63, lr = l & 15, lk = l >> 4;
     const int s = (i >> 6) & 15, xi = (i >> 10) % 9, w = (i >> 10) / 9;
     const int o = BWD ? 4 * s + lk : 16 * w + lr, c = BWD ? 16 * w + lr : 4 * s + lk;
     const double* g = w2 + o * 256 + c * 4;  // g[ty * 2 + tx]
-    const int xy = xi / 3, xx = xi % 3;
-    double r[2];
-#pragma unroll
-    for (int tx = 0; tx < 2; ++tx)
-        r[tx] = xy == 0 ? g[tx] : xy == 1 ? g[tx] + g[2 + tx] : g[2 + tx];
-    return xx == 0 ? r[0] : xx == 1 ? r[0] + r[1] : r[1];
+    return wino_u(g[0], g[1], g[2], g[3], xi);
 }
 
 __device__ __forceinline__ double pack_f1(const double* f1, int i) {
@@ -790,14 +813,18 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         const double* v2 = red + 5 * 256 + c;  // threads c, c + 64, c + 128, c + 192
         sl[P_B2 + c] = ((v2[0] + v2[64]) + v2[128]) + v2[192];
     }
+    // a lane's four taps of one (o, c) are 32 contiguous bytes (torch order o, c, tap): two
+    // 16-byte stores, so 16 lanes write 512 B in a row (per-tap 8-byte stores at a 32-byte stride
+    // took 2.4x the time of train A's slab write)
 #pragma unroll
-    for (int tap = 0; tap < 4; ++tap)
+    for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                sl[P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4 + tap] =
-                    gw2[tap * 4 + cb][r];
+        for (int r = 0; r < 4; ++r) {
+            double2* dst = reinterpret_cast<double2*>(
+                sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
+            dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
+            dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
+        }
     CPHASE(19);
 }
 
@@ -817,6 +844,7 @@ struct RedArgs {
     double *m, *v;
     double lr, b1, b2, eps;
     int adam;
+    double* pk;  // the packed operands to re-pack after Adam (null: none)
 };
 
 // Block = 128 positions (two per lane, 16-byte loads) x RW waves: wave w sums slabs w, w + RW,
@@ -832,6 +860,7 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
     double am[2] = {0.0, 0.0}, av[2] = {0.0, 0.0}, ap[2] = {0.0, 0.0};
     int kk[2] = {0, 0};
     unsigned long long tt = 0;
+    g2048::Adam64Coef cf{0.0, 0.0};
     if (A.adam && wave == 0) {
         tt = *A.step_next;
 #pragma unroll
@@ -849,12 +878,14 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
     double2 r = make_double2(0.0, 0.0);
     if (pos <= P_N) {
         double2 v[MAX_WG / RW];
+        // (wave 0: Adam's step scalars are formed while its slab loads are in flight)
 #pragma unroll
         for (int k = 0; k < MAX_WG / RW; ++k) {
             const int g = wave + RW * k;
             v[k] = g < A.nslab ? *reinterpret_cast<const double2*>(A.slab + (int64_t)g * SLAB + pos)
                                : make_double2(0.0, 0.0);
         }
+        if (A.adam && wave == 0) cf = g2048::adam64_coef((double)tt, A.lr, A.b1, A.b2);
 #pragma unroll
         for (int k = 0; k < MAX_WG / RW; ++k) {
             r.x += v[k].x;
@@ -870,6 +901,8 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             sum.y += part[k][lane].y;
         }
         const double sums[2] = {sum.x, sum.y};
+        const bool sync = A.sync_every && tt % A.sync_every == 0ull;
+        double np[2] = {0.0, 0.0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int ps = pos + h;
@@ -882,12 +915,43 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             if (A.adam) {
                 const int k = kk[h];
                 double m = am[h], v = av[h];
-                const double np =
-                    g2048::adam64((double)tt, A.lr, A.b1, A.b2, A.eps, sums[h], m, v, ap[h]);
+                np[h] = g2048::adam64_apply(cf, A.b1, A.b2, A.eps, sums[h], m, v, ap[h]);
                 A.m[ps] = m;
                 A.v[ps] = v;
-                A.p[k][ps - base[k]] = np;
-                if (A.sync_every && tt % A.sync_every == 0ull) A.tp[k][ps - base[k]] = np;
+                A.p[k][ps - base[k]] = np[h];
+                if (sync) A.tp[k][ps - base[k]] = np[h];
+            }
+        }
+        if (A.pk) {  // re-pack the updated weights (wave-uniform: every lane joins the shuffles)
+            // conv2.weight: lane pair (2i, 2i + 1) holds the four taps of one (o, c) -- the block's
+            // 128 positions start at a multiple of 4, as does P_W2; the even lane writes the
+            // forward operands U (and the target's on a sync), the odd lane the backward UB
+            const double x0 = __shfl_xor(np[0], 1), x1 = __shfl_xor(np[1], 1);
+            if (pos >= P_W2 && pos < P_B2) {
+                const int oc = (pos - P_W2) >> 2, o = oc >> 6, c = oc & 63;
+                const bool ev = (lane & 1) == 0;
+                const double g0 = ev ? np[0] : x0, g1 = ev ? np[1] : x1;
+                const double g2 = ev ? x0 : np[0], g3 = ev ? x1 : np[1];
+#pragma unroll
+                for (int xi = 0; xi < 9; ++xi) {
+                    const double u = wino_u(g0, g1, g2, g3, xi);
+                    if (ev) {
+                        A.pk[O_U_ON + idx_u(o, c, xi)] = u;
+                        if (sync) A.pk[O_U_TG + idx_u(o, c, xi)] = u;
+                    } else {
+                        A.pk[O_UB + idx_ub(o, c, xi)] = u;
+                    }
+                }
+            }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {  // fc1.weight: forward and backward operands
+                const int ps = pos + h;
+                if (ps >= P_F1 && ps < P_FB1) {
+                    const int j = (ps - P_F1) >> 8, k = (ps - P_F1) & 255;
+                    A.pk[O_F1_ON + idx_pf1(j, k)] = np[h];
+                    A.pk[O_F1B + idx_f1b(j, k)] = np[h];
+                    if (sync) A.pk[O_F1_TG + idx_pf1(j, k)] = np[h];
+                }
             }
         }
     }
@@ -998,6 +1062,28 @@ static bool params_ok(const g2048_convnet_params_f64* n) {
     return n && n->w1 && n->b1 && n->w2 && n->b2 && n->fc1_w && n->fc1_b && n->fc2_w && n->fc2_b;
 }
 
+static void launch_pack(const g2048_convnet_params_f64* online,
+                        const g2048_convnet_params_f64* target, double* pk, hipStream_t st) {
+    PackArgs P;
+    P.w2_on = online->w2;
+    P.f1_on = online->fc1_w;
+    P.w2_tg = target->w2;
+    P.f1_tg = target->fc1_w;
+    P.out = pk;
+    hipLaunchKernelGGL(k_pack, dim3(PACK_ALL / NT), dim3(NT), 0, st, P);
+}
+
+extern "C" G2048_API int g2048_convnet_pack_f64(const g2048_convnet_params_f64* online,
+                                                const g2048_convnet_params_f64* target,
+                                                double* workspace, void* stream) {
+    if (!params_ok(online) || !params_ok(target) || !workspace)
+        return g2048_fail(G2048_EINVAL, "convnet_pack_f64: NULL argument");
+    launch_pack(online, target, workspace, reinterpret_cast<hipStream_t>(stream));
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK
+                           : g2048_fail(G2048_EHIP, "convnet_pack_f64: %s", hipGetErrorString(e));
+}
+
 extern "C" G2048_API int g2048_convnet_forward_f64(const g2048_convnet_params_f64* p,
                                                    const uint8_t* rows, const int64_t* idx,
                                                    int64_t n, double* q_out, double* workspace,
@@ -1045,8 +1131,8 @@ extern "C" G2048_API int g2048_convnet_forward_greedy_f64(
 extern "C" G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch) {
     if (batch <= 0) return 0;
     const int64_t tiles = (batch + TB - 1) / TB;
-    // slabs | dZ2 rows | 6 packed matrices | the next-step word
-    return (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + PACK_ALL + 2;
+    // the packed operands | the next-step word (+ pad) | slabs | dZ2 rows
+    return WS_SLAB + (int64_t)grid_of(batch) * SLAB + tiles * TB * 256;
 }
 
 extern "C" G2048_API int g2048_convnet_update_f64(
@@ -1068,20 +1154,15 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     uint64_t* count = nullptr;
     if (g2048_replay_views(rb, &s, &s2, &a, &r, &d, &count) != G2048_OK) return G2048_EINVAL;
     const int grid = grid_of(batch);
-    const int64_t tiles = (batch + TB - 1) / TB;
-    double* slab = workspace;
+    double* pk = workspace;
+    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(workspace + WS_STEP);
+    double* slab = workspace + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
-    double* pk = dz2 + tiles * TB * 256;
-    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(pk + PACK_ALL);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
-    PackArgs P;
-    P.w2_on = online->w2;
-    P.f1_on = online->fc1_w;
-    P.w2_tg = target->w2;
-    P.f1_tg = target->fc1_w;
-    P.out = pk;
-    hipLaunchKernelGGL(k_pack, dim3(PACK_ALL / NT), dim3(NT), 0, st, P);
+    // with Adam folded in, the packed operands are current (g2048_convnet_pack_f64 or the
+    // previous update's reduce); a gradient-only update packs first (Adam runs elsewhere)
+    if (!adam) launch_pack(online, target, pk, st);
 
     Ring R;
     R.s = reinterpret_cast<const uint4*>(s);
@@ -1146,6 +1227,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     D.b2 = beta2;
     D.eps = eps;
     D.adam = adam ? 1 : 0;
+    D.pk = adam ? pk : nullptr;
     hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 127) / 128), dim3(64 * RW), 0, st, D);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK

@@ -79,6 +79,7 @@ SIGNATURES = {
     "g2048_adam_step_sync_f64": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
                                         _vp, _u64, _vp]),
     "g2048_convnet_update_f64_workspace": (_i64, [_i64]),
+    "g2048_convnet_pack_f64": (_int, [_vp, _vp, _vp, _vp]),
     "g2048_convnet_forward_f64": (_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp]),
     "g2048_convnet_forward_greedy_f64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp]),
     "g2048_convnet_update_f64": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp,

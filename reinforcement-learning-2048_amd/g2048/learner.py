@@ -215,12 +215,19 @@ class DQNLearner:
                 self._adam.exp_avg_sq.copy_(adam0[1])
                 self.step_dev.copy_(step0)
 
+    def before_replay(self) -> None:
+        """Host-side checks a captured update relies on: the float64 conv update's packed weight
+        operands must match the weights (re-packed when torch modified a parameter)."""
+        if self._upd is not None and hasattr(self._upd, "ensure_packed"):
+            self._upd.ensure_packed()
+
     def update(self) -> torch.Tensor:
         """One Double-DQN update (intended order zero_grad -> backward -> step). Returns the loss
         tensor of this update (device, no sync)."""
         if self.graph:
             if self._graphs is None:
                 self._capture()
+            self.before_replay()
             g1, g2 = self._graphs
             g1.replay()
             if g2 is not None:
@@ -397,6 +404,7 @@ class Trainer:
                     L._compute_grads()
                     L._apply()
             self._loop_graph = g
+        L.before_replay()
         self._loop_graph.replay()
         L.updates += self.updates_per_step
 
@@ -414,6 +422,7 @@ class Trainer:
                 L._apply()
             self._loop_graph = (ga, gb)
         ga, gb = self._loop_graph
+        L.before_replay()
         ga.replay()
         L._allreduce()
         gb.replay()

@@ -332,23 +332,47 @@ class Dense64Update64:
 
 
 class ConvUpdate64:
-    """One whole Double-DQN update of a float64 conv net (the reference's precision) in five
-    launches (g2048_convnet_update_f64): operand packing, targets, two train launches and the
-    reduction with Adam (Adam64) applied in place; the same call and step_dev protocol as
-    Dense64Update64."""
+    """One whole Double-DQN update of a float64 conv net (the reference's precision) in four
+    launches (g2048_convnet_update_f64): targets, two train launches and the reduction with Adam
+    (Adam64) applied in place, which also re-packs the weights it writes into the workspace's
+    f64-MFMA operand order; the same call and step_dev protocol as Dense64Update64.
+
+    The packed operands must match the weights: they are packed here at construction, and
+    ensure_packed() re-packs them when torch changed a parameter of either net since (every
+    in-place torch op bumps the tensor's version counter; the fused kernels write through raw
+    pointers and keep the packs current themselves).  __call__ runs it outside graph capture;
+    graph replays call it first (DQNLearner.update, Trainer)."""
 
     def __init__(self, model, target, batch: int, adam: Adam64 | None = None):
         if kind64_of(model) != "conv" or kind64_of(target) != "conv":
             raise TypeError("ConvUpdate64 needs fp64 Conv2048 online and target nets")
-        self.on = N.ConvNetParams(*[t.data_ptr() for t in
-                                    _tensors(model, _CONV_ORDER, torch.float64)])
-        self.tg = N.ConvNetParams(*[t.data_ptr() for t in
-                                    _tensors(target, _CONV_ORDER, torch.float64)])
+        self._params = (_tensors(model, _CONV_ORDER, torch.float64)
+                        + _tensors(target, _CONV_ORDER, torch.float64))
+        self.on = N.ConvNetParams(*[t.data_ptr() for t in self._params[:8]])
+        self.tg = N.ConvNetParams(*[t.data_ptr() for t in self._params[8:]])
         self.batch = int(batch)
         self.adam = adam
         dev = next(model.parameters()).device
         n = N.load().g2048_convnet_update_f64_workspace(self.batch)
         self.workspace = torch.empty(n, dtype=torch.float64, device=dev)
+        self._packed_at = None
+        self.ensure_packed()
+
+    def _versions(self):
+        return tuple(t._version for t in self._params)
+
+    def ensure_packed(self, force: bool = False) -> bool:
+        """Pack both nets into the workspace if torch modified a parameter since the last pack
+        (or force).  Stream-ordered; returns whether it packed."""
+        v = self._versions()
+        if not force and v == self._packed_at:
+            return False
+        N.check(N.load().g2048_convnet_pack_f64(C.byref(self.on), C.byref(self.tg),
+                                                N.ptr(self.workspace),
+                                                N.stream_of(self.workspace.device)),
+                "g2048_convnet_pack_f64")
+        self._packed_at = v
+        return True
 
     def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
                  idx_in=None, grad_out=None, loss_out=None):
@@ -358,6 +382,8 @@ class ConvUpdate64:
             raise TypeError("y_out must be float64")
         if self.adam is None and grad_out is None:
             raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        if not torch.cuda.is_current_stream_capturing():
+            self.ensure_packed()
         a = self.adam
         m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
         lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)

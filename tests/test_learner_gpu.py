@@ -260,6 +260,13 @@ def test_fused_f64_equals_torch_path(G, net, double_dqn):
     b.loss_fn = None  # ... run with the MSE(sum) loss, fed the fused learner's rows
     b.sampler = lambda B, r: rows
     assert not b.fused
+    # change a's weights through torch after construction: the fused conv update must re-pack
+    # its operands (ConvUpdate64.ensure_packed, tensor version counters), or its loss differs
+    with torch.no_grad():
+        for p in a.model.parameters():
+            p.mul_(0.9)
+        for p in a.target.parameters():
+            p.mul_(1.1)
     b.model.load_state_dict(a.model.state_dict())
     b.target.load_state_dict(a.target.state_dict())
     for k in range(3):

@@ -2,7 +2,9 @@
 // ticks of its targets / train kernels (s_memtime deltas of thread 0 of workgroup 0, charged to
 // the phase that ENDS at the marker), built only for kernel tuning:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_conv64.hip -o tools/prof_conv64
+#ifndef G2048_NO_PHASE_PROF
 #define G2048_PHASE_PROF 1
+#endif
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -68,10 +70,10 @@ int main(int argc, char** argv) {
     (void)hipMalloc(&ws, nws * 8);
     const int grid = grid_of(B);
     const int64_t tiles = (B + TB - 1) / TB;
-    double* slab = ws;
+    double* pk = ws;
+    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(ws + WS_STEP);
+    double* slab = ws + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
-    double* pk = dz2 + tiles * TB * 256;
-    unsigned long long* step_next = reinterpret_cast<unsigned long long*>(pk + PACK_ALL);
 
     PackArgs P{w[0][2], w[0][4], w[1][2], w[1][4], pk};
     Ring R{reinterpret_cast<const uint4*>(s), reinterpret_cast<const uint4*>(s2), a, d, r, count};
@@ -117,6 +119,7 @@ int main(int argc, char** argv) {
     D.b2 = 0.999;
     D.eps = 1e-8;
     D.adam = 1;
+    D.pk = pk;  // the reduce re-packs (k_pack is timed separately: the update no longer runs it)
 
     auto launch = [&](int k) {
         switch (k) {
@@ -132,8 +135,10 @@ int main(int argc, char** argv) {
     for (int it = 0; it < 3; ++it)
         for (int k = 0; k < 5; ++k) launch(k);
     (void)hipDeviceSynchronize();
+#ifdef G2048_PHASE_PROF
     unsigned long long zero[32] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_cphase), zero, sizeof(zero));
+#endif
     hipEvent_t ev[6];
     for (int i = 0; i < 6; ++i) (void)hipEventCreate(&ev[i]);
     float tk[5] = {0, 0, 0, 0, 0};
@@ -152,10 +157,31 @@ int main(int argc, char** argv) {
         }
     }
     printf("B=%d grid=%d  pack %.2f  targets %.2f  train_a %.2f  train_b %.2f  reduce %.2f  "
-           "(us)  sum %.2f\n", B, grid, tk[0], tk[1], tk[2], tk[3], tk[4],
-           tk[0] + tk[1] + tk[2] + tk[3] + tk[4]);
-    unsigned long long ph[32];
+           "(us)  update (no pack) %.2f\n", B, grid, tk[0], tk[1], tk[2], tk[3], tk[4],
+           tk[1] + tk[2] + tk[3] + tk[4]);
+    {  // the reduce alone, back to back (slabs resident, nothing dirty from the train kernels)
+        float ms;
+        (void)hipEventRecord(ev[0], nullptr);
+        for (int it = 0; it < N; ++it) launch(4);
+        (void)hipEventRecord(ev[1], nullptr);
+        (void)hipEventSynchronize(ev[1]);
+        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+        printf("reduce alone, back to back: %.2f us\n", ms * 1e3f / N);
+        (void)hipEventRecord(ev[0], nullptr);
+        for (int it = 0; it < N; ++it) {
+            launch(3);
+            (void)hipEventRecord(ev[2], nullptr);
+            launch(4);
+            (void)hipEventRecord(ev[3], nullptr);
+        }
+        (void)hipEventSynchronize(ev[3]);
+        (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
+        printf("reduce right after train_b (last pair): %.2f us\n", ms * 1e3f);
+    }
+    unsigned long long ph[32] = {0};
+#ifdef G2048_PHASE_PROF
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_cphase), sizeof(ph));
+#endif
     const double tpw = (double)N * ((tiles + grid - 1) / grid);  // tiles per workgroup x N
     const char* names[20] = {"-", "tgt sample", "stage_small", "conv1+V", "conv2 wino", "fc1",
                              "fc2", "tgt y", "A load", "A loss/dq", "A fc2 grad+dZ3",
