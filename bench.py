@@ -373,6 +373,16 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
     L.update()  # the learner's own graphs (the Trainer may run a graphed loop): captured here
     torch.cuda.synchronize()
     K = args.train_updates if dtype == "fp32" else max(args.train_updates // 4, 10)
+    # untimed updates for --settle-ms (the clock ramp, as for the rollout legs: a fp64 conv update
+    # timed right after a short warm-up reads ~160 us, sustained ~151 us)
+    if world == 1:
+        settle_ms = settle(L.update, args.settle_ms, max_calls=2000)
+    else:  # every rank must run the same number of updates (each holds a collective)
+        t0 = time.perf_counter()
+        for _ in range(int(args.settle_ms * 4)):  # ~0.25 ms per update at most here
+            L.update()
+        torch.cuda.synchronize()
+        settle_ms = (time.perf_counter() - t0) * 1e3
     upd_wall, upd_ev = timed(world, dev, L.update, K)
     K2 = max(K // 2, 1)
     loop_wall, _ = timed(world, dev, T.step, K2)
@@ -405,7 +415,7 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
             "loop_late_iter_ms": late_wall / K2 * 1e3,
             "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
             "loop_late_epsilon_mean": eps_late,
-            "batch": batch, "replay": C, "dtype": dtype, "loss": loss,
+            "batch": batch, "replay": C, "dtype": dtype, "loss": loss, "settle_ms": settle_ms,
             "params": L.n_params, "graphed_loop": T.graph, "ranks_lockstep": lockstep}
 
 
