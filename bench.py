@@ -379,7 +379,7 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
         settle_ms = settle(L.update, args.settle_ms, max_calls=2000)
     else:  # every rank must run the same number of updates (each holds a collective)
         t0 = time.perf_counter()
-        for _ in range(int(args.settle_ms * 4)):  # ~0.25 ms per update at most here
+        for _ in range(int(args.settle_ms)):  # one update per settle ms
             L.update()
         torch.cuda.synchronize()
         settle_ms = (time.perf_counter() - t0) * 1e3
