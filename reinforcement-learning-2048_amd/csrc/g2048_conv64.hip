@@ -1,10 +1,11 @@
 // g2048_conv64.hip -- the Double-DQN update of the reference conv Q-net in float64, the
 // reference's precision (src/configs/double_dqn_conv.py:19-28 `.double()`; BASELINE configs[3]):
-// train_step (src/dqn_lib.py:119-164) + the target sync (:227-228) as four launches:
-//   1. targets   per 16-row tile: sampler, Q_online(s') and Q_target(s') -> y (Double or vanilla)
-//   2. train A   per tile: Q_online(s) -> MSE(sum) -> fc2 / fc1 gradients, dH2 -> dZ2 (workspace)
-//   3. train B   per tile: conv1 recomputed, conv2 / conv1 gradients from dZ2
-//   4. reduce    fixed-order sum of the per-workgroup gradient slabs + torch's Adam in float64
+// train_step (src/dqn_lib.py:119-164) + the target sync (:227-228) as three launches:
+//   1. train A   per 16-row tile: sampler, Q_online(s') and Q_target(s') -> y (Double or
+//                vanilla), then Q_online(s) -> MSE(sum) -> fc2 / fc1 gradients, dH2 -> dZ2
+//                (workspace)
+//   2. train B   per tile: conv1 recomputed, conv2 / conv1 gradients from dZ2
+//   3. reduce    fixed-order sum of the per-workgroup gradient slabs + torch's Adam in float64
 //                (+ the target sync on the device update counter), and the updated weights
 //                re-packed into f64-MFMA operand order (B fragments) for the next update: the
 //                online net's every update, the target net's when the sync fires
@@ -417,7 +418,7 @@ __global__ __launch_bounds__(NT) void k_pack(PackArgs A) {
     A.out[e] = v;
 }
 
-// ------------------------------------------------------------------ 2. targets
+// ------------------------------------------------------------------ targets (train A's first half)
 struct TgtArgs {
     Net on, tg;
     Packed pon, ptg;
@@ -433,69 +434,6 @@ struct TgtArgs {
     unsigned long long* step_next;
 };
 
-__global__ __launch_bounds__(NT) void k_conv64_targets(TgtArgs A) {
-    __shared__ Smem M;
-    const int t = threadIdx.x;
-    const unsigned long long ep = A.idx_in ? 0ull : *A.step;
-    const unsigned long long count = A.idx_in ? 0ull : *A.R.count;
-    if (blockIdx.x == 0 && t == 0) *A.step_next = *A.step + 1ull;
-    CPHASE(-1);
-    stage_small(M.sw[0], A.on);
-    stage_small(M.sw[1], A.tg);
-    const int64_t ntiles = (A.batch + TB - 1) / TB;
-    // the sampled row of board t of a tile: index, s', r, (1 - d) * gamma (float32 in torch,
-    // src/dqn_lib.py:131); the next tile's row is fetched while the current one runs
-    uint4 s2v = make_uint4(0u, 0u, 0u, 0u);
-    double rj = 0.0;
-    float disc = 0.f;
-    auto fetch = [&](int64_t tile) {
-        s2v = make_uint4(0u, 0u, 0u, 0u);
-        rj = 0.0;
-        disc = 0.f;
-        const int64_t b = tile * TB + t;
-        if (t < TB && tile < ntiles && b < A.batch) {
-            const int64_t row =
-                A.idx_in ? A.idx_in[b] : sample_row(b, ep, count, A.seed_lo, A.seed_hi);
-            A.idx_out[b] = row;
-            s2v = A.R.s2[row];
-            rj = (double)A.R.r[row];
-            disc = (float)(1 - (int)A.R.d[row]) * A.gamma;
-        }
-    };
-    fetch(blockIdx.x);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        const int64_t b = tile * TB + t;
-        __syncthreads();  // the previous tile is done with M
-        if (t < TB) {
-            put_row(M.x + t * XS, s2v);
-            M.r[t] = rj;
-            M.disc[t] = disc;
-        }
-        fetch(tile + gridDim.x);
-        CPHASE(1);
-        // Q_online(s') (Double DQN) then Q_target(s'): one call site, so forward is inlined once
-#pragma unroll 1
-        for (int net = A.double_dqn ? 0 : 1; net < 2; ++net)
-            forward(M, M.sw[net], net ? A.ptg : A.pon, net ? M.q : M.q2);
-        CPHASE(2);
-        if (t < TB && b < A.batch) {
-            const double* qt = M.q + t * 4;
-            double next;
-            if (A.double_dqn) {
-                const double* qo = M.q2 + t * 4;
-                next = qt[g2048::argmax4_torch(qo[0], qo[1], qo[2], qo[3])];
-            } else {
-                next = g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);
-            }
-            {
-#pragma clang fp contract(off)
-                A.y_out[b] = M.r[t] + (double)M.disc[t] * next;
-            }
-        }
-        CPHASE(7);
-    }
-}
-
 // ------------------------------------------------------------------ 3. train A
 struct TrainArgs {
     Net on;
@@ -510,46 +448,99 @@ struct TrainArgs {
     double* slab;  // [grid][SLAB]
 };
 
-__global__ __launch_bounds__(NT) void k_conv64_train_a(TrainArgs A) {
+// Targets and the graded forward of the same tile in one launch (2 + 3 above): per tile the
+// sampled rows are fetched once (s', r, d, s, a in one round trip, one tile ahead), Q_online(s')
+// (Double DQN) and Q_target(s') give y, then Q_online(s) -> MSE -> fc2 / fc1 gradients and dZ2.
+// The three forwards share one call site (forward() is inlined once).
+struct FusedArgs {
+    TgtArgs T;
+    TrainArgs A;
+};
+
+__global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     __shared__ Smem M;
+    const TgtArgs& T = F.T;
+    const TrainArgs& A = F.A;
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
     d4 gf1[16];  // dWf1 of wave w: rows j = 16w + 4r + lk, columns 16 cb + lr
 #pragma unroll
     for (int c = 0; c < 16; ++c) gf1[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gf2 = 0.0, gfb2 = 0.0, gfb1 = 0.0, gloss = 0.0;
+    const unsigned long long ep = T.idx_in ? 0ull : *T.step;
+    const unsigned long long count = T.idx_in ? 0ull : *T.R.count;
+    if (blockIdx.x == 0 && t == 0) *T.step_next = *T.step + 1ull;
     CPHASE(-1);
     stage_small(M.sw[0], A.on);
+    stage_small(M.sw[1], T.tg);
     const SmallW& W = M.sw[0];
     const int64_t ntiles = (A.batch + TB - 1) / TB;
-    // board t of a tile: s, a, y; the next tile's are fetched while the current one runs
-    uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    // board t of a tile: the sampled row, its s', r, (1 - d) * gamma (float32 in torch,
+    // src/dqn_lib.py:131), s and a; the next tile's are fetched while the current one runs
+    uint4 s2v = make_uint4(0u, 0u, 0u, 0u), sv = s2v;
+    double rj = 0.0;
+    float disc = 0.f;
     int aj = 0;
-    double yj = 0.0;
     auto fetch = [&](int64_t tile) {
-        sv = make_uint4(0u, 0u, 0u, 0u);
+        s2v = sv = make_uint4(0u, 0u, 0u, 0u);
+        rj = 0.0;
+        disc = 0.f;
         aj = 0;
-        yj = 0.0;
         const int64_t b = tile * TB + t;
         if (t < TB && tile < ntiles && b < A.batch) {
-            const int64_t row = A.idx[b];
-            sv = A.R.s[row];
-            aj = A.R.a[row];
-            yj = A.y[b];
+            const int64_t row =
+                T.idx_in ? T.idx_in[b] : sample_row(b, ep, count, T.seed_lo, T.seed_hi);
+            T.idx_out[b] = row;
+            s2v = T.R.s2[row];
+            sv = T.R.s[row];
+            rj = (double)T.R.r[row];
+            disc = (float)(1 - (int)T.R.d[row]) * T.gamma;
+            aj = T.R.a[row];
         }
     };
     fetch(blockIdx.x);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * TB;
-        __syncthreads();
+        __syncthreads();  // the previous tile is done with M
+        const uint4 s_cur = sv;
+        const int a_cur = aj;
         if (t < TB) {
-            put_row(M.x + t * XS, sv);
-            M.act[t] = aj;
-            M.y[t] = yj;
+            put_row(M.x + t * XS, s2v);
+            M.r[t] = rj;
+            M.disc[t] = disc;
         }
         fetch(tile + gridDim.x);
+        CPHASE(1);
+        // k = 0: Q_online(s') -> q2 (Double DQN only); 1: Q_target(s') -> q; 2: Q_online(s) -> q
+#pragma unroll 1
+        for (int k = T.double_dqn ? 0 : 1; k < 3; ++k) {
+            if (k == 2) {  // y from the two target-side forwards, then s in place of s'
+                if (t < TB) {
+                    double yv = 0.0;
+                    if (b0 + t < A.batch) {
+                        const double* qt = M.q + t * 4;
+                        double next;
+                        if (T.double_dqn) {
+                            const double* qo = M.q2 + t * 4;
+                            next = qt[g2048::argmax4_torch(qo[0], qo[1], qo[2], qo[3])];
+                        } else {
+                            next = g2048::qmax4_torch(qt[0], qt[1], qt[2], qt[3]);
+                        }
+                        {
+#pragma clang fp contract(off)
+                            yv = M.r[t] + (double)M.disc[t] * next;
+                        }
+                        T.y_out[b0 + t] = yv;
+                    }
+                    M.y[t] = yv;
+                    put_row(M.x + t * XS, s_cur);
+                    M.act[t] = a_cur;
+                }
+                CPHASE(2);
+            }
+            forward(M, M.sw[k == 1 ? 1 : 0], k == 1 ? T.ptg : T.pon, k == 0 ? M.q2 : M.q);
+        }
         CPHASE(8);
-        forward(M, W, A.pon, M.q);  // Q_online(s); h2, h3 kept
         if (t < TB) {
             double dq = 0.0, ls = 0.0;
             if (b0 + t < A.batch) {
@@ -1172,7 +1163,8 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     R.r = r;
     R.count = reinterpret_cast<const unsigned long long*>(count);
 
-    TgtArgs T;
+    FusedArgs FA;
+    TgtArgs& T = FA.T;
     T.on = net_of(online);
     T.tg = net_of(target);
     T.pon = Packed{pk + O_U_ON, pk + O_F1_ON};
@@ -1188,9 +1180,8 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     T.idx_out = idx_out;
     T.y_out = y_out;
     T.step_next = step_next;
-    hipLaunchKernelGGL(k_conv64_targets, dim3(grid), dim3(NT), 0, st, T);
 
-    TrainArgs A;
+    TrainArgs& A = FA.A;
     A.on = T.on;
     A.pon = T.pon;
     A.pf1b = pk + O_F1B;
@@ -1201,7 +1192,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     A.batch = batch;
     A.dz2 = dz2;
     A.slab = slab;
-    hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, st, A);
+    hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, st, FA);
     hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, st, A);
 
     RedArgs D;

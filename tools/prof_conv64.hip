@@ -77,7 +77,8 @@ int main(int argc, char** argv) {
 
     PackArgs P{w[0][2], w[0][4], w[1][2], w[1][4], pk};
     Ring R{reinterpret_cast<const uint4*>(s), reinterpret_cast<const uint4*>(s2), a, d, r, count};
-    TgtArgs T{};
+    FusedArgs FA{};
+    TgtArgs& T = FA.T;
     T.on = Net{w[0][0], w[0][1], w[0][2], w[0][3], w[0][4], w[0][5], w[0][6], w[0][7]};
     T.tg = Net{w[1][0], w[1][1], w[1][2], w[1][3], w[1][4], w[1][5], w[1][6], w[1][7]};
     T.pon = Packed{pk + O_U_ON, pk + O_F1_ON};
@@ -91,7 +92,7 @@ int main(int argc, char** argv) {
     T.idx_out = idx;
     T.y_out = y;
     T.step_next = step_next;
-    TrainArgs A{};
+    TrainArgs& A = FA.A;
     A.on = T.on;
     A.pon = T.pon;
     A.pf1b = pk + O_F1B;
@@ -124,8 +125,8 @@ int main(int argc, char** argv) {
     auto launch = [&](int k) {
         switch (k) {
             case 0: hipLaunchKernelGGL(k_pack, dim3(PACK_ALL / NT), dim3(NT), 0, nullptr, P); break;
-            case 1: hipLaunchKernelGGL(k_conv64_targets, dim3(grid), dim3(NT), 0, nullptr, T); break;
-            case 2: hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, nullptr, A); break;
+            case 1: break;  // (targets: fused into train A)
+            case 2: hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, nullptr, FA); break;
             case 3: hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, nullptr, A); break;
             default:
                 hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 127) / 128), dim3(64 * RW), 0,
@@ -183,7 +184,7 @@ int main(int argc, char** argv) {
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_cphase), sizeof(ph));
 #endif
     const double tpw = (double)N * ((tiles + grid - 1) / grid);  // tiles per workgroup x N
-    const char* names[20] = {"-", "tgt sample", "stage_small", "conv1+V", "conv2 wino", "fc1",
+    const char* names[20] = {"-", "sample+put s'", "y + put s", "conv1+V", "conv2 wino", "fc1",
                              "fc2", "tgt y", "A load", "A loss/dq", "A fc2 grad+dZ3",
                              "A dWf1", "A dH2+store", "A slab", "B load", "B conv1",
                              "B db2+dW2", "B dD", "B dW1", "B slab"};
