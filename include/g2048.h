@@ -451,6 +451,29 @@ G2048_API int g2048_convnet_forward_greedy_f64(const g2048_convnet_params_f64* p
                                                double* q_out_dev, double* workspace_dev,
                                                void* stream);
 
+/* The forward of the reference's dense Q-net (src/configs/double_dqn_dense.py:7-15: Linear(16,
+ * 512) ReLU Linear(512,512) ReLU Linear(512,256) ReLU Linear(256,4)) in float32 or float64
+ * (dtype; every pointer below and q_out of that type): the rollout's `model(state)` of
+ * epsilon_greedy_policy (src/dqn_lib.py:20-24) for a learner that trains this net on the torch
+ * path.  g2048_densenet_forward: Q[b] (q_out[n][4]) of rows[idx ? idx[b] : b].
+ * g2048_densenet_forward_greedy: Q of exactly the env's boards whose next eps-greedy step takes
+ * the greedy branch (the step's own draw; eps forms of g2048_env_step_egreedy[_schedule]); rows
+ * of exploring boards are not written.  A row's Q does not depend on the other rows: the greedy
+ * rows are bitwise the all-rows forward's. */
+typedef struct {
+    const void *w1, *b1; /* Linear(16, 512)  */
+    const void *w2, *b2; /* Linear(512, 512) */
+    const void *w3, *b3; /* Linear(512, 256) */
+    const void *w4, *b4; /* Linear(256, 4)   */
+} g2048_densenet_params;
+G2048_API int g2048_densenet_forward(const g2048_densenet_params* params, int dtype,
+                                     const uint8_t* rows_dev, const int64_t* idx_dev, int64_t n,
+                                     void* q_out_dev, void* stream);
+G2048_API int g2048_densenet_forward_greedy(const g2048_densenet_params* params, int dtype,
+                                            g2048_env* env, const double* eps_dev, double eps,
+                                            double eps_decay_episodes, double eps_min,
+                                            void* q_out_dev, void* stream);
+
 /* g2048_adam_step_sync in float64: the Adam update of the float64 fused reductions (torch's Adam
  * with its scalars in double) over n_tensors (<= 16) float64 parameter tensors, for a
  * data-parallel float64 learner (gradient -> all-reduce -> this step). */

@@ -471,8 +471,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     const unsigned long long count = T.idx_in ? 0ull : *T.R.count;
     if (blockIdx.x == 0 && t == 0) *T.step_next = *T.step + 1ull;
     CPHASE(-1);
-    stage_small(M.sw[0], A.on);
-    stage_small(M.sw[1], T.tg);
     const SmallW& W = M.sw[0];
     const int64_t ntiles = (A.batch + TB - 1) / TB;
     // board t of a tile: the sampled row, its s', r, (1 - d) * gamma (float32 in torch,
@@ -498,7 +496,9 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
             aj = T.R.a[row];
         }
     };
-    fetch(blockIdx.x);
+    fetch(blockIdx.x);  // issued before the small weights' staging: the round trips overlap
+    stage_small(M.sw[0], A.on);
+    stage_small(M.sw[1], T.tg);
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
         const int64_t b0 = tile * TB;
         __syncthreads();  // the previous tile is done with M
@@ -668,29 +668,34 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gw1[4] = {0.0, 0.0, 0.0, 0.0}, gb1 = 0.0, gb2 = 0.0;
     CPHASE(-1);
-    stage_small(M.sw, A.on);
     const int64_t ntiles = (A.batch + TB - 1) / TB;
-    // the tile's boards (the next tile's fetched while the current one runs)
+    // the tile's boards and the thread's dZ2 (four (b = (t >> 6) + 4k, o = t & 63) pairs, four
+    // doubles (p) each): the next tile's are fetched while the current one runs, so neither the
+    // row gather nor the dZ2 round trip sits between two tiles
     uint4 sv = make_uint4(0u, 0u, 0u, 0u);
+    double2 zv[4][2];
     auto fetch = [&](int64_t tile) {
         sv = make_uint4(0u, 0u, 0u, 0u);
         const int64_t b = tile * TB + t;
         if (t < TB && tile < ntiles && b < A.batch) sv = A.R.s[A.idx[b]];
-    };
-    fetch(blockIdx.x);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-        __syncthreads();
-        if (t < TB) put_row(M.x + t * XS, sv);
-        {  // dM = A dY A^T of the thread's four (b = (t >> 6) + 4k, o = t & 63) pairs; db2
-            const int o = t & 63;
-            double2 zv[4][2];  // dZ2 of the pairs: four doubles (p) each
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < 4; ++k) {
+            zv[k][0] = zv[k][1] = make_double2(0.0, 0.0);
+            if (tile < ntiles) {
                 const double2* src = reinterpret_cast<const double2*>(
-                    A.dz2 + (tile * TB + (t >> 6) + 4 * k) * 256 + o * 4);
+                    A.dz2 + (tile * TB + (t >> 6) + 4 * k) * 256 + (t & 63) * 4);
                 zv[k][0] = src[0];
                 zv[k][1] = src[1];
             }
+        }
+    };
+    fetch(blockIdx.x);  // issued before the small weights' staging: the round trips overlap
+    stage_small(M.sw, A.on);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        __syncthreads();
+        if (t < TB) put_row(M.x + t * XS, sv);
+        {  // dM = A dY A^T of the thread's four (b, o) pairs; db2
+            const int o = t & 63;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const double y00 = zv[k][0].x, y01 = zv[k][0].y, y10 = zv[k][1].x, y11 = zv[k][1].y;

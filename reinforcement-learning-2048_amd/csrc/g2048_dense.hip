@@ -1,0 +1,322 @@
+// g2048_dense.hip -- the forward of the reference's dense Q-net (src/configs/double_dqn_dense.py:
+// 7-15: Linear(16,512) ReLU Linear(512,512) ReLU Linear(512,256) ReLU Linear(256,4)) on board rows,
+// in float32 or float64: the `model(state)` of epsilon_greedy_policy (src/dqn_lib.py:20-24) for a
+// Trainer whose learner trains that net on the torch path.  Two forms:
+//   all rows:      Q[b] of rows[idx ? idx[b] : b], b < n;
+//   greedy rows:   Q only of the env's boards whose next eps-greedy step takes the greedy branch
+//                  (the step kernel's own Philox draw and eps rule) -- the only rows the policy
+//                  evaluates the model on.  Early in the schedule (eps ~ 1) that is almost none.
+// A row's Q does not depend on which rows share its tile (every output element sums its k in one
+// fixed order), so the greedy rows are bitwise the all-rows forward's.
+//
+// Per 16-row tile, 4 waves; wave w owns output columns [w N/4, (w+1) N/4) of a layer, in 16-wide
+// blocks, on v_mfma_{f32,f64}_16x16x4.  Activations stay in LDS (two [16][K + pad] buffers); the
+// weights stream from L2 as B fragments, one "quad" of 4 k-steps ahead.  The K order is permuted
+// within each 16-wide k chunk so that every lane's A and B operands of 4 k-steps are 4
+// consecutive elements (one 16-byte LDS read / global load per 4 k-steps in f32, two in f64):
+// k-step 4q + u, lane k-group lk <-> k = 16 q + 4 lk + u.  The last layer (N = 4) runs on VALU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/g2048.h"
+#include "g2048_board.hpp"
+#include "g2048_common.hpp"
+
+namespace {
+
+constexpr int NT = 256;  // 4 waves
+constexpr int TB = 16;   // rows per tile
+constexpr int MAX_WG = 256;
+constexpr int H1 = 512, H2 = 512, H3 = 256;
+
+template <typename T>
+struct DenseNet {
+    const T *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4;
+};
+
+// four consecutive elements (16-byte aligned) as one (f32) or two (f64) 16-byte accesses
+__device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+}
+__device__ __forceinline__ void ld4(const double* p, double (&v)[4]) {
+    const double2 x = reinterpret_cast<const double2*>(p)[0];
+    const double2 y = reinterpret_cast<const double2*>(p)[1];
+    v[0] = x.x, v[1] = x.y, v[2] = y.x, v[3] = y.y;
+}
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef double d4v __attribute__((ext_vector_type(4)));
+template <typename T>
+struct Acc;
+template <>
+struct Acc<float> {
+    typedef f4v type;
+    static __device__ __forceinline__ f4v mfma(float a, float b, f4v c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // lane l, register r of a 16x16 result tile: row, column
+    static __device__ __forceinline__ int row(int l, int r) { return 4 * (l >> 4) + r; }
+};
+template <>
+struct Acc<double> {
+    typedef d4v type;
+    static __device__ __forceinline__ d4v mfma(double a, double b, d4v c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ int row(int l, int r) { return 4 * r + (l >> 4); }
+};
+
+// LDS row strides (elements): K + pad so that the 16 rows of a 16-byte read start 4 banks apart
+template <typename T>
+constexpr int stride_of(int k) {
+    return k + (sizeof(T) == 4 ? 4 : 2);
+}
+
+template <typename T>
+struct alignas(16) Smem {
+    T x[TB * stride_of<T>(16)];
+    T a[TB * stride_of<T>(H1)];  // layer 1 out, layer 3 out
+    T b[TB * stride_of<T>(H2)];  // layer 2 out
+};
+
+// One layer: out[r][j] = relu(sum_k in[r][k] W[j][k] + bias[j]) for the tile's 16 rows; wave w
+// computes columns w N/4 .. ; K % 16 == 0, N % 64 == 0.  Ends with a barrier.
+template <typename T, int K, int N>
+__device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__ W,
+                                      const T* __restrict__ bias) {
+    typedef typename Acc<T>::type AccT;
+    constexpr int CB = N / 64;  // 16-wide column blocks per wave
+    constexpr int NQ = K / 16;  // quads of 4 k-steps
+    constexpr int SI = stride_of<T>(K), SO = stride_of<T>(N);
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
+    AccT acc[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) acc[c] = AccT{0, 0, 0, 0};
+    // lane's B rows: W[(w CB + c) 16 + lr][16 q + 4 lk .. + 3]
+    const T* wr = W + (size_t)(w * CB * 16 + lr) * K + 4 * lk;
+    const T* ar = in + lr * SI + 4 * lk;
+    T bq[2][CB][4];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K, bq[0][c]);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (q + 1 < NQ) {
+#pragma unroll
+            for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K + 16 * (q + 1), bq[(q + 1) & 1][c]);
+        }
+        T av[4];
+        ld4(ar + 16 * q, av);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < CB; ++c) acc[c] = Acc<T>::mfma(av[u], bq[q & 1][c][u], acc[c]);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        const int j = (w * CB + c) * 16 + lr;
+        const T bj = bias[j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const T z = acc[c][r] + bj;
+            out[Acc<T>::row(l, r) * SO + j] = z > T(0) ? z : T(0);
+        }
+    }
+    __syncthreads();
+}
+
+// The tile's 16 rows (in S.x) through the net; Q of row b -> q[b * 4 + a] for b < nb.
+template <typename T>
+__device__ __forceinline__ void forward_tile(Smem<T>& S, const DenseNet<T>& P, T* q, int nb,
+                                             const int32_t* qrow) {
+    __syncthreads();  // S.x written
+    layer<T, 16, H1>(S.x, S.a, P.w1, P.b1);
+    layer<T, H1, H2>(S.a, S.b, P.w2, P.b2);
+    layer<T, H2, H3>(S.b, S.a, P.w3, P.b3);
+    // Linear(256, 4) on VALU: thread (row b, action a, part p) sums k = 64 p .. 64 p + 63 in two
+    // chains; the four parts are combined in a fixed order through lane shuffles
+    const int t = threadIdx.x, b = t >> 4, a = (t >> 2) & 3, part = t & 3;
+    const T* hr = S.a + b * stride_of<T>(H3) + 64 * part;
+    const T* wr = P.w4 + a * H3 + 64 * part;
+    T e = T(0), o = T(0);
+#pragma unroll 8
+    for (int k = 0; k < 64; k += 2) {
+        e = fma(wr[k], hr[k], e);
+        o = fma(wr[k + 1], hr[k + 1], o);
+    }
+    const T v = e + o;
+    const T v1 = __shfl_xor(v, 1), v2 = __shfl_xor(v, 2), v3 = __shfl_xor(v, 3);
+    if (part == 0 && b < nb) q[(int64_t)qrow[b] * 4 + a] = ((v + v1) + (v2 + v3)) + P.b4[a];
+    __syncthreads();  // S.a / S.x free for the next tile
+}
+
+template <typename T>
+struct FwdArgs {
+    DenseNet<T> net;
+    const uint4* rows;
+    const int64_t* idx;
+    int64_t n;
+    T* q;
+    const uint64_t* clock;  // null: every row
+    const uint32_t* ep;
+    uint64_t board_offset;
+    uint32_t seed_lo, seed_hi;
+    const double* eps_dev;
+    double eps, eps_decay, eps_min;
+    int64_t chunk;
+};
+
+template <typename T>
+__device__ __forceinline__ void put_row(T* xr, uint4 v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) xr[4 * k + j] = (T)((w[k] >> (8 * j)) & 0xFFu);
+}
+
+// The rows [c0, c1) of workgroup w: per window of NT rows the selected ones (all, or the greedy
+// branch's) are queued (ballot + prefix) and run in 16-row tiles; fewer than 16 left over carry
+// into the next window (the k_conv64_forward scheme).  The queue holds row offsets from c0.
+template <typename T>
+__global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
+    __shared__ Smem<T> S;
+    __shared__ int32_t queue[NT + TB];
+    __shared__ int32_t qrow[TB];
+    __shared__ int32_t wcnt[4];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * A.chunk;
+    const int64_t c1 = c0 + A.chunk < A.n ? c0 + A.chunk : A.n;
+    int qn = 0;
+    for (int64_t w0 = c0; w0 < c1; w0 += NT) {
+        const bool last = w0 + NT >= c1;
+        const int64_t i = w0 + t;
+        bool g = i < c1;
+        if (g && A.clock) {
+            const uint4 u = g2048::draw(A.seed_lo, A.seed_hi, A.board_offset + (uint64_t)i,
+                                        g2048::DOMAIN_STEP, A.clock[i >> 6]);
+            const uint32_t e = A.eps_decay > 0.0 ? A.ep[4 * i] : 0u;
+            g = !g2048::explores(u.y, g2048::step_eps(A.eps_decay, A.eps_min, A.eps_dev, A.eps, e));
+        }
+        const uint64_t bal = __ballot(g);
+        if (lane == 0) wcnt[wv] = __popcll(bal);
+        __syncthreads();
+        int base = qn;
+        for (int ww = 0; ww < wv; ++ww) base += wcnt[ww];
+        if (g) queue[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(i - c0);
+        qn += (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+        __syncthreads();
+        const int nt = last ? (qn + TB - 1) / TB : qn / TB;
+        for (int j = 0; j < nt; ++j) {
+            const int nb = qn - j * TB < TB ? qn - j * TB : TB;
+            if (t < TB) {
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                int32_t row = 0;
+                if (t < nb) {
+                    const int64_t b = c0 + queue[j * TB + t];
+                    v = A.rows[A.idx ? A.idx[b] : b];
+                    row = (int32_t)b;
+                }
+                put_row(S.x + t * stride_of<T>(16), v);
+                qrow[t] = row;
+            }
+            forward_tile<T>(S, A.net, A.q, nb, qrow);
+        }
+        // carry the remainder (< TB rows) to the front of the queue
+        const int rem = qn - nt * TB;
+        __syncthreads();
+        const int32_t keep = t < rem ? queue[nt * TB + t] : 0;
+        __syncthreads();
+        if (t < rem) queue[t] = keep;
+        qn = rem;
+    }
+}
+
+template <typename T>
+DenseNet<T> net_of(const g2048_densenet_params* p) {
+    return DenseNet<T>{(const T*)p->w1, (const T*)p->b1, (const T*)p->w2, (const T*)p->b2,
+                       (const T*)p->w3, (const T*)p->b3, (const T*)p->w4, (const T*)p->b4};
+}
+
+template <typename T>
+int launch(const g2048_densenet_params* p, FwdArgs<T>& F, void* stream, const char* what) {
+    F.net = net_of<T>(p);
+    const int64_t tiles = (F.n + TB - 1) / TB;
+    const int grid = (int)(tiles < MAX_WG ? tiles : MAX_WG);
+    F.chunk = (F.n + grid - 1) / grid;
+    hipLaunchKernelGGL(k_dense_forward<T>, dim3(grid), dim3(NT), 0,
+                       reinterpret_cast<hipStream_t>(stream), F);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool params_ok(const g2048_densenet_params* p) {
+    return p && p->w1 && p->b1 && p->w2 && p->b2 && p->w3 && p->b3 && p->w4 && p->b4;
+}
+
+}  // namespace
+
+extern "C" G2048_API int g2048_densenet_forward(const g2048_densenet_params* p, int dtype,
+                                                const uint8_t* rows, const int64_t* idx, int64_t n,
+                                                void* q_out, void* stream) {
+    if (!params_ok(p) || !rows || !q_out || n < 0 || (dtype != G2048_F32 && dtype != G2048_F64))
+        return g2048_fail(G2048_EINVAL, "densenet_forward: NULL argument, n < 0 or bad dtype");
+    if (n == 0) return G2048_OK;
+    if (n > INT32_MAX) return g2048_fail(G2048_EINVAL, "densenet_forward: n > 2^31 - 1");
+    if (dtype == G2048_F32) {
+        FwdArgs<float> F{};
+        F.rows = reinterpret_cast<const uint4*>(rows);
+        F.idx = idx;
+        F.n = n;
+        F.q = static_cast<float*>(q_out);
+        return launch(p, F, stream, "densenet_forward");
+    }
+    FwdArgs<double> F{};
+    F.rows = reinterpret_cast<const uint4*>(rows);
+    F.idx = idx;
+    F.n = n;
+    F.q = static_cast<double*>(q_out);
+    return launch(p, F, stream, "densenet_forward");
+}
+
+extern "C" G2048_API int g2048_densenet_forward_greedy(const g2048_densenet_params* p, int dtype,
+                                                       g2048_env* env, const double* eps_dev,
+                                                       double eps, double eps_decay_episodes,
+                                                       double eps_min, void* q_out, void* stream) {
+    if (!params_ok(p) || !env || !q_out || (dtype != G2048_F32 && dtype != G2048_F64))
+        return g2048_fail(G2048_EINVAL, "densenet_forward_greedy: NULL argument or bad dtype");
+    uint8_t* board = nullptr;
+    uint32_t* ep = nullptr;
+    uint64_t* clock = nullptr;
+    uint64_t seed = 0, offset = 0;
+    if (g2048_env_views(env, &board, nullptr, &ep, &clock) != G2048_OK ||
+        g2048_env_rng(env, &seed, &offset) != G2048_OK)
+        return G2048_EINVAL;
+    const int64_t n = g2048_env_size(env);
+    if (n <= 0) return g2048_fail(G2048_EINVAL, "densenet_forward_greedy: empty env");
+    if (n > INT32_MAX) return g2048_fail(G2048_EINVAL, "densenet_forward_greedy: n > 2^31 - 1");
+    auto fill = [&](auto& F) {
+        F.rows = reinterpret_cast<const uint4*>(board);
+        F.n = n;
+        F.clock = clock;
+        F.ep = ep;
+        F.board_offset = offset;
+        F.seed_lo = (uint32_t)seed;
+        F.seed_hi = (uint32_t)(seed >> 32);
+        F.eps_dev = eps_dev;
+        F.eps = eps;
+        F.eps_decay = eps_decay_episodes > 0.0 ? eps_decay_episodes : 0.0;
+        F.eps_min = eps_min;
+    };
+    if (dtype == G2048_F32) {
+        FwdArgs<float> F{};
+        fill(F);
+        F.q = static_cast<float*>(q_out);
+        return launch(p, F, stream, "densenet_forward_greedy");
+    }
+    FwdArgs<double> F{};
+    fill(F);
+    F.q = static_cast<double*>(q_out);
+    return launch(p, F, stream, "densenet_forward_greedy");
+}

@@ -87,6 +87,8 @@ SIGNATURES = {
                                         _u64, _vp]),
     "g2048_convnet_update": (_int, [_vp, _vp, _vp, _vp, _i64, _u64, _vp, C.c_float, _int, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl, _u64, _vp]),
+    "g2048_densenet_forward": (_int, [_vp, _int, _vp, _vp, _i64, _vp, _vp]),
+    "g2048_densenet_forward_greedy": (_int, [_vp, _int, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp]),
     "g2048_astar_search": (_int, [_vp, _i64, _int, _u64, _u64, _int, _i64, _i64, _vp, _vp, _vp,
                                   _vp, _vp, _vp, _vp]),
     "g2048_last_error": (C.c_char_p, []),
@@ -102,6 +104,11 @@ class ConvNetParams(C.Structure):
                                           "fc2_b")]
 
 
+
+
+class DenseNetParams(C.Structure):
+    """g2048_densenet_params: device pointers of the reference dense Q-net's 8 tensors."""
+    _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4")]
 
 
 class Dense64Params(C.Structure):

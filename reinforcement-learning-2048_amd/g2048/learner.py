@@ -94,6 +94,10 @@ class DQNLearner:
         self._upd = None
         # float64 conv: the rollout's Q through the fused forward as well
         self._fwd64 = qnet.ConvForward64(self.model) if self.f64 and self.kind == "conv" else None
+        # the reference dense net on the torch path: the rollout's Q through one HIP launch
+        # (g2048_densenet_forward[_greedy]) instead of torch's four GEMMs over every board
+        self._dfwd = (qnet.DenseForward(self.model) if not self.fused and self.device.type == "cuda"
+                      and qnet.is_dense_ref(self.model) else None)
         if self.fused:
             self._p_on = None if self.f64 else qnet.net_params(self.model)
             self._p_tgt = None if self.f64 else qnet.net_params(self.target)
@@ -238,10 +242,15 @@ class DQNLearner:
             self._allreduce()
             self._apply()
         self.updates += 1
+        self.host_target_sync()
+        return self.last_loss
+
+    def host_target_sync(self) -> None:
+        """The torch path's target sync every target_sync_every updates (src/dqn_lib.py:227-228),
+        after self.updates was counted; the fused paths sync on the device update counter."""
         if (not self.fused and self.target_sync_every
                 and self.updates % self.target_sync_every == 0):
             dqn_lib.sync_target(self.model, self.target)
-        return self.last_loss
 
     @torch.no_grad()
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
@@ -249,6 +258,8 @@ class DQNLearner:
             return qnet.forward(self.model, env.board, params=self._p_on)
         if self._fwd64 is not None:
             return self._fwd64(env.board)
+        if self._dfwd is not None:
+            return self._dfwd(env.board)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 
@@ -328,11 +339,15 @@ class Trainer:
                  episode_log_slots: int = 8, track_boards: int = 0,
                  history_len: int = 4096, graph: bool | None = None):
         self.env, self.replay, self.learner = env, replay, learner
-        # graph: replay one captured hipGraph per iteration (fused step + updates) once the
-        # learner is updating; default on for the fused fp32 learners on one process
-        self.graph = (learner.fused and learner.graph) if graph is None else bool(graph)
-        if self.graph and not learner.fused:
-            raise ValueError("the graphed loop needs a fused learner")
+        # graph: replay one captured hipGraph per iteration (step + updates) once the learner is
+        # updating; default on for the fused learners and for the reference dense net on the
+        # torch path (its rollout forward is the HIP g2048_densenet_forward_greedy)
+        capturable = learner.fused or (learner._dfwd is not None and learner.sampler is None)
+        self.graph = (capturable and learner.graph) if graph is None else bool(graph)
+        if self.graph and not capturable:
+            raise ValueError("the graphed loop needs a fused learner or the reference dense net")
+        # Q of the greedy-branch boards only (False: every board; tests compare the two)
+        self.greedy_forward = True
         self._loop_graph = None
         self.updates_per_step = int(updates_per_step)
         self.min_fill = int(min_fill if min_fill is not None else learner.B)
@@ -359,6 +374,8 @@ class Trainer:
         if learner.fused and learner.kind == "conv":
             self._q = torch.zeros((env.n, 4), dtype=torch.float64 if learner.f64 else torch.float32,
                                   device=env.device)
+        elif learner._dfwd is not None:
+            self._q = torch.zeros((env.n, 4), dtype=learner._dfwd.dtype, device=env.device)
         self._numbers = {}  # (board, board_episode) -> Experiment episode number
 
     def prefill(self, steps: int) -> None:
@@ -377,7 +394,10 @@ class Trainer:
                                           reward=self._reward, done=self._done,
                                           action=self._action, eps_schedule=sched, f64=L.f64)
         else:
-            if self._q is not None and self.learner._fwd64 is not None:  # greedy branch only
+            if self._q is not None and L._dfwd is not None:  # reference dense net, HIP forward
+                q = (L._dfwd.greedy(self.env, eps_schedule=sched, out=self._q)
+                     if self.greedy_forward else L._dfwd(self.env.board, out=self._q))
+            elif self._q is not None and self.learner._fwd64 is not None:  # greedy branch only
                 q = self.learner._fwd64.greedy(self.env, eps_schedule=sched, out=self._q)
             elif self._q is not None:  # the model runs on the greedy branch only (src/dqn_lib.py:20-24)
                 q = qnet.forward_greedy(self.learner.model, self.env, eps_schedule=sched,
@@ -396,17 +416,26 @@ class Trainer:
         L = self.learner
         if L.world > 1:
             return self._graphed_iteration_dp()
+        # the torch-path learner syncs its target on the host between updates: one update in the
+        # graph, the others through the learner's own graphed update
+        ups = self.updates_per_step if L.fused else 1
         if self._loop_graph is None:
+            if not L.fused and L._graphs is None:
+                L._capture()  # autograd warm-up on a side stream (leaves no trace)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 self._rollout_step()
-                for _ in range(self.updates_per_step):
+                for _ in range(ups):
                     L._compute_grads()
                     L._apply()
             self._loop_graph = g
         L.before_replay()
         self._loop_graph.replay()
-        L.updates += self.updates_per_step
+        for _ in range(ups):
+            L.updates += 1
+            L.host_target_sync()
+        for _ in range(self.updates_per_step - ups):
+            L.update()
 
     def _graphed_iteration_dp(self) -> None:
         """Data-parallel form: graph A = the rollout step + the first update's gradient, the
@@ -414,6 +443,8 @@ class Trainer:
         updates of the iteration run the learner's own two-graph update."""
         L = self.learner
         if self._loop_graph is None:
+            if not L.fused and L._graphs is None:
+                L._capture()  # autograd warm-up on a side stream (leaves no trace)
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self._rollout_step()
@@ -427,6 +458,7 @@ class Trainer:
         L._allreduce()
         gb.replay()
         L.updates += 1
+        L.host_target_sync()
         for _ in range(self.updates_per_step - 1):
             L.update()
 

@@ -24,6 +24,67 @@ _CONV_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias", "5.weight", "5.bias",
 _DENSE_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias")
 
 
+_DENSE_REF_ORDER = ("0.weight", "0.bias", "2.weight", "2.bias", "4.weight", "4.bias", "6.weight",
+                    "6.bias")
+
+
+def is_dense_ref(model) -> bool:
+    """The reference dense net, src/configs/double_dqn_dense.py:7-15: 16-512-512-256-4, ReLUs."""
+    dims = [(16, 512), (512, 512), (512, 256), (256, 4)]
+    return (isinstance(model, nn.Sequential) and len(model) == 7
+            and all(isinstance(model[2 * i], nn.Linear)
+                    and (model[2 * i].in_features, model[2 * i].out_features) == d
+                    for i, d in enumerate(dims))
+            and all(isinstance(model[2 * i + 1], nn.ReLU) for i in range(3)))
+
+
+class DenseForward:
+    """The reference dense net's forward as one HIP launch (g2048_densenet_forward / _greedy):
+    Q [n, 4] in the net's dtype (float32 or float64) of board rows, or only of the env boards
+    whose next eps-greedy step takes the greedy branch (the rows epsilon_greedy_policy evaluates
+    the model on, src/dqn_lib.py:20-24).  Parameter pointers are read at construction."""
+
+    def __init__(self, model):
+        if not is_dense_ref(model):
+            raise TypeError("DenseForward needs the reference dense net (16-512-512-256-4)")
+        dt = next(model.parameters()).dtype
+        if dt not in (torch.float32, torch.float64):
+            raise TypeError("DenseForward runs float32 or float64 nets")
+        self.dtype = dt
+        self.code = N.F32 if dt == torch.float32 else N.F64
+        self._params = _tensors(model, _DENSE_REF_ORDER, dt)
+        self.p = N.DenseNetParams(*[t.data_ptr() for t in self._params])
+
+    def _out(self, n, device, out):
+        if out is None:
+            return torch.empty((n, 4), dtype=self.dtype, device=device)
+        if out.shape != (n, 4) or out.dtype != self.dtype or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous {self.dtype} [{n}, 4] tensor")
+        return out
+
+    def __call__(self, rows: torch.Tensor, idx: torch.Tensor | None = None,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+        if rows.dtype != torch.uint8 or rows.dim() != 2 or rows.shape[1] != 16 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous uint8 [*, 16] board tensor")
+        if idx is not None and (idx.dtype != torch.int64 or not idx.is_contiguous()):
+            raise ValueError("idx must be contiguous int64")
+        n = rows.shape[0] if idx is None else idx.numel()
+        out = self._out(n, rows.device, out)
+        N.check(N.load().g2048_densenet_forward(C.byref(self.p), self.code, N.ptr(rows),
+                                                N.ptr(idx), n, N.ptr(out),
+                                                N.stream_of(rows.device)),
+                "g2048_densenet_forward")
+        return out
+
+    def greedy(self, env, epsilon=0.0, eps_schedule=None, out: torch.Tensor | None = None):
+        out = self._out(env.n, env.device, out)
+        eps_ptr, eps_val, dec, mn = env.eps_args(epsilon, eps_schedule)
+        N.check(N.load().g2048_densenet_forward_greedy(
+            C.byref(self.p), self.code, env.handle, eps_ptr, eps_val, dec, mn, N.ptr(out),
+            N.stream_of(env.device)), "g2048_densenet_forward_greedy")
+        return out
+
+
 def is_dense64(model) -> bool:
     return (isinstance(model, nn.Sequential) and len(model) == 3
             and isinstance(model[0], nn.Linear) and model[0].in_features == 16
