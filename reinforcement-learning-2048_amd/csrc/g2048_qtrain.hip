@@ -629,6 +629,9 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         }
     }
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    // Adam's step scalars (two f64 pow) formed while the slab loads are in flight, not after the
+    // barrier on the update's critical path
+    g2048::AdamCoef c{};
     for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
         float4 r[16];
 #pragma unroll
@@ -638,6 +641,7 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
                        ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
                        : make_float4(0.f, 0.f, 0.f, 0.f);
         }
+        if (adam && g0 == 0) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
             v.x += r[u].x;
@@ -658,8 +662,6 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         sv.w += part[k][lane].w;
     }
     const float se[4] = {sv.x, sv.y, sv.z, sv.w};
-    g2048::AdamCoef c{};
-    if (adam) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int pos = p4 * 4 + e;
