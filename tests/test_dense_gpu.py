@@ -101,11 +101,12 @@ def test_dense_trainer_graphed_greedy_equals_full_forward(G, dtype):
     iteration (HIP greedy-branch forward + fused eps-greedy step + the torch update), and 25
     iterations are bitwise those of the same loop computing every board's Q (the boards start at
     mixed episode counts, so eps spans 1 .. min_epsilon)."""
+    from g2048 import train
     from test_train_gpu import _fingerprint, _small
 
     outs = []
     for greedy in (True, False):
-        tr = _small(G, "dense", min_fill=3 * 1024, target_sync_every=3, track_boards=0,
+        tr = _small(train, "dense", min_fill=3 * 1024, target_sync_every=3, track_boards=0,
                     dtype=getattr(torch, dtype))
         assert tr.graph and tr.learner._dfwd is not None and not tr.learner.fused
         tr.greedy_forward = greedy
@@ -127,11 +128,12 @@ def test_dense_trainer_graphed_greedy_equals_full_forward(G, dtype):
 def test_dense_trainer_graphed_equals_eager(G):
     """The captured iteration (step + update) against the eager loop (graph=False), same seeds:
     boards, ring, episode log bitwise; weights to fp32 roundoff of the two torch launches."""
+    from g2048 import train
     from test_train_gpu import _fingerprint, _small
 
     outs = []
     for graph in (True, False):
-        tr = _small(G, "dense", min_fill=3 * 1024, target_sync_every=3, track_boards=0,
+        tr = _small(train, "dense", min_fill=3 * 1024, target_sync_every=3, track_boards=0,
                     loop_graph=graph)
         assert tr.graph == graph
         for _ in range(12):
