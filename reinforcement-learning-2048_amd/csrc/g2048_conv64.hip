@@ -629,7 +629,8 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
         }
         CPHASE(12);
     }
-    // slab: fc1.weight [64][256], fc1.bias, fc2.weight [4][64], fc2.bias, loss
+    // slab: fc1.weight [64][256], fc1.bias, fc2.weight [4][64], fc2.bias, loss.  (Issued inside
+    // the last tile, before dH2, these stores made the kernel spill: 312 B of scratch.)
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
 #pragma unroll
     for (int cb = 0; cb < 16; ++cb)
@@ -728,6 +729,21 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             }
         }
         CPHASE(16);
+        if (tile + gridDim.x >= ntiles) {
+            // last tile: conv2.weight's slab terms are final; a lane's four taps of one (o, c)
+            // are 32 contiguous bytes (torch order o, c, tap), two 16-byte stores, so 16 lanes
+            // write 512 B in a row; they drain while dV's MFMAs run
+            double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    double2* dst = reinterpret_cast<double2*>(
+                        sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
+                    dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
+                    dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
+                }
+        }
         // dV_xi: wave w -> channels c = 16w .., K = 64 o in 16 k-steps, nine chains; B two
         // steps ahead
         d4 dv[9];
@@ -809,18 +825,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         const double* v2 = red + 5 * 256 + c;  // threads c, c + 64, c + 128, c + 192
         sl[P_B2 + c] = ((v2[0] + v2[64]) + v2[128]) + v2[192];
     }
-    // a lane's four taps of one (o, c) are 32 contiguous bytes (torch order o, c, tap): two
-    // 16-byte stores, so 16 lanes write 512 B in a row (per-tap 8-byte stores at a 32-byte stride
-    // took 2.4x the time of train A's slab write)
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            double2* dst = reinterpret_cast<double2*>(
-                sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
-            dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
-            dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
-        }
     CPHASE(19);
 }
 
