@@ -175,7 +175,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         act = rw.w >> 30;
         if (A.legal_out) legal = legal_mask(b);
         uint4 F, I;
-        dir_sel_const(act, F, I);
+        dir_sel_reg(act, F, I);
         r = lean_step(b, rw.w, p410 ? spawn_exp<true>(rw.w, rw.v, A.p4_thresh)
                                    : spawn_exp<false>(rw.w, rw.v, A.p4_thresh), F, I, done);
     } else {

@@ -115,6 +115,7 @@ struct alignas(16) Smem {
     double r[TB];
     double dq[TB];
     double loss[TB];
+    double f2p[4 * TB * 4];  // fc2 partials of the four waves [w][b][a]
     float disc[TB];
     int act[TB];
 };
@@ -304,25 +305,30 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
             M.h3[(4 * r + lk) * H3S + j] = z > 0.0 ? z : 0.0;
         }
     }
-    __syncthreads();
     CPHASE(5);
-    // fc2 (VALU): thread (b = t >> 4, a = (t >> 2) & 3, part = t & 3) sums units 16 part ..
-    // 16 part + 15; the four parts are combined in a fixed order through lane shuffles
+    // fc2 on MFMA, split by unit: wave w sums its own units j = 16w .. 16w+15 -- the h3 columns
+    // its fc1 epilogue just wrote, so no workgroup barrier is needed before it (one wave's LDS
+    // accesses complete in order) -- as Q_w[b][a] = sum_j h3[b][j] W2[a][j] in 4 k-steps (B
+    // columns a >= 4 are zero); the four partials are then added in wave order.
     {
-        const int b = t >> 4, a = (t >> 2) & 3, part = t & 3;
-        const double* hr = M.h3 + b * H3S + 16 * part;
-        const double* wr = W.f2 + a * 64 + 16 * part;
-        double e = 0.0, o = 0.0;
+        __builtin_amdgcn_wave_barrier();
+        d4 acc = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < 16; j += 2) {
-            e = fma(wr[j], hr[j], e);
-            o = fma(wr[j + 1], hr[j + 1], o);
+        for (int s = 0; s < 4; ++s) {
+            const int j = 16 * w + 4 * s + lk;
+            const double av = M.h3[lr * H3S + j];
+            const double bv = lr < 4 ? W.f2[lr * 64 + j] : 0.0;
+            acc = mfma(av, bv, acc);
         }
-        const double v = e + o;
-        const double v1 = __shfl_xor(v, 1);  // the parts of lanes part ^ 1, ^ 2, ^ 3
-        const double v2 = __shfl_xor(v, 2);
-        const double v3 = __shfl_xor(v, 3);
-        if (part == 0) q[b * 4 + a] = ((v + v1) + (v2 + v3)) + W.fb2[a];
+        if (lr < 4) {  // lane (lr, lk), register r: Q_w[b = 4r + lk][a = lr]
+#pragma unroll
+            for (int r = 0; r < 4; ++r) M.f2p[(w * TB + 4 * r + lk) * 4 + lr] = acc[r];
+        }
+    }
+    __syncthreads();
+    if (t < TB * 4) {  // (b, a) = (t >> 2, t & 3)
+        const double* p = M.f2p + t;
+        q[t] = ((p[0] + p[TB * 4]) + (p[2 * TB * 4] + p[3 * TB * 4])) + W.fb2[t & 3];
     }
     __syncthreads();
     CPHASE(6);

@@ -358,6 +358,32 @@ __device__ __forceinline__ void dir_sel_const(uint32_t a, uint4& F, uint4& I) {
     I = t[2u * a + 1u];
 }
 
+// The same quads selected in registers (immediate operands, three v_cndmask per word): the
+// one-launch-per-step kernel's table load was a dependent memory round trip (a fresh dispatch
+// misses L1) between the step's action draw and its slide.
+__device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t v0, uint32_t v1, uint32_t v2,
+                                         uint32_t v3) {
+    const uint32_t lo = (a & 1u) ? v1 : v0, hi = (a & 1u) ? v3 : v2;
+    return (a & 2u) ? hi : lo;
+}
+
+__device__ __forceinline__ void dir_sel_reg(uint32_t a, uint4& F, uint4& I) {
+#define G2048_SEL(h, k) sel4(a, kDirNetH[0][h][k], kDirNetH[1][h][k], kDirNetH[2][h][k], kDirNetH[3][h][k])
+    constexpr uint32_t kDirNetH[4][2][4] = {
+        {{0x03020100u, 0x07060504u, 0x03020100u, 0x07060504u},
+         {0x03020100u, 0x07060504u, 0x03020100u, 0x07060504u}},
+        {{0x07060504u, 0x03020100u, 0x07060504u, 0x03020100u},
+         {0x07060504u, 0x03020100u, 0x07060504u, 0x03020100u}},
+        {{0x06020400u, 0x07030501u, 0x05040100u, 0x07060302u},
+         {0x06020400u, 0x07030501u, 0x05040100u, 0x07060302u}},
+        {{0x05010703u, 0x04000602u, 0x05040100u, 0x07060302u},
+         {0x02060004u, 0x03070105u, 0x01000504u, 0x03020706u}},
+    };
+    F = make_uint4(G2048_SEL(0, 0), G2048_SEL(0, 1), G2048_SEL(0, 2), G2048_SEL(0, 3));
+    I = make_uint4(G2048_SEL(1, 0), G2048_SEL(1, 1), G2048_SEL(1, 2), G2048_SEL(1, 3));
+#undef G2048_SEL
+}
+
 // The random-policy transition of board b (rows) along the line words given by the selector
 // quads F (rows -> lines) and I (lines -> rows): slide, terminal test of the board as given,
 // spawn of exponent e (1 or 2) when the board moved.  The spawn cell is the k-th empty cell,
