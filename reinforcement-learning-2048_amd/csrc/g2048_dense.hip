@@ -9,8 +9,8 @@
 // A row's Q does not depend on which rows share its tile (every output element sums its k in one
 // fixed order), so the greedy rows are bitwise the all-rows forward's.
 //
-// Per 16-row tile, 4 waves; wave w owns output columns [w N/4, (w+1) N/4) of a layer, in 16-wide
-// blocks, on v_mfma_{f32,f64}_16x16x4.  Activations stay in LDS (two [16][K + pad] buffers); the
+// Per 16-row tile, 8 waves (two per SIMD); wave w owns output columns [w N/8, (w+1) N/8) of a
+// layer, in 16-wide blocks, on v_mfma_{f32,f64}_16x16x4.  Activations stay in LDS (two [16][K + pad] buffers); the
 // weights stream from L2 as B fragments, one "quad" of 4 k-steps ahead.  The K order is permuted
 // within each 16-wide k chunk so that every lane's A and B operands of 4 k-steps are 4
 // consecutive elements (one 16-byte LDS read / global load per 4 k-steps in f32, two in f64):
@@ -24,7 +24,8 @@
 
 namespace {
 
-constexpr int NT = 256;  // 4 waves
+constexpr int NT = 512;  // 8 waves: two per SIMD, so one wave's operand waits hide under the other's MFMAs
+constexpr int NW = NT / 64;
 constexpr int TB = 16;   // rows per tile
 constexpr int MAX_WG = 256;
 constexpr int H1 = 512, H2 = 512, H3 = 256;
@@ -81,12 +82,12 @@ struct alignas(16) Smem {
 };
 
 // One layer: out[r][j] = relu(sum_k in[r][k] W[j][k] + bias[j]) for the tile's 16 rows; wave w
-// computes columns w N/4 .. ; K % 16 == 0, N % 64 == 0.  Ends with a barrier.
+// computes columns w N/8 .. ; K % 16 == 0, N % 128 == 0.  Ends with a barrier.
 template <typename T, int K, int N>
 __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__ W,
                                       const T* __restrict__ bias) {
     typedef typename Acc<T>::type AccT;
-    constexpr int CB = N / 64;  // 16-wide column blocks per wave
+    constexpr int CB = N / (16 * NW);  // 16-wide column blocks per wave
     constexpr int NQ = K / 16;  // quads of 4 k-steps
     constexpr int SI = stride_of<T>(K), SO = stride_of<T>(N);
     const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
@@ -99,19 +100,31 @@ __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__
     T bq[2][CB][4];
 #pragma unroll
     for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K, bq[0][c]);
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
+    // one quad of B fragments in flight ahead of the MFMAs; the loop is unrolled by two (static
+    // buffer indices), not fully: fully unrolled, the scheduler hoisted later quads' loads and
+    // the kernel spilled
+    auto quad = [&](int q, T (&cur)[CB][4], T (&nxt)[CB][4]) {
         if (q + 1 < NQ) {
 #pragma unroll
-            for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K + 16 * (q + 1), bq[(q + 1) & 1][c]);
+            for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K + 16 * (q + 1), nxt[c]);
         }
         T av[4];
         ld4(ar + 16 * q, av);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int c = 0; c < CB; ++c) acc[c] = Acc<T>::mfma(av[u], bq[q & 1][c][u], acc[c]);
+            for (int c = 0; c < CB; ++c) acc[c] = Acc<T>::mfma(av[u], cur[c][u], acc[c]);
         __builtin_amdgcn_sched_barrier(0);
+    };
+    static_assert(NQ % 2 == 0 || NQ == 1, "quads in pairs");
+    if constexpr (NQ == 1) {
+        quad(0, bq[0], bq[1]);
+    } else {
+#pragma unroll 1
+        for (int q = 0; q < NQ; q += 2) {
+            quad(q, bq[0], bq[1]);
+            quad(q + 1, bq[1], bq[0]);
+        }
     }
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
@@ -134,20 +147,22 @@ __device__ __forceinline__ void forward_tile(Smem<T>& S, const DenseNet<T>& P, T
     layer<T, 16, H1>(S.x, S.a, P.w1, P.b1);
     layer<T, H1, H2>(S.a, S.b, P.w2, P.b2);
     layer<T, H2, H3>(S.b, S.a, P.w3, P.b3);
-    // Linear(256, 4) on VALU: thread (row b, action a, part p) sums k = 64 p .. 64 p + 63 in two
-    // chains; the four parts are combined in a fixed order through lane shuffles
-    const int t = threadIdx.x, b = t >> 4, a = (t >> 2) & 3, part = t & 3;
-    const T* hr = S.a + b * stride_of<T>(H3) + 64 * part;
-    const T* wr = P.w4 + a * H3 + 64 * part;
+    // Linear(256, 4) on VALU: thread (row b, action a, part p) sums k = 32 p .. 32 p + 31 in two
+    // chains; the eight parts are combined in a fixed order through lane shuffles
+    const int t = threadIdx.x, b = t >> 5, a = (t >> 3) & 3, part = t & 7;
+    const T* hr = S.a + b * stride_of<T>(H3) + 32 * part;
+    const T* wr = P.w4 + a * H3 + 32 * part;
     T e = T(0), o = T(0);
 #pragma unroll 8
-    for (int k = 0; k < 64; k += 2) {
+    for (int k = 0; k < 32; k += 2) {
         e = fma(wr[k], hr[k], e);
         o = fma(wr[k + 1], hr[k + 1], o);
     }
-    const T v = e + o;
-    const T v1 = __shfl_xor(v, 1), v2 = __shfl_xor(v, 2), v3 = __shfl_xor(v, 3);
-    if (part == 0 && b < nb) q[(int64_t)qrow[b] * 4 + a] = ((v + v1) + (v2 + v3)) + P.b4[a];
+    T v = e + o;
+    v = v + __shfl_xor(v, 1);
+    v = v + __shfl_xor(v, 2);
+    v = v + __shfl_xor(v, 4);
+    if (part == 0 && b < nb) q[(int64_t)qrow[b] * 4 + a] = v + P.b4[a];
     __syncthreads();  // S.a / S.x free for the next tile
 }
 
@@ -184,7 +199,7 @@ __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
     __shared__ Smem<T> S;
     __shared__ int32_t queue[NT + TB];
     __shared__ int32_t qrow[TB];
-    __shared__ int32_t wcnt[4];
+    __shared__ int32_t wcnt[NW];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t c0 = (int64_t)blockIdx.x * A.chunk;
     const int64_t c1 = c0 + A.chunk < A.n ? c0 + A.chunk : A.n;
@@ -205,7 +220,7 @@ __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
         int base = qn;
         for (int ww = 0; ww < wv; ++ww) base += wcnt[ww];
         if (g) queue[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int32_t)(i - c0);
-        qn += (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+        for (int ww = 0; ww < NW; ++ww) qn += wcnt[ww];
         __syncthreads();
         const int nt = last ? (qn + TB - 1) / TB : qn / TB;
         for (int j = 0; j < nt; ++j) {
