@@ -35,15 +35,29 @@ struct DenseNet {
     const T *w1, *b1, *w2, *b2, *w3, *b3, *w4, *b4;
 };
 
-// four consecutive elements (16-byte aligned) as one (f32) or two (f64) 16-byte accesses
-__device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
-    const float4 x = *reinterpret_cast<const float4*>(p);
-    v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+// E consecutive elements (16-byte aligned) as 16-byte accesses
+template <int E>
+__device__ __forceinline__ void ldE(const float* p, float (&v)[E]) {
+#pragma unroll
+    for (int h = 0; h < E / 4; ++h) {
+        const float4 x = reinterpret_cast<const float4*>(p)[h];
+        v[4 * h] = x.x, v[4 * h + 1] = x.y, v[4 * h + 2] = x.z, v[4 * h + 3] = x.w;
+    }
 }
-__device__ __forceinline__ void ld4(const double* p, double (&v)[4]) {
-    const double2 x = reinterpret_cast<const double2*>(p)[0];
-    const double2 y = reinterpret_cast<const double2*>(p)[1];
-    v[0] = x.x, v[1] = x.y, v[2] = y.x, v[3] = y.y;
+template <int E>
+__device__ __forceinline__ void ldE(const double* p, double (&v)[E]) {
+#pragma unroll
+    for (int h = 0; h < E / 2; ++h) {
+        const double2 x = reinterpret_cast<const double2*>(p)[h];
+        v[2 * h] = x.x, v[2 * h + 1] = x.y;
+    }
+}
+
+// k-steps per operand run: a lane's A and B operands of E consecutive k-steps are E consecutive
+// elements (32 bytes, so the 4 lanes of a B row fill a 128-byte line), fewer when K is short
+template <typename T, int K>
+constexpr int run_of() {
+    return sizeof(T) == 4 && K >= 64 ? 8 : 4;
 }
 
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -88,35 +102,37 @@ __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__
                                       const T* __restrict__ bias) {
     typedef typename Acc<T>::type AccT;
     constexpr int CB = N / (16 * NW);  // 16-wide column blocks per wave
-    constexpr int NQ = K / 16;  // quads of 4 k-steps
+    constexpr int E = run_of<T, K>();  // k-steps per operand run
+    constexpr int NQ = K / (4 * E);    // runs of E k-steps
     constexpr int SI = stride_of<T>(K), SO = stride_of<T>(N);
     const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
     AccT acc[CB];
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[c] = AccT{0, 0, 0, 0};
-    // lane's B rows: W[(w CB + c) 16 + lr][16 q + 4 lk .. + 3]
-    const T* wr = W + (size_t)(w * CB * 16 + lr) * K + 4 * lk;
-    const T* ar = in + lr * SI + 4 * lk;
-    T bq[2][CB][4];
+    // k-step E q + u of lane k-group lk is k = 4 E q + E lk + u; lane's B rows:
+    // W[(w CB + c) 16 + lr][4 E q + E lk .. + E - 1]
+    const T* wr = W + (size_t)(w * CB * 16 + lr) * K + E * lk;
+    const T* ar = in + lr * SI + E * lk;
+    T bq[2][CB][E];
 #pragma unroll
-    for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K, bq[0][c]);
-    // one quad of B fragments in flight ahead of the MFMAs; the loop is unrolled by two (static
-    // buffer indices), not fully: fully unrolled, the scheduler hoisted later quads' loads and
+    for (int c = 0; c < CB; ++c) ldE<E>(wr + (size_t)c * 16 * K, bq[0][c]);
+    // one run of B fragments in flight ahead of the MFMAs; the loop is unrolled by two (static
+    // buffer indices), not fully: fully unrolled, the scheduler hoisted later runs' loads and
     // the kernel spilled
-    auto quad = [&](int q, T (&cur)[CB][4], T (&nxt)[CB][4]) {
+    auto quad = [&](int q, T (&cur)[CB][E], T (&nxt)[CB][E]) {
         if (q + 1 < NQ) {
 #pragma unroll
-            for (int c = 0; c < CB; ++c) ld4(wr + (size_t)c * 16 * K + 16 * (q + 1), nxt[c]);
+            for (int c = 0; c < CB; ++c) ldE<E>(wr + (size_t)c * 16 * K + 4 * E * (q + 1), nxt[c]);
         }
-        T av[4];
-        ld4(ar + 16 * q, av);
+        T av[E];
+        ldE<E>(ar + 4 * E * q, av);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < E; ++u)
 #pragma unroll
             for (int c = 0; c < CB; ++c) acc[c] = Acc<T>::mfma(av[u], cur[c][u], acc[c]);
         __builtin_amdgcn_sched_barrier(0);
     };
-    static_assert(NQ % 2 == 0 || NQ == 1, "quads in pairs");
+    static_assert(NQ % 2 == 0 || NQ == 1, "runs in pairs");
     if constexpr (NQ == 1) {
         quad(0, bq[0], bq[1]);
     } else {

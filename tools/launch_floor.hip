@@ -2,7 +2,11 @@
 //   empty      : no work
 //   touch64k   : 65536 lanes, one dwordx4 load + store each (the step kernel's minimum traffic)
 //   copy32B    : 65536 lanes, 2 x dwordx4 load + store (board + meta)
-// hipcc --offload-arch=gfx950 -O3 tools/launch_floor.hip -o tools/launch_floor
+//   copy32B_s  : the same, pointers in a by-value struct (read from the kernarg segment, never
+//                preloaded into SGPRs)
+// hipcc --offload-arch=gfx950 -O3 tools/launch_floor.hip -o tools/bin/launch_floor
+// hipcc ... -mllvm -amdgpu-kernarg-preload-count=8 -o tools/bin/launch_floor_pre  (leading
+//   non-aggregate kernel arguments arrive in SGPRs: no scalar-load round trip before the loads)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
@@ -20,6 +24,20 @@ __global__ __launch_bounds__(256) void k_copy(uint4* a, uint4* b) {
     y.x ^= x.z;
     a[i] = x;
     b[i] = y;
+}
+
+struct CopyArgs {
+    uint4* a;
+    uint4* b;
+    int64_t pad[6];
+};
+__global__ __launch_bounds__(256) void k_copy_s(CopyArgs A) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    uint4 x = A.a[i], y = A.b[i];
+    x.x += y.y;
+    y.x ^= x.z;
+    A.a[i] = x;
+    A.b[i] = y;
 }
 
 template <typename F>
@@ -55,5 +73,7 @@ int main() {
     printf("empty256 %.3f us\n", per_launch_us([&] { hipLaunchKernelGGL(k_empty, dim3(256), dim3(256), 0, st); }, st));
     printf("touch64k %.3f us\n", per_launch_us([&] { hipLaunchKernelGGL(k_touch, dim3(256), dim3(256), 0, st, p); }, st));
     printf("copy32B  %.3f us\n", per_launch_us([&] { hipLaunchKernelGGL(k_copy, dim3(256), dim3(256), 0, st, p, q); }, st));
+    CopyArgs ca{p, q, {0, 0, 0, 0, 0, 0}};
+    printf("copy32B_s %.3f us\n", per_launch_us([&] { hipLaunchKernelGGL(k_copy_s, dim3(256), dim3(256), 0, st, ca); }, st));
     return 0;
 }
