@@ -268,14 +268,18 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
 
 // kFull: every block is full (n % BS == 0), so there is no bounds test and every kernel argument
 // load can be issued at once (with the test, the pointer loads wait for n's round trip).
+// The four per-board pointers are leading scalar arguments (copies of A's): the library is built
+// with kernel-argument preloading, so they arrive in SGPRs and the board loads issue without first
+// waiting for a scalar load of the argument block.
 template <int MODE, bool kFull, bool kPre, int BS>
-__global__ __launch_bounds__(BS) void k_step(StepArgs A) {
+__global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2* __restrict__ meta_p,
+                                             uint4* ep_p, uint64_t* clock_p, StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     if (!kFull && i >= A.n) return;
-    const uint64_t t = load_clock(A.clock, i);
-    Board b = load_board(A.board[i]);
-    uint2 m = A.meta[i];
-    uint4 ep = kPre ? A.ep[i] : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t t = load_clock(clock_p, i);
+    Board b = load_board(board_p[i]);
+    uint2 m = meta_p[i];
+    uint4 ep = kPre ? ep_p[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
         // src/dqn_lib.py:184-188 per board: ep.x = its episode count
@@ -290,9 +294,9 @@ __global__ __launch_bounds__(BS) void k_step(StepArgs A) {
     double qs = ((kPre || kGreedy) && A.qsum) ? A.qsum[i] : 0.0;
     step_one<MODE, kPre>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
                          act, ep);
-    A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
-    if ((i & 63) == 0) A.clock[i >> 6] = t + 1u;
+    board_p[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
+    meta_p[i] = m;
+    if ((i & 63) == 0) clock_p[i >> 6] = t + 1u;
     if (kGreedy && A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
     if (A.done) A.done[i] = (uint8_t)done;
@@ -1248,15 +1252,17 @@ void launch_step_k(g2048_env* e, const StepArgs& A, hipStream_t st) {
         constexpr int BS = kStepBlockSmall;
         const unsigned grid = (unsigned)((e->n + BS - 1) / BS);
         if (e->n % BS == 0)
-            hipLaunchKernelGGL((k_step<MODE, true, kPre, BS>), dim3(grid), dim3(BS), 0, st, A);
+            hipLaunchKernelGGL((k_step<MODE, true, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
+                               A.meta, A.ep, A.clock, A);
         else
-            hipLaunchKernelGGL((k_step<MODE, false, kPre, BS>), dim3(grid), dim3(BS), 0, st, A);
+            hipLaunchKernelGGL((k_step<MODE, false, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
+                               A.meta, A.ep, A.clock, A);
     } else if (e->n % kBlock == 0) {
         hipLaunchKernelGGL((k_step<MODE, true, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock), 0,
-                           st, A);
+                           st, A.board, A.meta, A.ep, A.clock, A);
     } else {
         hipLaunchKernelGGL((k_step<MODE, false, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock),
-                           0, st, A);
+                           0, st, A.board, A.meta, A.ep, A.clock, A);
     }
 }
 

@@ -9,12 +9,17 @@
 // A row's Q does not depend on which rows share its tile (every output element sums its k in one
 // fixed order), so the greedy rows are bitwise the all-rows forward's.
 //
-// Per 16-row tile, 8 waves (two per SIMD); wave w owns output columns [w N/8, (w+1) N/8) of a
-// layer, in 16-wide blocks, on v_mfma_{f32,f64}_16x16x4.  Activations stay in LDS (two [16][K + pad] buffers); the
-// weights stream from L2 as B fragments, one "quad" of 4 k-steps ahead.  The K order is permuted
-// within each 16-wide k chunk so that every lane's A and B operands of 4 k-steps are 4
-// consecutive elements (one 16-byte LDS read / global load per 4 k-steps in f32, two in f64):
-// k-step 4q + u, lane k-group lk <-> k = 16 q + 4 lk + u.  The last layer (N = 4) runs on VALU.
+// Per tile of TB rows (64 in f32, 32 in f64: RB = TB / 16 row blocks), 8 waves (two per SIMD);
+// wave w owns output columns [w N/8, (w+1) N/8) of a layer, in 16-wide blocks, on
+// v_mfma_{f32,f64}_16x16x4, for all RB row blocks at once, so every weight fragment read from L2
+// feeds RB MFMAs (a 16-row tile re-read the 1.6 MB (f32) of weights per 16 rows and ran at 0.43 of
+// the f32 MFMA spec).  Activations stay in one LDS buffer [TB][512 + pad], each layer overwriting
+// its own input (a barrier between the last read and the first write).  The weights stream from
+// L2 as B fragments, one run of E k-steps ahead.  The K order is permuted within each 4E-wide k
+// chunk so that every lane's A and B operands of E k-steps are E consecutive elements -- 32 bytes
+// (E = 8 in f32, 4 in f64; 4 in f32's first layer, K = 16), so the four lanes of a B row read one
+// 128-byte line: k-step E q + u, lane k-group lk <-> k = 4E q + E lk + u.  The last layer (N = 4)
+// runs on VALU.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,9 +31,13 @@ namespace {
 
 constexpr int NT = 512;  // 8 waves: two per SIMD, so one wave's operand waits hide under the other's MFMAs
 constexpr int NW = NT / 64;
-constexpr int TB = 16;   // rows per tile
 constexpr int MAX_WG = 256;
 constexpr int H1 = 512, H2 = 512, H3 = 256;
+// rows per tile: as many 16-row blocks as one LDS activation buffer [TB][H1 + pad] holds
+template <typename T>
+constexpr int tile_rows() {
+    return sizeof(T) == 4 ? 64 : 32;
+}
 
 template <typename T>
 struct DenseNet {
@@ -90,25 +99,28 @@ constexpr int stride_of(int k) {
 
 template <typename T>
 struct alignas(16) Smem {
+    static constexpr int TB = tile_rows<T>();
     T x[TB * stride_of<T>(16)];
-    T a[TB * stride_of<T>(H1)];  // layer 1 out, layer 3 out
-    T b[TB * stride_of<T>(H2)];  // layer 2 out
+    T h[TB * stride_of<T>(H1)];  // every hidden layer's output, written over its input
 };
 
-// One layer: out[r][j] = relu(sum_k in[r][k] W[j][k] + bias[j]) for the tile's 16 rows; wave w
-// computes columns w N/8 .. ; K % 16 == 0, N % 128 == 0.  Ends with a barrier.
-template <typename T, int K, int N>
+// One layer: out[r][j] = relu(sum_k in[r][k] W[j][k] + bias[j]) for the tile's TB rows (row
+// stride SI in, SO out); wave w computes columns w N/8 .. ; K % 16 == 0, N % 128 == 0.
+// kInPlace: out overwrites in (a barrier after the K loop).  Ends with a barrier.
+template <typename T, int K, int N, int SI, int SO, bool kInPlace>
 __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__ W,
                                       const T* __restrict__ bias) {
     typedef typename Acc<T>::type AccT;
-    constexpr int CB = N / (16 * NW);  // 16-wide column blocks per wave
-    constexpr int E = run_of<T, K>();  // k-steps per operand run
-    constexpr int NQ = K / (4 * E);    // runs of E k-steps
-    constexpr int SI = stride_of<T>(K), SO = stride_of<T>(N);
+    constexpr int RB = tile_rows<T>() / 16;  // 16-row blocks per tile
+    constexpr int CB = N / (16 * NW);        // 16-wide column blocks per wave
+    constexpr int E = run_of<T, K>();        // k-steps per operand run
+    constexpr int NQ = K / (4 * E);          // runs of E k-steps
     const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
-    AccT acc[CB];
+    AccT acc[RB][CB];
 #pragma unroll
-    for (int c = 0; c < CB; ++c) acc[c] = AccT{0, 0, 0, 0};
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) acc[rb][c] = AccT{0, 0, 0, 0};
     // k-step E q + u of lane k-group lk is k = 4 E q + E lk + u; lane's B rows:
     // W[(w CB + c) 16 + lr][4 E q + E lk .. + E - 1]
     const T* wr = W + (size_t)(w * CB * 16 + lr) * K + E * lk;
@@ -119,67 +131,75 @@ __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__
     // one run of B fragments in flight ahead of the MFMAs; the loop is unrolled by two (static
     // buffer indices), not fully: fully unrolled, the scheduler hoisted later runs' loads and
     // the kernel spilled
-    auto quad = [&](int q, T (&cur)[CB][E], T (&nxt)[CB][E]) {
+    auto run = [&](int q, T (&cur)[CB][E], T (&nxt)[CB][E]) {
         if (q + 1 < NQ) {
 #pragma unroll
             for (int c = 0; c < CB; ++c) ldE<E>(wr + (size_t)c * 16 * K + 4 * E * (q + 1), nxt[c]);
         }
-        T av[E];
-        ldE<E>(ar + 4 * E * q, av);
+        // row block by row block: one block's A operands live at a time
 #pragma unroll
-        for (int u = 0; u < E; ++u)
+        for (int rb = 0; rb < RB; ++rb) {
+            T av[E];
+            ldE<E>(ar + rb * 16 * SI + 4 * E * q, av);
 #pragma unroll
-            for (int c = 0; c < CB; ++c) acc[c] = Acc<T>::mfma(av[u], cur[c][u], acc[c]);
+            for (int u = 0; u < E; ++u)
+#pragma unroll
+                for (int c = 0; c < CB; ++c) acc[rb][c] = Acc<T>::mfma(av[u], cur[c][u], acc[rb][c]);
+        }
         __builtin_amdgcn_sched_barrier(0);
     };
     static_assert(NQ % 2 == 0 || NQ == 1, "runs in pairs");
     if constexpr (NQ == 1) {
-        quad(0, bq[0], bq[1]);
+        run(0, bq[0], bq[1]);
     } else {
 #pragma unroll 1
         for (int q = 0; q < NQ; q += 2) {
-            quad(q, bq[0], bq[1]);
-            quad(q + 1, bq[1], bq[0]);
+            run(q, bq[0], bq[1]);
+            run(q + 1, bq[1], bq[0]);
         }
     }
+    if constexpr (kInPlace) __syncthreads();  // every wave's last read of in
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
         const int j = (w * CB + c) * 16 + lr;
         const T bj = bias[j];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const T z = acc[c][r] + bj;
-            out[Acc<T>::row(l, r) * SO + j] = z > T(0) ? z : T(0);
-        }
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const T z = acc[rb][c][r] + bj;
+                out[(rb * 16 + Acc<T>::row(l, r)) * SO + j] = z > T(0) ? z : T(0);
+            }
     }
     __syncthreads();
 }
 
-// The tile's 16 rows (in S.x) through the net; Q of row b -> q[b * 4 + a] for b < nb.
+// The tile's TB rows (in S.x) through the net; Q of row b -> q[qrow[b] * 4 + a] for b < nb.
 template <typename T>
 __device__ __forceinline__ void forward_tile(Smem<T>& S, const DenseNet<T>& P, T* q, int nb,
                                              const int32_t* qrow) {
+    constexpr int TB = tile_rows<T>(), SX = stride_of<T>(16), SH = stride_of<T>(H1);
     __syncthreads();  // S.x written
-    layer<T, 16, H1>(S.x, S.a, P.w1, P.b1);
-    layer<T, H1, H2>(S.a, S.b, P.w2, P.b2);
-    layer<T, H2, H3>(S.b, S.a, P.w3, P.b3);
-    // Linear(256, 4) on VALU: thread (row b, action a, part p) sums k = 32 p .. 32 p + 31 in two
-    // chains; the eight parts are combined in a fixed order through lane shuffles
-    const int t = threadIdx.x, b = t >> 5, a = (t >> 3) & 3, part = t & 7;
-    const T* hr = S.a + b * stride_of<T>(H3) + 32 * part;
-    const T* wr = P.w4 + a * H3 + 32 * part;
+    layer<T, 16, H1, SX, SH, false>(S.x, S.h, P.w1, P.b1);
+    layer<T, H1, H2, SH, SH, true>(S.h, S.h, P.w2, P.b2);
+    layer<T, H2, H3, SH, SH, true>(S.h, S.h, P.w3, P.b3);
+    // Linear(256, 4) on VALU: thread (row b, action a, part p) sums NP consecutive k in two
+    // chains; the parts are combined in a fixed order through lane shuffles
+    constexpr int PARTS = NT / (TB * 4), NP = H3 / PARTS;
+    const int t = threadIdx.x, part = t % PARTS, a = (t / PARTS) & 3, b = t / (4 * PARTS);
+    const T* hr = S.h + b * SH + NP * part;
+    const T* wr = P.w4 + a * H3 + NP * part;
     T e = T(0), o = T(0);
 #pragma unroll 8
-    for (int k = 0; k < 32; k += 2) {
+    for (int k = 0; k < NP; k += 2) {
         e = fma(wr[k], hr[k], e);
         o = fma(wr[k + 1], hr[k + 1], o);
     }
     T v = e + o;
-    v = v + __shfl_xor(v, 1);
-    v = v + __shfl_xor(v, 2);
-    v = v + __shfl_xor(v, 4);
+#pragma unroll
+    for (int m = 1; m < PARTS; m *= 2) v = v + __shfl_xor(v, m);
     if (part == 0 && b < nb) q[(int64_t)qrow[b] * 4 + a] = v + P.b4[a];
-    __syncthreads();  // S.a / S.x free for the next tile
+    __syncthreads();  // S.h / S.x free for the next tile
 }
 
 template <typename T>
@@ -208,10 +228,11 @@ __device__ __forceinline__ void put_row(T* xr, uint4 v) {
 }
 
 // The rows [c0, c1) of workgroup w: per window of NT rows the selected ones (all, or the greedy
-// branch's) are queued (ballot + prefix) and run in 16-row tiles; fewer than 16 left over carry
+// branch's) are queued (ballot + prefix) and run in TB-row tiles; fewer than TB left over carry
 // into the next window (the k_conv64_forward scheme).  The queue holds row offsets from c0.
 template <typename T>
 __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
+    constexpr int TB = tile_rows<T>();
     __shared__ Smem<T> S;
     __shared__ int32_t queue[NT + TB];
     __shared__ int32_t qrow[TB];
@@ -273,7 +294,7 @@ DenseNet<T> net_of(const g2048_densenet_params* p) {
 template <typename T>
 int launch(const g2048_densenet_params* p, FwdArgs<T>& F, void* stream, const char* what) {
     F.net = net_of<T>(p);
-    const int64_t tiles = (F.n + TB - 1) / TB;
+    const int64_t tiles = (F.n + tile_rows<T>() - 1) / tile_rows<T>();
     const int grid = (int)(tiles < MAX_WG ? tiles : MAX_WG);
     F.chunk = (F.n + grid - 1) / grid;
     hipLaunchKernelGGL(k_dense_forward<T>, dim3(grid), dim3(NT), 0,
