@@ -85,5 +85,45 @@ __device__ __forceinline__ double adam64(double t, double lr, double b1, double 
     return adam64_apply(adam64_coef(t, lr, b1, b2), b1, b2, eps, g, m, v, p);
 }
 
+// Fixed-order sum of the previous launch's per-workgroup gradient slabs, run in the shadow of
+// this launch's MFMA phases instead of in a reduction launch of its own.  Wave w of the block sums
+// the slabs w, w + 4, w + 8, ... (ascending) at one vector element per lane; loads go out NB at a
+// time into one of two register batches and are added one phase later, so a batch's memory round
+// trip overlaps the phase between its issue and its consume:
+//   issue(s1); phase 0; consume(s0) ... -- issue(b) / consume(b) alternate b = 0, 1 as the
+// caller's phases go by.  The order of the additions is the slab order, whatever the batching,
+// so the result is bitwise the same for any phase layout.
+template <typename V, int NB>
+struct SlabShadow {
+    const V* p = nullptr;  // this lane's element in slab 0 (null: the lane sums nothing)
+    int64_t stride = 0;    // V elements from one slab to the next
+    int next = 0;          // the next slab this wave issues
+    int nslab = 0;
+    V acc{};
+    V buf[2][NB];
+
+    __device__ __forceinline__ void init(const V* lane_p, int64_t stride_v, int nslab_, int wave) {
+        p = lane_p;
+        stride = stride_v;
+        nslab = nslab_;
+        next = wave;
+    }
+    __device__ __forceinline__ bool pending() const { return p != nullptr && next < nslab; }
+    template <int B>
+    __device__ __forceinline__ void issue() {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int g = next + 4 * u;
+            buf[B][u] = (p != nullptr && g < nslab) ? p[(int64_t)g * stride] : V{};
+        }
+        next += 4 * NB;
+    }
+    template <int B>
+    __device__ __forceinline__ void consume() {
+#pragma unroll
+        for (int u = 0; u < NB; ++u) acc += buf[B][u];
+    }
+};
+
 }  // namespace g2048
 #endif

@@ -46,6 +46,13 @@ constexpr int MAX_WG = 256;
 constexpr int P_W1 = 0, P_B1 = 256, P_W2 = 320, P_B2 = 16704, P_F1 = 16768, P_FB1 = 33152,
               P_F2 = 33216, P_FB2 = 33472, P_N = 33476;
 constexpr int SLAB = P_N + 4;  // + the loss at P_N
+// train B sums train A's slab terms (fc1, fc2, the loss: double2s [FC_D2_LO, FC_D2_HI)) in the
+// shadow of its MFMAs (SlabShadow): block g owns [FC_D2_LO + g * chunk, + chunk), one double2 per
+// lane, chunk <= 64, so the grid needs >= SHADOW_MIN_GRID blocks.  conv1 / conv2 (train B's own
+// terms) stay with k_conv64_reduce.
+constexpr int FC_D2_LO = P_F1 / 2, FC_D2_HI = P_N / 2 + 1, FC_D2 = FC_D2_HI - FC_D2_LO;
+constexpr int SHADOW_MIN_GRID = (FC_D2 + 63) / 64;
+static_assert(P_F1 % 2 == 0 && P_N % 2 == 0 && SLAB % 2 == 0, "double2 ranges");
 constexpr int PACK = 16384;    // doubles per packed 64 x 256 matrix
 constexpr int PACKU = 9 * 4096;  // doubles of the packed Winograd conv2 weights U
 // packed operands (workspace): U and fc1 of the online net, U and fc1 of the target net, the
@@ -452,6 +459,7 @@ struct TrainArgs {
     int64_t batch;
     double* dz2;   // [ntiles * TB][256]
     double* slab;  // [grid][SLAB]
+    double* pre;   // [SLAB] train A's slab terms summed by train B (null: the reduce sums them)
 };
 
 // Targets and the graded forward of the same tile in one launch (2 + 3 above): per tile the
@@ -670,6 +678,15 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     __shared__ SmemB M;
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
     const int lr = l & 15, lk = l >> 4;
+    // train A's slab terms, summed between this launch's phases (A.pre: the grid is
+    // >= SHADOW_MIN_GRID, so a block's chunk fits one double2 per lane)
+    g2048::SlabShadow<double2, 16> sh;
+    const int chunk = (FC_D2 + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int d2 = FC_D2_LO + (int)blockIdx.x * chunk + l;
+    const bool sh_on = A.pre != nullptr && l < chunk && d2 < FC_D2_HI;
+    if (A.pre)
+        sh.init(sh_on ? reinterpret_cast<const double2*>(A.slab) + d2 : nullptr, SLAB / 2,
+                (int)gridDim.x, w);
     d4 gw2[16];  // dW2 of wave w: o = 16w + 4r + lk, c = 16 cb + lr, tap; index tap * 4 + cb
 #pragma unroll
     for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
@@ -721,19 +738,32 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         CPHASE(15);
         // dW2 += dY^T im2col(d): wave w -> rows o = 16w .., K = 64 rows (p, b) in 16 k-steps;
         // dY[b][o][p] is dM at the corner xi = 0, 2, 6, 8 of p = 0, 1, 2, 3
+        auto dw2_steps = [&](int s0) {
 #pragma unroll 2
-        for (int s = 0; s < 16; ++s) {
-            const int p = s >> 2, bq = 4 * (s & 3) + lk;
-            const int xc = (p >> 1) * 6 + (p & 1) * 2;
-            const double a = M.dm[xc * DPL + bq * DSB + 16 * w + lr];
+            for (int s = s0; s < s0 + 8; ++s) {
+                const int p = s >> 2, bq = 4 * (s & 3) + lk;
+                const int xc = (p >> 1) * 6 + (p & 1) * 2;
+                const double a = M.dm[xc * DPL + bq * DSB + 16 * w + lr];
 #pragma unroll
-            for (int tap = 0; tap < 4; ++tap) {
-                const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
+                for (int tap = 0; tap < 4; ++tap) {
+                    const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
 #pragma unroll
-                for (int cb = 0; cb < 4; ++cb)
-                    gw2[tap * 4 + cb] = mfma(a, dr[16 * cb], gw2[tap * 4 + cb]);
+                    for (int cb = 0; cb < 4; ++cb)
+                        gw2[tap * 4 + cb] = mfma(a, dr[16 * cb], gw2[tap * 4 + cb]);
+                }
             }
+        };
+        // slab batches: two per tile, both inside dW2, whose operands all come from LDS -- vmcnt
+        // counts in order, so a batch in flight across dV's B-fragment loads would make every
+        // wait for them wait for the slab loads too
+        if (A.pre) sh.issue<0>();
+        dw2_steps(0);
+        if (A.pre) {
+            sh.consume<0>();
+            sh.issue<0>();
         }
+        dw2_steps(8);
+        if (A.pre) sh.consume<0>();
         CPHASE(16);
         if (tile + gridDim.x >= ntiles) {
             // last tile: conv2.weight's slab terms are final; a lane's four taps of one (o, c)
@@ -807,6 +837,12 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         }
         CPHASE(18);
     }
+    if (A.pre) {  // whatever the tiles did not cover
+        while (sh.pending()) {
+            sh.issue<0>();
+            sh.consume<0>();
+        }
+    }
     // combine in a fixed order through LDS: the 4 lane groups of a conv1 channel (dW1, db1) and
     // the 4 threads of a conv2 channel (db2); then the slab: conv1.weight [64][1][2][2],
     // conv1.bias, conv2.weight [64][64][2][2], conv2.bias
@@ -831,6 +867,16 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         const double* v2 = red + 5 * 256 + c;  // threads c, c + 64, c + 128, c + 192
         sl[P_B2 + c] = ((v2[0] + v2[64]) + v2[128]) + v2[192];
     }
+    if (A.pre) {  // the four waves' slab sums, added in wave order
+        __shared__ double2 part[3][64];
+        if (w > 0) part[w - 1][l] = sh.acc;
+        __syncthreads();
+        if (w == 0 && sh_on) {
+            const double2 a = sh.acc, b = part[0][l], c = part[1][l], d = part[2][l];
+            reinterpret_cast<double2*>(A.pre)[d2] =
+                make_double2(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y);
+        }
+    }
     CPHASE(19);
 }
 
@@ -839,6 +885,7 @@ static_assert(MAX_WG % RW == 0 && SLAB % 2 == 0, "reduction: MAX_WG / RW slabs p
 
 struct RedArgs {
     const double* slab;
+    const double* pre;  // train B's sums of train A's terms (null: summed here)
     int nslab;
     double* grad;
     double* loss;
@@ -881,8 +928,13 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             ap[h] = A.p[k][ps - base[k]];
         }
     }
+    // positions train B has summed already (fc1, fc2, the loss): one load, issued with the rest
+    const bool summed = A.pre != nullptr && pos >= P_F1;
+    const double2 pv = (summed && wave == 0 && pos <= P_N)
+                           ? *reinterpret_cast<const double2*>(A.pre + pos)
+                           : make_double2(0.0, 0.0);
     double2 r = make_double2(0.0, 0.0);
-    if (pos <= P_N) {
+    if (pos <= P_N && !summed) {
         double2 v[MAX_WG / RW];
         // (wave 0: Adam's step scalars are formed while its slab loads are in flight)
 #pragma unroll
@@ -891,13 +943,14 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             v[k] = g < A.nslab ? *reinterpret_cast<const double2*>(A.slab + (int64_t)g * SLAB + pos)
                                : make_double2(0.0, 0.0);
         }
-        if (A.adam && wave == 0) cf = g2048::adam64_coef((double)tt, A.lr, A.b1, A.b2);
 #pragma unroll
         for (int k = 0; k < MAX_WG / RW; ++k) {
             r.x += v[k].x;
             r.y += v[k].y;
         }
     }
+    // (wave 0: Adam's step scalars are formed while its loads are in flight)
+    if (A.adam && wave == 0) cf = g2048::adam64_coef((double)tt, A.lr, A.b1, A.b2);
     part[wave][lane] = r;
     __syncthreads();
     if (wave == 0) {
@@ -906,6 +959,7 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
             sum.x += part[k][lane].x;
             sum.y += part[k][lane].y;
         }
+        if (summed) sum = pv;
         const double sums[2] = {sum.x, sum.y};
         const bool sync = A.sync_every && tt % A.sync_every == 0ull;
         double np[2] = {0.0, 0.0};
@@ -1137,8 +1191,8 @@ extern "C" G2048_API int g2048_convnet_forward_greedy_f64(
 extern "C" G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch) {
     if (batch <= 0) return 0;
     const int64_t tiles = (batch + TB - 1) / TB;
-    // the packed operands | the next-step word (+ pad) | slabs | dZ2 rows
-    return WS_SLAB + (int64_t)grid_of(batch) * SLAB + tiles * TB * 256;
+    // the packed operands | the next-step word (+ pad) | slabs | dZ2 rows | train B's slab sums
+    return WS_SLAB + (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + SLAB;
 }
 
 extern "C" G2048_API int g2048_convnet_update_f64(
@@ -1164,6 +1218,7 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     unsigned long long* step_next = reinterpret_cast<unsigned long long*>(workspace + WS_STEP);
     double* slab = workspace + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
+    double* pre = grid >= SHADOW_MIN_GRID ? dz2 + ((batch + TB - 1) / TB) * TB * 256 : nullptr;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
     // with Adam folded in, the packed operands are current (g2048_convnet_pack_f64 or the
@@ -1207,11 +1262,13 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     A.batch = batch;
     A.dz2 = dz2;
     A.slab = slab;
+    A.pre = pre;
     hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, st, FA);
     hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, st, A);
 
     RedArgs D;
     D.slab = slab;
+    D.pre = pre;
     D.nslab = grid;
     D.grad = grad_out;
     D.loss = loss_out;

@@ -74,6 +74,7 @@ int main(int argc, char** argv) {
     unsigned long long* step_next = reinterpret_cast<unsigned long long*>(ws + WS_STEP);
     double* slab = ws + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
+    double* pre = grid >= SHADOW_MIN_GRID ? dz2 + tiles * TB * 256 : nullptr;
 
     PackArgs P{w[0][2], w[0][4], w[1][2], w[1][4], pk};
     Ring R{reinterpret_cast<const uint4*>(s), reinterpret_cast<const uint4*>(s2), a, d, r, count};
@@ -103,8 +104,10 @@ int main(int argc, char** argv) {
     A.batch = B;
     A.dz2 = dz2;
     A.slab = slab;
+    A.pre = pre;
     RedArgs D{};
     D.slab = slab;
+    D.pre = pre;
     D.nslab = grid;
     D.grad = grad;
     D.loss = loss;
