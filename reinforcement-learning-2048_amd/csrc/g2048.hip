@@ -117,6 +117,16 @@ __device__ __forceinline__ uint64_t load_clock(const uint64_t* clock, int64_t i)
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
+// k_step's form: the group index is wave-uniform by construction (a wave never straddles two
+// groups and its first live lane is 64-aligned), so the address is an SGPR value and the load is a
+// scalar one -- a shorter round trip than a vector load + readfirstlane, and the first one on the
+// step's critical path (the Philox counter needs t).
+template <int BS>
+__device__ __forceinline__ uint64_t load_clock_s(const uint64_t* clock) {
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+    return clock[(int64_t)blockIdx.x * (BS / 64) + wave];
+}
+
 // Ring row of step t (t mod rows) -- wave-uniform.
 __device__ __forceinline__ uint64_t ring_row(uint64_t t, int64_t rows) {
     return (t >> 32) ? (t % (uint64_t)rows) : (uint64_t)((uint32_t)t % (uint32_t)rows);
@@ -268,15 +278,23 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
 
 // kFull: every block is full (n % BS == 0), so there is no bounds test and every kernel argument
 // load can be issued at once (with the test, the pointer loads wait for n's round trip).
-// The four per-board pointers are leading scalar arguments (copies of A's): the library is built
-// with kernel-argument preloading, so they arrive in SGPRs and the board loads issue without first
-// waiting for a scalar load of the argument block.
+// The four per-board pointers and the scalars the Philox draw needs first (board offset, seed,
+// p(4) threshold, flags) are leading scalar arguments (copies of A's): the library is built with
+// kernel-argument preloading (16 SGPRs), so they arrive in SGPRs and neither the board loads nor
+// the draw wait for a scalar load of the argument block.
 template <int MODE, bool kFull, bool kPre, int BS>
 __global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2* __restrict__ meta_p,
-                                             uint4* ep_p, uint64_t* clock_p, StepArgs A) {
+                                             uint4* ep_p, uint64_t* clock_p, uint64_t board_offset,
+                                             uint32_t seed_lo, uint32_t seed_hi,
+                                             uint32_t p4_thresh, uint32_t flags, StepArgs A) {
     const int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
     if (!kFull && i >= A.n) return;
-    const uint64_t t = load_clock(clock_p, i);
+    A.board_offset = board_offset;
+    A.seed_lo = seed_lo;
+    A.seed_hi = seed_hi;
+    A.p4_thresh = p4_thresh;
+    A.flags = flags;
+    const uint64_t t = load_clock_s<BS>(clock_p);
     Board b = load_board(board_p[i]);
     uint2 m = meta_p[i];
     uint4 ep = kPre ? ep_p[i] : make_uint4(0u, 0u, 0u, 0u);
@@ -292,7 +310,7 @@ __global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2*
     uint32_t done, legal, act;
     constexpr bool kGreedy = MODE == MODE_EG_F32 || MODE == MODE_EG_F64;
     double qs = ((kPre || kGreedy) && A.qsum) ? A.qsum[i] : 0.0;
-    step_one<MODE, kPre>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
+    step_one<MODE, kPre>(A, i, board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
                          act, ep);
     board_p[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
     meta_p[i] = m;
@@ -1253,16 +1271,20 @@ void launch_step_k(g2048_env* e, const StepArgs& A, hipStream_t st) {
         const unsigned grid = (unsigned)((e->n + BS - 1) / BS);
         if (e->n % BS == 0)
             hipLaunchKernelGGL((k_step<MODE, true, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
-                               A.meta, A.ep, A.clock, A);
+                               A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                               A.p4_thresh, A.flags, A);
         else
             hipLaunchKernelGGL((k_step<MODE, false, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
-                               A.meta, A.ep, A.clock, A);
+                               A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                               A.p4_thresh, A.flags, A);
     } else if (e->n % kBlock == 0) {
         hipLaunchKernelGGL((k_step<MODE, true, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock), 0,
-                           st, A.board, A.meta, A.ep, A.clock, A);
+                           st, A.board, A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                           A.p4_thresh, A.flags, A);
     } else {
         hipLaunchKernelGGL((k_step<MODE, false, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock),
-                           0, st, A.board, A.meta, A.ep, A.clock, A);
+                           0, st, A.board, A.meta, A.ep, A.clock, A.board_offset, A.seed_lo,
+                           A.seed_hi, A.p4_thresh, A.flags, A);
     }
 }
 

@@ -252,7 +252,7 @@ __device__ void forward(Smem& M, const SmallW& W, const Packed& pk, double* q) {
         la9(aa[0], 0);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
-            if (s + 1 < 16) la9(aa[(s + 1) & 1], s + 1);
+            la9(aa[s & 1], s);
             if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
 #pragma unroll
             for (int x = 0; x < 9; ++x) acc[x] = mfma(aa[s & 1][x], bb[s % 3][x], acc[x]);
@@ -523,7 +523,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
             M.r[t] = rj;
             M.disc[t] = disc;
         }
-        fetch(tile + gridDim.x);
         CPHASE(1);
         // k = 0: Q_online(s') -> q2 (Double DQN only); 1: Q_target(s') -> q; 2: Q_online(s) -> q
 #pragma unroll 1
@@ -554,6 +553,10 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
             }
             forward(M, M.sw[k == 1 ? 1 : 0], k == 1 ? T.ptg : T.pon, k == 0 ? M.q2 : M.q);
         }
+        // the next tile's rows, issued here and not at the top of the tile: vmcnt counts in
+        // order, so the forwards' waits for their L2-resident B fragments would also wait for
+        // these replay-ring (HBM) loads; the loss, fc2 and dWf1 phases wait on LDS only
+        fetch(tile + gridDim.x);
         CPHASE(8);
         if (t < TB) {
             double dq = 0.0, ls = 0.0;
@@ -599,13 +602,18 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
             gfb1 += acc;
         }
         CPHASE(10);
-        // dWf1 += dZ3^T H2: wave w -> rows j = 16w .., 16 column blocks, K = 16 boards
+        // dWf1 += dZ3^T H2: wave w -> rows j = 16w .., 16 column blocks, K = 16 boards.  A
+        // step's 17 LDS operands are read together (one wait per 16 MFMAs, not one per two)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const double a = M.h3[(4 * s + lk) * H3S + 16 * w + lr];
+            double op[17];
+            op[0] = M.h3[(4 * s + lk) * H3S + 16 * w + lr];
 #pragma unroll
-            for (int cb = 0; cb < 16; ++cb)
-                gf1[cb] = mfma(a, M.h2[(4 * s + lk) * HS + 16 * cb + lr], gf1[cb]);
+            for (int cb = 0; cb < 16; ++cb) op[1 + cb] = M.h2[(4 * s + lk) * HS + 16 * cb + lr];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int cb = 0; cb < 16; ++cb) gf1[cb] = mfma(op[0], op[1 + cb], gf1[cb]);
+            __builtin_amdgcn_sched_barrier(0);
         }
         CPHASE(11);
         // dH2 = dZ3 Wf1 (masked by relu'(H2)) -> dZ2: wave w -> columns 64w .. 64w+63
@@ -619,10 +627,13 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
 #pragma unroll
                 for (int cb = 0; cb < 4; ++cb) b[cb] = bp[(cb * 16 + s) * 64];
             };
-            auto mm4 = [&](const double(&b)[4], int s) {
-                const double a = M.h3[lr * H3S + 4 * s + lk];
+            // A (dZ3 row lr) of all 16 k-steps read up front: one LDS wait, not one per step
+            double ah[16];
 #pragma unroll
-                for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(a, b[cb], acc[cb]);
+            for (int s = 0; s < 16; ++s) ah[s] = M.h3[lr * H3S + 4 * s + lk];
+            auto mm4 = [&](const double(&b)[4], int s) {
+#pragma unroll
+                for (int cb = 0; cb < 4; ++cb) acc[cb] = mfma(ah[s], b[cb], acc[cb]);
             };
             double bb[3][4];
             ld4(bb[0], 0);
@@ -680,7 +691,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     const int lr = l & 15, lk = l >> 4;
     // train A's slab terms, summed between this launch's phases (A.pre: the grid is
     // >= SHADOW_MIN_GRID, so a block's chunk fits one double2 per lane)
-    g2048::SlabShadow<double2, 16> sh;
+    g2048::SlabShadow<double2, 8> sh;
     const int chunk = (FC_D2 + (int)gridDim.x - 1) / (int)gridDim.x;
     const int d2 = FC_D2_LO + (int)blockIdx.x * chunk + l;
     const bool sh_on = A.pre != nullptr && l < chunk && d2 < FC_D2_HI;
@@ -731,39 +742,47 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
                 for (int x = 0; x < 9; ++x) dst[x * DPL] = m[x];
             }
         }
-        fetch(tile + gridDim.x);
         CPHASE(14);
         const uint64_t mask = conv1_mfma<false>(M.x, M.d, M.sw);
         __syncthreads();
+        // the next tile's row and dZ2 (HBM), issued at the start of dW2, whose operands all come
+        // from LDS: vmcnt counts in order, so issued before conv1 (as before) they made dV's waits
+        // for its L2-resident B fragments wait for them too
+        fetch(tile + gridDim.x);
         CPHASE(15);
         // dW2 += dY^T im2col(d): wave w -> rows o = 16w .., K = 64 rows (p, b) in 16 k-steps;
         // dY[b][o][p] is dM at the corner xi = 0, 2, 6, 8 of p = 0, 1, 2, 3
-        auto dw2_steps = [&](int s0) {
-#pragma unroll 2
-            for (int s = s0; s < s0 + 8; ++s) {
-                const int p = s >> 2, bq = 4 * (s & 3) + lk;
-                const int xc = (p >> 1) * 6 + (p & 1) * 2;
-                const double a = M.dm[xc * DPL + bq * DSB + 16 * w + lr];
+        // The 17 LDS operands of a k-step (dY column, four taps x four channel blocks of d) are
+        // read into registers together, so a step's 16 MFMAs issue back to back after one LDS
+        // wait instead of each waiting on its own round trip (the compiler's interleaved form:
+        // one ds_read + lgkmcnt(0) per MFMA, ~150 cycles per f64 MFMA); a scheduling barrier per
+        // step, unrolled by four (fully unrolled, or reading a step ahead,
+        // the kernel spills).
+        auto lds17 = [&](double(&v)[17], int s) {
+            const int p = s >> 2, bq = 4 * (s & 3) + lk;
+            const int xc = (p >> 1) * 6 + (p & 1) * 2;
+            v[0] = M.dm[xc * DPL + bq * DSB + 16 * w + lr];
 #pragma unroll
-                for (int tap = 0; tap < 4; ++tap) {
-                    const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
+            for (int tap = 0; tap < 4; ++tap) {
+                const double* dr = M.d + pos_of(p, tap) * DPL + bq * DSB + lr;
 #pragma unroll
-                    for (int cb = 0; cb < 4; ++cb)
-                        gw2[tap * 4 + cb] = mfma(a, dr[16 * cb], gw2[tap * 4 + cb]);
-                }
+                for (int cb = 0; cb < 4; ++cb) v[1 + tap * 4 + cb] = dr[16 * cb];
             }
         };
-        // slab batches: two per tile, both inside dW2, whose operands all come from LDS -- vmcnt
+        // slab batches: four per tile, all inside dW2, whose operands all come from LDS -- vmcnt
         // counts in order, so a batch in flight across dV's B-fragment loads would make every
         // wait for them wait for the slab loads too
-        if (A.pre) sh.issue<0>();
-        dw2_steps(0);
-        if (A.pre) {
-            sh.consume<0>();
-            sh.issue<0>();
+#pragma unroll 4
+        for (int s = 0; s < 16; ++s) {
+            if (A.pre && (s & 3) == 0) sh.issue<0>();
+            double op[17];
+            lds17(op, s);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) gw2[k] = mfma(op[0], op[1 + k], gw2[k]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (A.pre && (s & 3) == 3) sh.consume<0>();
         }
-        dw2_steps(8);
-        if (A.pre) sh.consume<0>();
         CPHASE(16);
         if (tile + gridDim.x >= ntiles) {
             // last tile: conv2.weight's slab terms are final; a lane's four taps of one (o, c)
@@ -794,12 +813,21 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             double bb[3][9];
             ld9(bb[0], 0);
             ld9(bb[1], 1);
-#pragma unroll
-            for (int s = 0; s < 16; ++s) {
-                if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
+            // A (dM) of a step read into registers together: one LDS wait per step, not one per
+            // MFMA (a step ahead needs 36 more VGPRs: spills)
+            auto la9 = [&](double(&a)[9], int s) {
                 const double* ar = M.dm + lr * DSB + 4 * s + lk;
 #pragma unroll
-                for (int x = 0; x < 9; ++x) dv[x] = mfma(ar[x * DPL], bb[s % 3][x], dv[x]);
+                for (int x = 0; x < 9; ++x) a[x] = ar[x * DPL];
+            };
+            double aa[2][9];
+#pragma unroll
+            for (int s = 0; s < 16; ++s) {
+                la9(aa[s & 1], s);
+                if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int x = 0; x < 9; ++x) dv[x] = mfma(aa[s & 1][x], bb[s % 3][x], dv[x]);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }

@@ -57,14 +57,9 @@ def timed(g, label):
 
 
 variants = {"all": mk(N.ptr(r), N.ptr(d), N.ptr(lg)), "none": mk(None, None, None),
-            "reward": mk(N.ptr(r), None, None), "done+legal": mk(None, N.ptr(d), N.ptr(lg))}
+            "reward": mk(N.ptr(r), None, None), "done+legal": mk(None, N.ptr(d), N.ptr(lg)),
+            "legal": mk(None, None, N.ptr(lg)), "reward+done": mk(N.ptr(r), N.ptr(d), None)}
 for name, f in variants.items():
     timed(side_stream_graph(f), name)
 timed(bench.capture(lambda: env.step(None, reward=r, done=d, legal=lg), 100), "bench.capture")
 
-# bench.py's own env measurement, in this process
-import argparse  # noqa: E402
-args = argparse.Namespace(boards=n, seed=0x2048, warmup=200, steps=2000, graph_steps=100)
-for _ in range(2):
-    res = bench.bench_env(args, 1, 0, dev)
-    print("bench.bench_env", round(res["ev_s"] / args.steps * 1e6, 3), "us/step", flush=True)
