@@ -784,21 +784,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             if (A.pre && (s & 3) == 3) sh.consume<0>();
         }
         CPHASE(16);
-        if (tile + gridDim.x >= ntiles) {
-            // last tile: conv2.weight's slab terms are final; a lane's four taps of one (o, c)
-            // are 32 contiguous bytes (torch order o, c, tap), two 16-byte stores, so 16 lanes
-            // write 512 B in a row; they drain while dV's MFMAs run
-            double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    double2* dst = reinterpret_cast<double2*>(
-                        sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
-                    dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
-                    dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
-                }
-        }
         // dV_xi: wave w -> channels c = 16w .., K = 64 o in 16 k-steps, nine chains; B two
         // steps ahead
         d4 dv[9];
@@ -864,6 +849,23 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             }
         }
         CPHASE(18);
+    }
+    {
+        // conv2.weight's slab terms, after the last tile: vmcnt counts in order, so stores issued
+        // before dV (the round-3 placement, meant to drain under its MFMAs) made every wait for
+        // dV's B fragments wait for 33 MB of slab stores to be acknowledged.  A lane's four taps
+        // of one (o, c) are 32 contiguous bytes (torch order o, c, tap), two 16-byte stores, so
+        // 16 lanes write 512 B in a row
+        double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double2* dst = reinterpret_cast<double2*>(
+                    sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
+                dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
+                dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
+            }
     }
     if (A.pre) {  // whatever the tiles did not cover
         while (sh.pending()) {

@@ -98,6 +98,13 @@ class DQNLearner:
         # (g2048_densenet_forward[_greedy]) instead of torch's four GEMMs over every board
         self._dfwd = (qnet.DenseForward(self.model) if not self.fused and self.device.type == "cuda"
                       and qnet.is_dense_ref(self.model) else None)
+        # ... and, in float64, the update's two no-grad forwards (Q_online(s'), Q_target(s') of
+        # the Bellman target, src/dqn_lib.py:125-144) as the same HIP launch on the sampled s'
+        # rows: only Q_online(s) goes through torch autograd (B = 8192: 1.44 -> 1.14 ms per
+        # update).  Not in float32: its 64-row tiles put B = 8192 rows on 128 of the 256 CUs,
+        # slower than torch's two GEMM forwards (0.74 -> 0.80 ms).
+        self._dfwd_tg = (qnet.DenseForward(self.target)
+                         if self._dfwd is not None and self.dtype == torch.float64 else None)
         if self.fused:
             self._p_on = None if self.f64 else qnet.net_params(self.model)
             self._p_tgt = None if self.f64 else qnet.net_params(self.target)
@@ -147,6 +154,13 @@ class DQNLearner:
                       self.use_double_dqn, self.sample_seed, idx_in,
                       grad_out=self.grad_flat, loss_out=self.last_loss)
             return
+        elif self._dfwd_tg is not None:
+            s, a, r, _, d, _ = self.replay.sample_encode(self.B, self.dtype, idx=idx, want_s2=False)
+            y = dqn_lib.targets_from_q(self._dfwd(self.replay.s2, idx),
+                                       self._dfwd_tg(self.replay.s2, idx), r, d, self.gamma,
+                                       self.use_double_dqn)
+            q = self.model(self._layout(s)).gather(1, a[:, None])[:, 0]
+            loss = ((q - y) ** 2).sum() if self.loss_fn is None else self.loss_fn(q, y)
         else:
             s, a, r, s2, d = dqn_lib.sample_experiences(self.B, self.replay, self.device, None,
                                                         self._layout, dtype=self.dtype, idx=idx)
