@@ -53,8 +53,14 @@ class _LinearSplitK(torch.autograd.Function):
                            x.reshape(s, m // s, -1)).sum(0)
         else:
             gw = gy.t() @ x
+        # the bias gradient as a GEMM (ones[1, m] @ dY) rather than torch's sum over dim 0: in
+        # replays of the captured update that reduction returned stale, deterministic garbage
+        # for the conv and fc biases (weights' gradients right, eager runs right) once another
+        # learner's work ran between the replays (tests/test_learner_gpu.py
+        # test_fused_f64_equals_torch_path at B = 4096)
+        gb = torch.mm(gy.new_ones(1, m), gy)[0] if ctx.needs_input_grad[2] else None
         # b is None for a bias-free layer: autograd takes no gradient for a non-tensor input
-        return gx, gw, (gy.sum(0) if ctx.needs_input_grad[2] else None)
+        return gx, gw, gb
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None) -> torch.Tensor:

@@ -236,25 +236,27 @@ def test_fused_f64_matches_reference(G, golden_dir, net):
     np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
 
 
+@pytest.mark.parametrize("batch", [1000, 4096])
 @pytest.mark.parametrize("double_dqn", [True, False])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
-def test_fused_f64_equals_torch_path(G, net, double_dqn):
+def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
     """Three fused float64 updates (Philox sampler, Adam, target sync every 2) against the torch
     float64 learner on the same rows: losses and gradients to 1e-9 relative; weights to 1e-6
     absolute (Adam divides by |g| + eps, so a parameter whose summed gradient nearly cancels
     (|g| ~ eps) moves by a step that depends on g's last bits -- the two paths sum the rows in
-    different orders)."""
+    different orders).  B = 4096 puts the conv update on 256 workgroups, where train B sums
+    train A's slab terms itself (SlabShadow) and the reduce reads them summed."""
     from g2048.learner import DQNLearner
 
     n = 2048
     env = G.VecEnv2048(n, seed=3, device=DEV)
     rb = G.ReplayBuffer(16 * n, device=DEV)
     env.rollout(16, replay=rb)
-    a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=1000, target_sync_every=2,
+    a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=batch, target_sync_every=2,
                    seed=9, use_double_dqn=double_dqn)
     assert a.fused and a.f64
-    rows = torch.zeros(1000, dtype=torch.int64, device=DEV)  # (captured by b's graphs)
-    b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=1000, target_sync_every=2,
+    rows = torch.zeros(batch, dtype=torch.int64, device=DEV)  # (captured by b's graphs)
+    b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=batch, target_sync_every=2,
                    seed=9, loss_fn=torch.nn.L1Loss(reduction="sum"),  # any torch-path learner
                    use_double_dqn=double_dqn)
     b.loss_fn = None  # ... run with the MSE(sum) loss, fed the fused learner's rows
@@ -411,3 +413,82 @@ def test_torch_path_vanilla_and_b5000_match_reference(G, golden_dir, name, net, 
     else:
         np.testing.assert_allclose(after[g["grad_sel"]], g["params_after_sampled"], rtol=1e-10,
                                    atol=1e-10)
+
+
+@pytest.mark.parametrize("double_dqn", [True, False])
+def test_dense_ref_f64_hip_targets(G, double_dqn):
+    """The torch-path learner of the reference dense net in float64 forms the Bellman target's
+    two no-grad forwards with the HIP dense forward (DQNLearner._dfwd_tg): loss and gradient of
+    three updates against torch autograd through dqn_lib.dqn_loss on the same rows and the same
+    pre-update weights, to 1e-9 relative."""
+    import copy
+
+    from g2048 import dqn_lib
+    from g2048.learner import DQNLearner
+
+    n = 2048
+    env = G.VecEnv2048(n, seed=13, device=DEV)
+    rb = G.ReplayBuffer(8 * n, device=DEV)
+    env.rollout(8, replay=rb)
+    rows = torch.zeros(2000, dtype=torch.int64, device=DEV)
+    L = DQNLearner(rb, net="dense", dtype=torch.float64, batch_size=2000, target_sync_every=2,
+                   seed=4, use_double_dqn=double_dqn)
+    assert not L.fused and L._dfwd_tg is not None
+    L.sampler = lambda B, r: rows
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    for k in range(3):
+        rows.copy_(torch.randint(0, 8 * n, (2000,), device=DEV, generator=gen))
+        m0, t0 = copy.deepcopy(L.model), copy.deepcopy(L.target)
+        L.update()
+        s, a, r, s2, d = dqn_lib.sample_experiences(2000, rb, DEV, None,
+                                                    dqn_lib.extract_samples_dense,
+                                                    dtype=torch.float64, idx=rows)
+        loss, _, _ = dqn_lib.dqn_loss(m0, t0, s, a, r, s2, d, L.gamma, double_dqn, None)
+        loss.backward()
+        torch.cuda.synchronize()
+        assert abs(float(L.last_loss) - float(loss)) <= 1e-9 * abs(float(loss)), k
+        gref = torch.cat([p.grad.reshape(-1) for p in m0.parameters()])
+        assert float((L.grad_flat - gref).norm()) <= 1e-9 * float(gref.norm()), k
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("net", ["dense", "conv"])
+def test_torch_path_graph_replays_match_eager(G, net, dtype):
+    """Back-to-back replays of the torch-path learner's captured update against the same learner
+    run eagerly on the same rows and weights, at B = 8192: every parameter's gradient to 1e-9
+    relative on every update.  (torch's dim-0 sum for the bias gradients gave stale results in
+    replays of the captured update -- the weights' gradients stayed right -- so nets.Linear
+    forms them as a GEMM.)"""
+    from g2048.learner import DQNLearner
+
+    n, B = 4096, 8192
+    env = G.VecEnv2048(n, seed=17, device=DEV)
+    rb = G.ReplayBuffer(8 * n, device=DEV)
+    env.rollout(8, replay=rb)
+    rows = torch.zeros(B, dtype=torch.int64, device=DEV)
+    kw = dict(net=net, dtype=dtype, batch_size=B, target_sync_every=2, seed=7,
+              loss_fn=torch.nn.L1Loss(reduction="sum"),  # any torch-path learner ...
+              sampler=lambda b, r: rows)
+    a = DQNLearner(rb, graph=True, **kw)
+    b = DQNLearner(rb, graph=False, **kw)
+    assert not a.fused and not b.fused
+    a.loss_fn = b.loss_fn = None  # ... run with the MSE(sum) loss
+    b.model.load_state_dict(a.model.state_dict())
+    b.target.load_state_dict(a.target.state_dict())
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    sizes = [p.numel() for p in a.model.parameters()]
+    tol = 1e-9 if dtype == torch.float64 else 1e-4
+    for k in range(4):
+        rows.copy_(torch.randint(0, 8 * n, (B,), device=DEV, generator=gen))
+        a.update()
+        b.update()
+        torch.cuda.synchronize()
+        off = 0
+        for i, sz in enumerate(sizes):
+            ga, gb = a.grad_flat[off:off + sz], b.grad_flat[off:off + sz]
+            assert float((ga - gb).norm()) <= tol * float(gb.norm()), (k, i)
+            off += sz
+        with torch.no_grad():  # the next update starts from the same weights on both sides
+            for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
+                            list(b.model.parameters()) + list(b.target.parameters())):
+                p.copy_(q)
