@@ -47,6 +47,16 @@ constexpr int SL_W2 = 0, SL_WF1 = 16384, SL_SMALL = 32768, SL_LOSS = SL_SMALL + 
 constexpr int SLAB = 33480;
 static_assert(SL_LOSS == P_TOTAL && SLAB % 4 == 0, "slab layout");
 constexpr int TMAXT = 4;               // tiles per workgroup (B <= 16384 on 256 workgroups)
+// k_conv_train_bwd sums k_conv_train_fwd's slab terms in the shadow of its phases (SlabShadow):
+// block g owns the float4s [g * chunk, (g + 1) * chunk) of the slab, one per lane, chunk <= 64, so
+// the grid needs >= SHADOW_MIN_GRID blocks.  conv1's weight and bias (float4s [C1_F4_LO,
+// C1_F4_HI)) are train bwd's own terms and stay with k_reduce_slabs, spread over C1_BLOCKS blocks
+// of C1_PER_BLOCK float4s each.
+constexpr int SLAB_F4 = SLAB / 4;
+constexpr int SHADOW_MIN_GRID = (SLAB_F4 + 63) / 64;
+constexpr int C1_F4_LO = SL_SMALL / 4, C1_F4_HI = (SL_SMALL + 320) / 4;
+constexpr int C1_PER_BLOCK = 16, C1_BLOCKS = (C1_F4_HI - C1_F4_LO) / C1_PER_BLOCK;
+static_assert(SL_SMALL % 4 == 0 && (C1_F4_HI - C1_F4_LO) % C1_PER_BLOCK == 0, "conv1 float4 ranges");
 constexpr int DM_TILE = 9 * S * 64;    // dM floats per tile in the workspace: [xi][b][o]
 
 // k_conv_train_fwd LDS carve (floats)
@@ -89,6 +99,7 @@ struct TrainArgs {
     int64_t batch;
     float* slab;             // [gridDim.x][SLAB]
     float* dm;               // [ntiles][DM_TILE]
+    float* pre;              // [SLAB] train fwd's slab terms summed by train bwd (null: the reduce)
     unsigned long long* step;  // optional update counter, += 1 by one thread (nullable)
 };
 
@@ -430,9 +441,19 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
 
 __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     __shared__ __attribute__((aligned(16))) float lds[K2_FLOATS];
-    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, l16 = lane & 15;
+    const int t = threadIdx.x, lane = t & 63, g = lane >> 4, l16 = lane & 15, wave = t >> 6;
     const int64_t ntiles = (A.batch + S - 1) / S;
     const int T = tiles_here(ntiles);
+    // train fwd's slab terms, summed between this launch's phases (A.pre: the grid is
+    // >= SHADOW_MIN_GRID, so a block's chunk fits one float4 per lane)
+    g2048::SlabShadow<float4, 8> sh;
+    const int chunk = (SLAB_F4 + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int f4 = (int)blockIdx.x * chunk + lane;
+    const bool sh_on =
+        A.pre != nullptr && lane < chunk && f4 < SLAB_F4 && (f4 < C1_F4_LO || f4 >= C1_F4_HI);
+    if (A.pre)
+        sh.init(sh_on ? reinterpret_cast<const float4*>(A.slab) + f4 : nullptr, SLAB_F4,
+                (int)gridDim.x, wave);
     // dM of tiles k and k + 1 -> the two LDS buffers [xi][b][VS] in one memory round trip
     // (coalesced float4: 9 per thread per tile)
     auto copy_pair = [&](int k) {
@@ -465,6 +486,10 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     lds_barrier();
     TPHASE_BEGIN();
     TPHASE(8);
+    // slab batches: phase p of a tile (three dV groups, then dh1) issues batch (p + 1) & 1 and
+    // adds batch p & 1 (this kernel loads no other global data after its first pair of tiles, so
+    // no wait below is held up by them)
+    if (A.pre) sh.issue<0>();
     for (int k = 0; k < T; ++k) {
         float* dms = lds + K2_DM + (k & 1) * 9 * VXI;
         if ((k & 1) == 0 && k > 0) {
@@ -481,6 +506,10 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
         for (int xi = 0; xi < 9; ++xi) acc[xi] = f32x4{0, 0, 0, 0};
 #pragma unroll
         for (int grp = 0; grp < 3; ++grp) {
+            if (A.pre) {
+                if (grp & 1) sh.issue<0>();
+                else sh.issue<1>();
+            }
             f32x4 a4[3][4];
 #pragma unroll
             for (int e = 0; e < 3; ++e) {
@@ -494,8 +523,13 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
                 for (int e = 0; e < 3; ++e)
                     acc[3 * grp + e] = __builtin_amdgcn_mfma_f32_16x16x4f32(
                         a4[e][kk >> 2][kk & 3], R.u[3 * grp + e][kk], acc[3 * grp + e], 0, 0, 0);
+            if (A.pre) {
+                if (grp & 1) sh.consume<1>();
+                else sh.consume<0>();
+            }
         }
         TPHASE(10);
+        if (A.pre) sh.issue<0>();
         // ---- dh1 = B dV B^T, relu'(h1), dW1 / db1 for (board 4g + i, channel c)
         const float* xs = lds + K2_X + k * S * 16;
         f32x4 pre[9];
@@ -532,6 +566,14 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
                 }
             }
         }
+        if (A.pre) sh.consume<1>();
+    }
+    if (A.pre) {  // the batch still in flight, then whatever the tiles did not cover
+        sh.consume<0>();
+        while (sh.pending()) {
+            sh.issue<0>();
+            sh.consume<0>();
+        }
     }
     TPHASE(11);
     // ---- fixed-order sum over the 4 lane groups that share channel c -> the slab
@@ -549,6 +591,17 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
             const float v = ((rw[e] + rw[80 + e]) + rw[160 + e]) + rw[240 + e];
             if (e < 4) slab[SL_SMALL + t * 4 + e] = v;  // w1[c][0][kh][kw]
             else slab[SL_SMALL + 256 + t] = v;          // b1
+        }
+    }
+    if (A.pre) {  // the four waves' slab sums, added in wave order
+        __shared__ float4 part[3][64];
+        if (wave > 0) part[wave - 1][lane] = sh.acc;
+        __syncthreads();
+        if (wave == 0 && sh_on) {
+            const float4 a = sh.acc, b = part[0][lane], c = part[1][lane], d = part[2][lane];
+            reinterpret_cast<float4*>(A.pre)[f4] =
+                make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
+                            ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
         }
     }
 }
@@ -595,17 +648,28 @@ struct ReduceAdam {
 // Deterministic slab reduction: a block owns 256 slab positions (a float4 per lane); its 16
 // waves sum the slabs g = wave, wave + 16, ... (16 independent float4 loads per lane in flight:
 // one memory round trip per 256 slabs), then the 16 partials are added in a fixed order.
+// With `pre` (train bwd summed train fwd's terms): blocks [0, nb_pre) take their float4s from
+// `pre` (one load by wave 0; conv1's float4s are skipped), and blocks nb_pre + c sum conv1's
+// float4s [C1_F4_LO + 16 c, + 16) over the slabs -- lane (q = l % 16, h = l / 16) of wave w sums
+// the slabs j, j + 64, ... (j = 4 w + h), then 16 threads add the 64 partials in j order -- so
+// conv1's 328 KB of slab terms are read by five blocks, not by two whole-slab-width ones.
 constexpr int RW = 16;  // waves per reduction block
 
 __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int nslab,
+                                                          const float* pre, int nb_pre,
                                                           float* grad, float* loss, ReduceAdam R) {
     __shared__ float4 part[RW][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int p4 = blockIdx.x * 64 + lane;  // float4 index within a slab
+    const bool c1 = pre != nullptr && (int)blockIdx.x >= nb_pre;
+    const int p4 = c1 ? C1_F4_LO + ((int)blockIdx.x - nb_pre) * C1_PER_BLOCK + (lane & 15)
+                      : (int)blockIdx.x * 64 + lane;  // float4 index within a slab
     const bool in = p4 * 4 <= SL_LOSS;
-    // Adam operands of this lane's 4 positions (wave 0), loaded with the slabs: they do not
-    // depend on the sums, so the update costs no memory round trip of its own.
-    const bool adam = R.on && wave == 0 && in;
+    const bool from_pre = pre != nullptr && !c1;
+    const bool skip = from_pre && p4 >= C1_F4_LO && p4 < C1_F4_HI;  // a conv1 block's
+    const bool fin = wave == 0 && in && !skip && (!c1 || lane < C1_PER_BLOCK);
+    // Adam operands of this lane's 4 positions (the finishing lanes), loaded with the slabs:
+    // they do not depend on the sums, so the update costs no memory round trip of its own.
+    const bool adam = R.on && fin;
     int kt[4], ei[4];
     float am[4], av[4], ap[4];
     unsigned long long t = 0;
@@ -628,52 +692,88 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
             ap[e] = R.p[k][ei[e]];
         }
     }
+    const float4 pv = (from_pre && fin) ? reinterpret_cast<const float4*>(pre)[p4]
+                                        : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    // Adam's step scalars (two f64 pow) formed while the slab loads are in flight, not after the
-    // barrier on the update's critical path
-    g2048::AdamCoef c{};
-    for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
-        float4 r[16];
+    if (c1) {
+        const int j = 4 * wave + (lane >> 4);
+        for (int g0 = 0; g0 < nslab; g0 += 256) {
+            float4 r[4];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            const int g = g0 + wave + RW * u;
-            r[u] = (in && g < nslab)
-                       ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < 4; ++u) {
+                const int g = g0 + j + 64 * u;
+                r[u] = g < nslab ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v.x += r[u].x;
+                v.y += r[u].y;
+                v.z += r[u].z;
+                v.w += r[u].w;
+            }
         }
-        if (adam && g0 == 0) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
+    } else if (!from_pre) {
+        for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
+            float4 r[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) {
-            v.x += r[u].x;
-            v.y += r[u].y;
-            v.z += r[u].z;
-            v.w += r[u].w;
+            for (int u = 0; u < 16; ++u) {
+                const int g = g0 + wave + RW * u;
+                r[u] = (in && g < nslab)
+                           ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                v.x += r[u].x;
+                v.y += r[u].y;
+                v.z += r[u].z;
+                v.w += r[u].w;
+            }
         }
     }
+    // Adam's step scalars (two f64 pow) formed while the loads are in flight, not after the
+    // barrier on the update's critical path
+    g2048::AdamCoef c{};
+    if (adam) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
     part[wave][lane] = v;
     __syncthreads();
-    if (wave != 0 || !in) return;
-    float4 sv = part[0][lane];
+    if (!fin) return;
+    float4 sv;
+    if (from_pre) {
+        sv = pv;
+    } else if (c1) {
+        sv = part[0][lane];
+        for (int j = 1; j < 64; ++j) {
+            const float4 pj = part[j >> 2][(j & 3) * 16 + lane];
+            sv.x += pj.x;
+            sv.y += pj.y;
+            sv.z += pj.z;
+            sv.w += pj.w;
+        }
+    } else {
+        sv = part[0][lane];
 #pragma unroll
-    for (int k = 1; k < RW; ++k) {
-        sv.x += part[k][lane].x;
-        sv.y += part[k][lane].y;
-        sv.z += part[k][lane].z;
-        sv.w += part[k][lane].w;
+        for (int k = 1; k < RW; ++k) {
+            sv.x += part[k][lane].x;
+            sv.y += part[k][lane].y;
+            sv.z += part[k][lane].z;
+            sv.w += part[k][lane].w;
+        }
     }
     const float se[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int pos = p4 * 4 + e;
-        const float s = se[e];
+        const float sm = se[e];
         if (pos > SL_LOSS) break;
         if (pos == SL_LOSS) {
-            if (loss) *loss = s;
+            if (loss) *loss = sm;
         } else {
             const int pi = slab_to_param(pos);
-            if (grad) grad[pi] = s;
+            if (grad) grad[pi] = sm;
             if (adam) {
-                const float np = g2048::adam_update(c, s, am[e], av[e], ap[e]);
+                const float np = g2048::adam_update(c, sm, am[e], av[e], ap[e]);
                 R.m[pi] = am[e];
                 R.v[pi] = av[e];
                 R.p[kt[e]][ei[e]] = np;
@@ -692,11 +792,16 @@ static int64_t train_grid(int64_t batch) {
     return g;
 }
 
+// float offset of train bwd's slab sums (16-byte aligned)
+static int64_t pre_offset(int64_t batch) {
+    const int64_t ntiles = (batch + S - 1) / S;
+    return (train_grid(batch) * SLAB + ntiles * DM_TILE + conv_split_floats(batch) + 3) & ~3ll;
+}
+
 extern "C" G2048_API int64_t g2048_convnet_train_workspace(int64_t batch) {
     if (batch <= 0) return 0;
-    const int64_t ntiles = (batch + S - 1) / S;
-    // slabs | dM of every tile | split-target scratch of g2048_convnet_update
-    return train_grid(batch) * SLAB + ntiles * DM_TILE + conv_split_floats(batch);
+    // slabs | dM of every tile | split-target scratch of g2048_convnet_update | train bwd's sums
+    return pre_offset(batch) + SLAB;
 }
 
 static float* split_scratch(float* workspace, int64_t batch) {
@@ -723,6 +828,7 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
     A.slab = workspace;
     const int grid = (int)train_grid(batch);
     A.dm = workspace + (int64_t)grid * SLAB;
+    A.pre = grid >= SHADOW_MIN_GRID ? workspace + pre_offset(batch) : nullptr;
     A.step = reinterpret_cast<unsigned long long*>(step_dev);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     hipLaunchKernelGGL(k_conv_train_fwd, dim3(grid), dim3(NT), 0, st, A);
@@ -731,8 +837,9 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
     hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, st, A);
     e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train_bwd: %s", hipGetErrorString(e));
-    hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS / 4 + 64) / 64), dim3(64 * RW), 0, st,
-                       workspace, grid, grad_out, loss_out, R);
+    const int nb = (SL_LOSS / 4 + 64) / 64;
+    hipLaunchKernelGGL(k_reduce_slabs, dim3(nb + (A.pre ? C1_BLOCKS : 0)), dim3(64 * RW), 0, st,
+                       workspace, grid, A.pre, nb, grad_out, loss_out, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "k_reduce_slabs: %s", hipGetErrorString(e));
