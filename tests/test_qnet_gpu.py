@@ -177,15 +177,17 @@ def test_fused_adam_matches_torch_adam(G):
         torch.testing.assert_close(p1, p2, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("B", [2048, 4096])
 @pytest.mark.parametrize("sync_every", [0, 2])
-def test_conv_train_adam_equals_grad_then_adam(G, sync_every):
+def test_conv_train_adam_equals_grad_then_adam(G, sync_every, B):
     """g2048_convnet_train_adam (Adam + target sync folded into the gradient reduction) is
-    bitwise train_grad followed by g2048_adam_step_sync, over 3 updates."""
+    bitwise train_grad followed by g2048_adam_step_sync, over 3 updates.  B = 4096 runs on 256
+    workgroups, where train bwd sums train fwd's slab terms itself (SlabShadow)."""
     from g2048.nets import make_net
     from g2048.optim import FusedAdam
     from g2048.qnet import ConvTrainGrad
 
-    C, B = 16384, 2048
+    C = 16384
     env = G.VecEnv2048(4096, device=DEV, seed=5)
     rb = G.ReplayBuffer(C, device=DEV)
     env.rollout(C // 4096, replay=rb)
