@@ -289,11 +289,13 @@ def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
                 p.copy_(q)
 
 
+@pytest.mark.parametrize("batch", [700, 4096])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
-def test_fused_f64_adam_step_equals_folded(G, net):
+def test_fused_f64_adam_step_equals_folded(G, net, batch):
     """The data-parallel float64 split (fused gradient -> grad_out, then g2048_adam_step_sync_f64)
     moves online and target weights bitwise like the single-process update with Adam folded into
-    the reduction, over three updates with a target sync every 2."""
+    the reduction, over three updates with a target sync every 2 (B = 4096: the conv update with
+    train B's slab sums)."""
     from g2048 import qnet
     from g2048.learner import DQNLearner
 
@@ -301,10 +303,10 @@ def test_fused_f64_adam_step_equals_folded(G, net):
     env = G.VecEnv2048(n, seed=21, device=DEV)
     rb = G.ReplayBuffer(8 * n, device=DEV)
     env.rollout(8, replay=rb)
-    a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=700, target_sync_every=2, seed=5,
-                   graph=False)
-    b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=700, target_sync_every=2, seed=5,
-                   graph=False)
+    a = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=batch, target_sync_every=2,
+                   seed=5, graph=False)
+    b = DQNLearner(rb, net=net, dtype=torch.float64, batch_size=batch, target_sync_every=2,
+                   seed=5, graph=False)
     assert a.f64 and b.f64
     b.model.load_state_dict(a.model.state_dict())
     b.target.load_state_dict(a.target.state_dict())
