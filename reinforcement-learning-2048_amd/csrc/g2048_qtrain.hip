@@ -744,6 +744,7 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
         sv = pv;
     } else if (c1) {
         sv = part[0][lane];
+#pragma unroll 8  // eight LDS reads in flight per dependent-add chain, not one
         for (int j = 1; j < 64; ++j) {
             const float4 pj = part[j >> 2][(j & 3) * 16 + lane];
             sv.x += pj.x;
