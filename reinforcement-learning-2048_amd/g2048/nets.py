@@ -48,17 +48,21 @@ class _LinearSplitK(torch.autograd.Function):
         gx = gy @ w if ctx.needs_input_grad[0] else None
         m = x.shape[0]
         s = _splits(m)
+        gys = gy.reshape(s, m // s, -1)
         if s > 1:
-            gw = torch.bmm(gy.reshape(s, m // s, -1).transpose(1, 2),
-                           x.reshape(s, m // s, -1)).sum(0)
+            gw = torch.bmm(gys.transpose(1, 2), x.reshape(s, m // s, -1)).sum(0)
         else:
             gw = gy.t() @ x
-        # the bias gradient as a GEMM (ones[1, m] @ dY) rather than torch's sum over dim 0: in
-        # replays of the captured update that reduction returned stale, deterministic garbage
-        # for the conv and fc biases (weights' gradients right, eager runs right) once another
-        # learner's work ran between the replays (tests/test_learner_gpu.py
-        # test_fused_f64_equals_torch_path at B = 4096)
-        gb = torch.mm(gy.new_ones(1, m), gy)[0] if ctx.needs_input_grad[2] else None
+        # the bias gradient through the same chunked GEMMs (dY_chunk^T 1) plus the same small
+        # sum over chunks as dW, not torch's dim-0 sum over all m rows: in replays of the captured
+        # update that reduction returned stale, deterministic garbage for the conv and fc biases
+        # (weights' gradients right, eager runs right) once another learner's work ran between
+        # the replays (tests/test_learner_gpu.py test_fused_f64_equals_torch_path at B = 4096).
+        # (A [1 x m] x [m x n] GEMM was right too, but a poor rocBLAS shape: +0.9 ms per f64
+        # dense-ref update.)
+        gb = None
+        if ctx.needs_input_grad[2]:
+            gb = torch.bmm(gys.transpose(1, 2), gy.new_ones(s, m // s, 1)).sum(0)[:, 0]
         # b is None for a bias-free layer: autograd takes no gradient for a non-tensor input
         return gx, gw, gb
 
