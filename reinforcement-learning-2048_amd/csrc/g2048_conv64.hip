@@ -64,21 +64,40 @@ static_assert(PACK_ALL % 256 == 0 && PACK_FWD % 256 == 0, "pack grid");
 // workspace: packed operands | the next-step word (+ pad to 256 B) | slabs | dZ2 rows
 constexpr int WS_STEP = PACK_ALL, WS_SLAB = PACK_ALL + 32;
 
-// Phase ticks (s_memtime deltas of thread 0 of workgroup 0, charged to the phase that ENDS at the
-// marker), compiled in only for kernel tuning (tools/prof_conv64.hip).
+// Phase ticks (s_memtime deltas of wave 0 of workgroup 0, charged to the phase that ENDS at the
+// marker), compiled in only for kernel tuning (tools/prof_conv64.hip).  Every workgroup keeps its
+// ticks in LDS (wave 0, a uniform branch: an s_memtime and an LDS update, so a marker waits on
+// lgkmcnt only; markers that updated global memory waited on vmcnt, i.e. on every prefetch in
+// flight); workgroup 0 adds them to g_cphase at the end of the launch.  Even so the markers move
+// register allocation: train B spills ~55 VGPRs in this build (none in the library), so its
+// phase ticks are indicative only -- time changes with the -DG2048_NO_PHASE_PROF build.
 #ifdef G2048_PHASE_PROF
 __device__ unsigned long long g_cphase[32];
-__device__ unsigned long long g_clast;
-#define CPHASE(k)                                                         \
+__shared__ unsigned long long g_lph[24];  // [k]: ticks of phase k; [23]: the last marker
+#define CPHASE_INIT()                                                     \
     do {                                                                  \
-        if (blockIdx.x == 0 && threadIdx.x == 0) {                        \
-            const unsigned long long n_ = __builtin_amdgcn_s_memtime();   \
-            if ((k) >= 0) g_cphase[(k) < 0 ? 0 : (k)] += n_ - g_clast;    \
-            g_clast = n_;                                                 \
+        if (threadIdx.x == 0) {                                           \
+            for (int k_ = 0; k_ < 23; ++k_) g_lph[k_] = 0ull;             \
+            g_lph[23] = __builtin_amdgcn_s_memtime();                     \
         }                                                                 \
     } while (0)
+#define CPHASE(k)                                                         \
+    do {                                                                  \
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) < 64) {           \
+            const unsigned long long n_ = __builtin_amdgcn_s_memtime();   \
+            if ((k) >= 0) g_lph[(k) < 0 ? 0 : (k)] += n_ - g_lph[23];     \
+            g_lph[23] = n_;                                               \
+        }                                                                 \
+    } while (0)
+#define CPHASE_FLUSH()                                                    \
+    do {                                                                  \
+        if (blockIdx.x == 0 && threadIdx.x == 0)                          \
+            for (int k_ = 0; k_ < 23; ++k_) atomicAdd(&g_cphase[k_], g_lph[k_]); \
+    } while (0)
 #else
+#define CPHASE_INIT()
 #define CPHASE(k)
+#define CPHASE_FLUSH()
 #endif
 
 // The packed weights are the same for every tile, so loop-invariant code motion would hoist all
@@ -484,7 +503,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     const unsigned long long ep = T.idx_in ? 0ull : *T.step;
     const unsigned long long count = T.idx_in ? 0ull : *T.R.count;
     if (blockIdx.x == 0 && t == 0) *T.step_next = *T.step + 1ull;
-    CPHASE(-1);
+    CPHASE_INIT();
     const SmallW& W = M.sw[0];
     const int64_t ntiles = (A.batch + TB - 1) / TB;
     // board t of a tile: the sampled row, its s', r, (1 - d) * gamma (float32 in torch,
@@ -666,6 +685,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     if (l == 0) sl[P_FB2 + w] = gfb2;
     if (t == 0) sl[P_N] = gloss;
     CPHASE(13);
+    CPHASE_FLUSH();
 }
 
 // ------------------------------------------------------------------ 4. train B
@@ -702,7 +722,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) gw2[c] = d4{0.0, 0.0, 0.0, 0.0};
     double gw1[4] = {0.0, 0.0, 0.0, 0.0}, gb1 = 0.0, gb2 = 0.0;
-    CPHASE(-1);
+    CPHASE_INIT();
     const int64_t ntiles = (A.batch + TB - 1) / TB;
     // the tile's boards and the thread's dZ2 (four (b = (t >> 6) + 4k, o = t & 63) pairs, four
     // doubles (p) each): the next tile's are fetched while the current one runs, so neither the
@@ -799,7 +819,10 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             ld9(bb[0], 0);
             ld9(bb[1], 1);
             // A (dM) of a step read into registers together: one LDS wait per step, not one per
-            // MFMA (a step ahead needs 36 more VGPRs: spills)
+            // MFMA (a step ahead needs 36 more VGPRs: spills).  One scheduling barrier per step,
+            // at its end: without a second one between the step's loads and its MFMAs (all 18
+            // loads issued, then 9 MFMAs) the compiler spreads the B loads over the MFMAs and
+            // packs conv1's relu mask under the first step (train B 46.5 -> 46.1 us per update)
             auto la9 = [&](double(&a)[9], int s) {
                 const double* ar = M.dm + lr * DSB + 4 * s + lk;
 #pragma unroll
@@ -810,7 +833,6 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             for (int s = 0; s < 16; ++s) {
                 la9(aa[s & 1], s);
                 if (s + 2 < 16) ld9(bb[(s + 2) % 3], s + 2);
-                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int x = 0; x < 9; ++x) dv[x] = mfma(aa[s & 1][x], bb[s % 3][x], dv[x]);
                 __builtin_amdgcn_sched_barrier(0);
@@ -908,6 +930,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         }
     }
     CPHASE(19);
+    CPHASE_FLUSH();
 }
 
 constexpr int RW = 16;

@@ -100,7 +100,7 @@ class DQNLearner:
                       and qnet.is_dense_ref(self.model) else None)
         # ... and, in float64, the update's two no-grad forwards (Q_online(s'), Q_target(s') of
         # the Bellman target, src/dqn_lib.py:125-144) as the same HIP launch on the sampled s'
-        # rows: only Q_online(s) goes through torch autograd (B = 8192: 1.44 -> 1.14 ms per
+        # rows: only Q_online(s) goes through torch autograd (B = 8192: 1.44 -> 1.18 ms per
         # update).  Not in float32: its 64-row tiles put B = 8192 rows on 128 of the 256 CUs,
         # slower than torch's two GEMM forwards (0.74 -> 0.80 ms).
         self._dfwd_tg = (qnet.DenseForward(self.target)

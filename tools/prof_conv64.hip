@@ -1,7 +1,9 @@
 // Per-kernel event timing of the float64 conv update (g2048_conv64.hip) at B = 8192 and the phase
-// ticks of its targets / train kernels (s_memtime deltas of thread 0 of workgroup 0, charged to
+// ticks of its targets / train kernels (s_memtime deltas of wave 0 of workgroup 0, charged to
 // the phase that ENDS at the marker), built only for kernel tuning:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_conv64.hip -o tools/prof_conv64
+// (-DG2048_NO_PHASE_PROF: no markers, the library's code generation -- the event times to trust;
+// the markers make train B spill).  Arguments: [B [nopre]].
 #ifndef G2048_NO_PHASE_PROF
 #define G2048_PHASE_PROF 1
 #endif
@@ -74,7 +76,9 @@ int main(int argc, char** argv) {
     unsigned long long* step_next = reinterpret_cast<unsigned long long*>(ws + WS_STEP);
     double* slab = ws + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
-    double* pre = grid >= SHADOW_MIN_GRID ? dz2 + tiles * TB * 256 : nullptr;
+    // argv[2] == "nopre": train A's slab terms summed by the reduce, not in train B's shadow
+    const bool nopre = argc > 2 && strcmp(argv[2], "nopre") == 0;
+    double* pre = grid >= SHADOW_MIN_GRID && !nopre ? dz2 + tiles * TB * 256 : nullptr;
 
     PackArgs P{w[0][2], w[0][4], w[1][2], w[1][4], pk};
     Ring R{reinterpret_cast<const uint4*>(s), reinterpret_cast<const uint4*>(s2), a, d, r, count};
@@ -160,6 +164,11 @@ int main(int argc, char** argv) {
             tk[k] += ms * 1e3f / N;
         }
     }
+    // the phase ticks of the N timed updates only (the loops below launch train B again)
+    unsigned long long ph[32] = {0};
+#ifdef G2048_PHASE_PROF
+    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_cphase), sizeof(ph));
+#endif
     printf("B=%d grid=%d  pack %.2f  targets %.2f  train_a %.2f  train_b %.2f  reduce %.2f  "
            "(us)  update (no pack) %.2f\n", B, grid, tk[0], tk[1], tk[2], tk[3], tk[4],
            tk[1] + tk[2] + tk[3] + tk[4]);
@@ -182,10 +191,6 @@ int main(int argc, char** argv) {
         (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
         printf("reduce right after train_b (last pair): %.2f us\n", ms * 1e3f);
     }
-    unsigned long long ph[32] = {0};
-#ifdef G2048_PHASE_PROF
-    (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_cphase), sizeof(ph));
-#endif
     const double tpw = (double)N * ((tiles + grid - 1) / grid);  // tiles per workgroup x N
     const char* names[20] = {"-", "sample+put s'", "y + put s", "conv1+V", "conv2 wino", "fc1",
                              "fc2", "tgt y", "A load", "A loss/dq", "A fc2 grad+dZ3",
