@@ -36,13 +36,16 @@ __device__ __forceinline__ AdamCoef adam_coef(double t, double lr, double b1, do
     return c;
 }
 
-// One element on values: m, v updated; returns the updated parameter.
+// One element on values: m, v updated; returns the updated parameter.  The fused multiply-adds
+// are spelled out: left to contraction, the compiler fused them differently in different
+// kernels (k_adam vs the reductions that fold Adam in), so the "bitwise the same update" of
+// those kernels depended on their surrounding code.
 __device__ __forceinline__ float adam_update(const AdamCoef& c, float g, float& m, float& v,
                                              float p) {
-    m = m + c.w1 * (g - m);                      // lerp(m, g, 1 - b1), weight < 0.5 branch
-    v = v * c.b2 + c.w2 * g * g;                 // mul_(b2).addcmul_(g, g, 1 - b2)
+    m = __fmaf_rn(c.w1, g - m, m);                 // lerp(m, g, 1 - b1), weight < 0.5 branch
+    v = __fmaf_rn(c.w2 * g, g, v * c.b2);          // mul_(b2).addcmul_(g, g, 1 - b2)
     const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
-    return p + (-c.step_size) * (m / denom);     // addcdiv_(m, denom, value=-step_size)
+    return __fmaf_rn(-c.step_size, m / denom, p);  // addcdiv_(m, denom, value=-step_size)
 }
 
 // returns the updated parameter; m / v updated in place

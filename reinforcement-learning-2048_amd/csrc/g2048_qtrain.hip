@@ -16,8 +16,10 @@
 //   k_conv_train_bwd  per tile: dV_xi = dM_xi U_xi^T (U in the transposed register layout),
 //                     dh1 = B dV B^T, relu'(h1) from conv1 recomputed in the forward's float
 //                     order, dW1 / db1 -> the same slab.
-//   k_reduce_slabs    fixed-order sum of the slabs (deterministic) -> the flat gradient bucket,
-//                     optionally with Adam folded in.
+//   k_reduce_pre      fixed-order sums (deterministic) -> the flat gradient bucket, optionally
+//                     with Adam folded in: train fwd's slab terms arrive summed (train bwd adds
+//                     them in the shadow of its MFMAs), conv1's are summed here over the slabs.
+//                     (k_reduce_slabs: every term over the slabs, for grids too small to shadow.)
 //
 // g2048_convnet_update puts the targets launch (g2048_qnet.hip) in front: one whole train_step
 // per call; with Double DQN, k_conv_train_fwd forms y from the targets' online / target halves.
@@ -645,123 +647,36 @@ struct ReduceAdam {
     int on;
 };
 
-// Deterministic slab reduction: a block owns 256 slab positions (a float4 per lane); its 16
-// waves sum the slabs g = wave, wave + 16, ... (16 independent float4 loads per lane in flight:
-// one memory round trip per 256 slabs), then the 16 partials are added in a fixed order.
-// With `pre` (train bwd summed train fwd's terms): blocks [0, nb_pre) take their float4s from
-// `pre` (one load by wave 0; conv1's float4s are skipped), and blocks nb_pre + c sum conv1's
-// float4s [C1_F4_LO + 16 c, + 16) over the slabs -- lane (q = l % 16, h = l / 16) of wave w sums
-// the slabs j, j + 64, ... (j = 4 w + h), then 16 threads add the 64 partials in j order -- so
-// conv1's 328 KB of slab terms are read by five blocks, not by two whole-slab-width ones.
-constexpr int RW = 16;  // waves per reduction block
-
-__global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int nslab,
-                                                          const float* pre, int nb_pre,
-                                                          float* grad, float* loss, ReduceAdam R) {
-    __shared__ float4 part[RW][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const bool c1 = pre != nullptr && (int)blockIdx.x >= nb_pre;
-    const int p4 = c1 ? C1_F4_LO + ((int)blockIdx.x - nb_pre) * C1_PER_BLOCK + (lane & 15)
-                      : (int)blockIdx.x * 64 + lane;  // float4 index within a slab
-    const bool in = p4 * 4 <= SL_LOSS;
-    const bool from_pre = pre != nullptr && !c1;
-    const bool skip = from_pre && p4 >= C1_F4_LO && p4 < C1_F4_HI;  // a conv1 block's
-    const bool fin = wave == 0 && in && !skip && (!c1 || lane < C1_PER_BLOCK);
-    // Adam operands of this lane's 4 positions (the finishing lanes), loaded with the slabs:
-    // they do not depend on the sums, so the update costs no memory round trip of its own.
-    const bool adam = R.on && fin;
+// The Adam operands of the four positions of slab float4 p4 (loaded with the slabs: they do not
+// depend on the sums, so the update costs no memory round trip of its own).
+struct AdamLane {
     int kt[4], ei[4];
     float am[4], av[4], ap[4];
-    unsigned long long t = 0;
-    if (adam) {
-        t = *R.step;
-        constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
+};
+
+__device__ __forceinline__ void adam_load(const ReduceAdam& R, int p4, AdamLane& L) {
+    constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const int pos = p4 * 4 + e;
-            kt[e] = -1;
-            if (pos >= SL_LOSS) continue;
-            const int pi = slab_to_param(pos);
-            int k = 0;
+    for (int e = 0; e < 4; ++e) {
+        const int pos = p4 * 4 + e;
+        L.kt[e] = -1;
+        if (pos >= SL_LOSS) continue;
+        const int pi = slab_to_param(pos);
+        int k = 0;
 #pragma unroll
-            for (int j = 1; j < 8; ++j) k += pi >= off[j] ? 1 : 0;
-            kt[e] = k;
-            ei[e] = pi - off[k];
-            am[e] = R.m[pi];
-            av[e] = R.v[pi];
-            ap[e] = R.p[k][ei[e]];
-        }
+        for (int j = 1; j < 8; ++j) k += pi >= off[j] ? 1 : 0;
+        L.kt[e] = k;
+        L.ei[e] = pi - off[k];
+        L.am[e] = R.m[pi];
+        L.av[e] = R.v[pi];
+        L.ap[e] = R.p[k][L.ei[e]];
     }
-    const float4 pv = (from_pre && fin) ? reinterpret_cast<const float4*>(pre)[p4]
-                                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (c1) {
-        const int j = 4 * wave + (lane >> 4);
-        for (int g0 = 0; g0 < nslab; g0 += 256) {
-            float4 r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int g = g0 + j + 64 * u;
-                r[u] = g < nslab ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
-                                 : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                v.x += r[u].x;
-                v.y += r[u].y;
-                v.z += r[u].z;
-                v.w += r[u].w;
-            }
-        }
-    } else if (!from_pre) {
-        for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
-            float4 r[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const int g = g0 + wave + RW * u;
-                r[u] = (in && g < nslab)
-                           ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                v.x += r[u].x;
-                v.y += r[u].y;
-                v.z += r[u].z;
-                v.w += r[u].w;
-            }
-        }
-    }
-    // Adam's step scalars (two f64 pow) formed while the loads are in flight, not after the
-    // barrier on the update's critical path
-    g2048::AdamCoef c{};
-    if (adam) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
-    part[wave][lane] = v;
-    __syncthreads();
-    if (!fin) return;
-    float4 sv;
-    if (from_pre) {
-        sv = pv;
-    } else if (c1) {
-        sv = part[0][lane];
-#pragma unroll 8  // eight LDS reads in flight per dependent-add chain, not one
-        for (int j = 1; j < 64; ++j) {
-            const float4 pj = part[j >> 2][(j & 3) * 16 + lane];
-            sv.x += pj.x;
-            sv.y += pj.y;
-            sv.z += pj.z;
-            sv.w += pj.w;
-        }
-    } else {
-        sv = part[0][lane];
-#pragma unroll
-        for (int k = 1; k < RW; ++k) {
-            sv.x += part[k][lane].x;
-            sv.y += part[k][lane].y;
-            sv.z += part[k][lane].z;
-            sv.w += part[k][lane].w;
-        }
-    }
+}
+
+// The summed float4 p4: the loss, the gradient (torch order) and, with Adam, the update.
+__device__ __forceinline__ void finish4(const ReduceAdam& R, bool adam, const g2048::AdamCoef& c,
+                                        unsigned long long t, int p4, float4 sv, AdamLane& L,
+                                        float* grad, float* loss) {
     const float se[4] = {sv.x, sv.y, sv.z, sv.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -774,14 +689,133 @@ __global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int
             const int pi = slab_to_param(pos);
             if (grad) grad[pi] = sm;
             if (adam) {
-                const float np = g2048::adam_update(c, sm, am[e], av[e], ap[e]);
-                R.m[pi] = am[e];
-                R.v[pi] = av[e];
-                R.p[kt[e]][ei[e]] = np;
-                if (R.sync_every && t % R.sync_every == 0ull) R.tp[kt[e]][ei[e]] = np;
+                const float np = g2048::adam_update(c, sm, L.am[e], L.av[e], L.ap[e]);
+                R.m[pi] = L.am[e];
+                R.v[pi] = L.av[e];
+                R.p[L.kt[e]][L.ei[e]] = np;
+                if (R.sync_every && t % R.sync_every == 0ull) R.tp[L.kt[e]][L.ei[e]] = np;
             }
         }
     }
+}
+
+// With `pre` (train bwd summed train fwd's slab terms): four waves per block.  Blocks
+// [0, NB_PRE4) take one float4 of `pre` per thread (conv1's float4s skipped); blocks NB_PRE4 + c
+// sum conv1's float4s [C1_F4_LO + 16 c, + 16) over the slabs -- thread (q = t % 16, j = t / 16)
+// the slabs j, j + 16, ... (16 loads in flight), then 16 threads add the 16 partials in j order.
+constexpr int NB_PRE4 = (SL_LOSS / 4 + 256) / 256;
+
+__global__ __launch_bounds__(256) void k_reduce_pre(const float* slab, int nslab, const float* pre,
+                                                    float* grad, float* loss, ReduceAdam R) {
+    __shared__ float4 part[16][16];
+    const int t = threadIdx.x;
+    const bool c1 = (int)blockIdx.x >= NB_PRE4;
+    const int p4 = c1 ? C1_F4_LO + ((int)blockIdx.x - NB_PRE4) * C1_PER_BLOCK + (t & 15)
+                      : (int)blockIdx.x * 256 + t;
+    const bool fin = c1 ? t < C1_PER_BLOCK
+                        : p4 * 4 <= SL_LOSS && !(p4 >= C1_F4_LO && p4 < C1_F4_HI);
+    const bool adam = R.on && fin;
+    AdamLane L;
+    unsigned long long st = 0;
+    if (adam) {
+        st = *R.step;
+        adam_load(R, p4, L);
+    }
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (!c1) {
+        if (fin) sv = reinterpret_cast<const float4*>(pre)[p4];
+    } else {
+        const int j = t >> 4;
+        for (int g0 = 0; g0 < nslab; g0 += 256) {
+            float4 r[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int g = g0 + j + 16 * u;
+                r[u] = g < nslab ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                sv.x += r[u].x;
+                sv.y += r[u].y;
+                sv.z += r[u].z;
+                sv.w += r[u].w;
+            }
+        }
+        part[j][t & 15] = sv;
+    }
+    g2048::AdamCoef c{};
+    if (adam) c = g2048::adam_coef((double)st, R.lr, R.b1, R.b2, R.eps);
+    if (c1) {
+        __syncthreads();
+        if (!fin) return;
+        sv = part[0][t];
+#pragma unroll
+        for (int j = 1; j < 16; ++j) {
+            const float4 pj = part[j][t];
+            sv.x += pj.x;
+            sv.y += pj.y;
+            sv.z += pj.z;
+            sv.w += pj.w;
+        }
+    }
+    if (!fin) return;
+    finish4(R, adam, c, st, p4, sv, L, grad, loss);
+}
+
+// Deterministic slab reduction (without `pre`: small batches, grid < SHADOW_MIN_GRID): a block
+// owns 256 slab positions (a float4 per lane); its 16 waves sum the slabs g = wave, wave + 16, ...
+// (16 independent float4 loads per lane in flight: one memory round trip per 256 slabs), then the
+// 16 partials are added in a fixed order.
+constexpr int RW = 16;  // waves per reduction block
+
+__global__ __launch_bounds__(64 * RW) void k_reduce_slabs(const float* slab, int nslab,
+                                                          float* grad, float* loss, ReduceAdam R) {
+    __shared__ float4 part[RW][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int p4 = (int)blockIdx.x * 64 + lane;  // float4 index within a slab
+    const bool in = p4 * 4 <= SL_LOSS;
+    const bool fin = wave == 0 && in;
+    const bool adam = R.on && fin;
+    AdamLane L;
+    unsigned long long t = 0;
+    if (adam) {
+        t = *R.step;
+        adam_load(R, p4, L);
+    }
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int g0 = 0; g0 < nslab; g0 += RW * 16) {
+        float4 r[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int g = g0 + wave + RW * u;
+            r[u] = (in && g < nslab) ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
+                                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            v.x += r[u].x;
+            v.y += r[u].y;
+            v.z += r[u].z;
+            v.w += r[u].w;
+        }
+    }
+    // Adam's step scalars (two f64 pow) formed while the loads are in flight, not after the
+    // barrier on the update's critical path
+    g2048::AdamCoef c{};
+    if (adam) c = g2048::adam_coef((double)t, R.lr, R.b1, R.b2, R.eps);
+    part[wave][lane] = v;
+    __syncthreads();
+    if (!fin) return;
+    float4 sv = part[0][lane];
+#pragma unroll
+    for (int k = 1; k < RW; ++k) {
+        sv.x += part[k][lane].x;
+        sv.y += part[k][lane].y;
+        sv.z += part[k][lane].z;
+        sv.w += part[k][lane].w;
+    }
+    finish4(R, adam, c, t, p4, sv, L, grad, loss);
 }
 
 }  // namespace
@@ -838,9 +872,12 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
     hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, st, A);
     e = hipGetLastError();
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train_bwd: %s", hipGetErrorString(e));
-    const int nb = (SL_LOSS / 4 + 64) / 64;
-    hipLaunchKernelGGL(k_reduce_slabs, dim3(nb + (A.pre ? C1_BLOCKS : 0)), dim3(64 * RW), 0, st,
-                       workspace, grid, A.pre, nb, grad_out, loss_out, R);
+    if (A.pre)
+        hipLaunchKernelGGL(k_reduce_pre, dim3(NB_PRE4 + C1_BLOCKS), dim3(256), 0, st, workspace,
+                           grid, A.pre, grad_out, loss_out, R);
+    else
+        hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS / 4 + 64) / 64), dim3(64 * RW), 0, st,
+                           workspace, grid, grad_out, loss_out, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "k_reduce_slabs: %s", hipGetErrorString(e));

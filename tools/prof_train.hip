@@ -1,10 +1,12 @@
-// Per-kernel event timing of the conv train launches and phase ticks of k_conv_train_fwd
-// (s_memtime deltas of thread 0 of block 0, charged to the phase that ENDS at the marker),
-// built only for kernel tuning:
+// Per-kernel event timing of the float32 conv train launches (train fwd, train bwd, the slab
+// reduce) at B = 8192 and phase ticks of k_conv_train_fwd / bwd (s_memtime deltas of thread 0
+// of block 0, charged to the phase that ENDS at the marker), built only for kernel tuning:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/prof_train.hip -o tools/prof_train
+// Argument: "nopre" (the reduce sums train fwd's slab terms too).
 #define G2048_PHASE_PROF 1
 #include <cstdarg>
 #include <cstdio>
+#include <cstring>
 #include <vector>
 int g2048_fail(int code, const char* fmt, ...) {
     va_list ap;
@@ -22,7 +24,7 @@ extern "C" int g2048_conv_targets_launch(const g2048_convnet_params*, const g204
                                          const uint64_t*, float, int, int64_t*, float*, float*,
                                          void*) { return 1; }
 
-int main() {
+int main(int argc, char** argv) {
     const int B = 8192, C = 1 << 20;
     const int sizes[8] = {256, 64, 16384, 64, 16384, 64, 256, 4};
     float* w[8];
@@ -67,9 +69,23 @@ int main() {
     A.slab = ws;
     const int grid = (int)train_grid(B);
     A.dm = ws + (int64_t)grid * SLAB;
+    // train bwd sums train fwd's slab terms into pre (the library's layout, pre_offset); argv[1]
+    // == "nopre": the reduce sums every slab term itself
+    const bool nopre = argc > 1 && strcmp(argv[1], "nopre") == 0;
+    A.pre = grid >= SHADOW_MIN_GRID && !nopre ? ws + pre_offset(B) : nullptr;
     A.step = nullptr;
     ReduceAdam R;
     memset(&R, 0, sizeof(R));
+    // the library's choice (train_launch): the four-wave reduce of the pre path, else the
+    // 16-wave one over every slab term
+    auto reduce = [&]() {
+        if (A.pre)
+            hipLaunchKernelGGL(k_reduce_pre, dim3(NB_PRE4 + C1_BLOCKS), dim3(256), 0, nullptr, ws,
+                               grid, A.pre, grad, loss, R);
+        else
+            hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS / 4 + 64) / 64), dim3(64 * RW), 0,
+                               nullptr, ws, grid, grad, loss, R);
+    };
     hipEvent_t ev[4];
     for (int i = 0; i < 4; ++i) (void)hipEventCreate(&ev[i]);
     float tk[3] = {0, 0, 0};
@@ -80,8 +96,7 @@ int main() {
         (void)hipEventRecord(ev[1], nullptr);
         hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, nullptr, A);
         (void)hipEventRecord(ev[2], nullptr);
-        hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, nullptr,
-                           ws, grid, grad, loss, R);
+        reduce();
         (void)hipEventRecord(ev[3], nullptr);
         (void)hipEventSynchronize(ev[3]);
         for (int k = 0; k < 3; ++k) {
@@ -90,9 +105,20 @@ int main() {
             tk[k] += ms * 1e3f / N;
         }
     }
-    printf("B=%d grid=%d  fwd %.2f us  bwd %.2f us  reduce %.2f us\n", B, grid, tk[0], tk[1], tk[2]);
+    // the phase ticks of the N timed updates only
     unsigned long long ph[16];
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_tphase), sizeof(ph));
+    printf("B=%d grid=%d%s  fwd %.2f us  bwd %.2f us  reduce %.2f us\n", B, grid,
+           A.pre ? "" : " (nopre)", tk[0], tk[1], tk[2]);
+    {  // the reduce alone, back to back (nothing dirty from the train kernels)
+        float ms;
+        (void)hipEventRecord(ev[0], nullptr);
+        for (int it = 0; it < N; ++it) reduce();
+        (void)hipEventRecord(ev[1], nullptr);
+        (void)hipEventSynchronize(ev[1]);
+        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+        printf("reduce alone, back to back: %.2f us\n", ms * 1e3f / N);
+    }
     const char* names[8] = {"stage", "conv1+V", "conv2", "fc1", "loss+df", "dWf1+dY", "dM+dU+st", "slab"};
     const double tiles = (double)N * ((B / 16 + grid - 1) / grid);
     for (int k = 0; k < 8; ++k)
@@ -101,53 +127,5 @@ int main() {
     const char* n2[4] = {"bwd stage", "bwd dM ld", "bwd dV", "bwd epi"};
     for (int k = 8; k < 12; ++k)
         printf("%-10s %9.0f ticks/%s\n", n2[k - 8], ph[k] / (k == 8 ? N : tiles), k == 8 ? "launch" : "tile");
-
-    // Timing only (the reduction races with bwd here): do graph branches overlap?  Graph 1 =
-    // fwd, bwd, reduce in one stream; graph 2 = fwd, then bwd and reduce on two forked streams.
-    hipStream_t s0, s1;
-    (void)hipStreamCreateWithFlags(&s0, hipStreamNonBlocking);
-    (void)hipStreamCreateWithFlags(&s1, hipStreamNonBlocking);
-    hipEvent_t fork, join;
-    (void)hipEventCreateWithFlags(&fork, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&join, hipEventDisableTiming);
-    hipGraphExec_t gx[2];
-    for (int v = 0; v < 2; ++v) {
-        hipGraph_t g;
-        (void)hipStreamBeginCapture(s0, hipStreamCaptureModeGlobal);
-        for (int rep = 0; rep < 10; ++rep) {
-            hipLaunchKernelGGL(k_conv_train_fwd, dim3(grid), dim3(NT), 0, s0, A);
-            hipStream_t rs = s0;
-            if (v == 1) {
-                (void)hipEventRecord(fork, s0);
-                (void)hipStreamWaitEvent(s1, fork, 0);
-                rs = s1;
-            }
-            hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS + 64) / 64), dim3(64 * RW), 0, rs, ws,
-                               grid, grad, loss, R);
-            hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, s0, A);
-            if (v == 1) {
-                (void)hipEventRecord(join, s1);
-                (void)hipStreamWaitEvent(s0, join, 0);
-            }
-        }
-        (void)hipStreamEndCapture(s0, &g);
-        (void)hipGraphInstantiate(&gx[v], g, nullptr, nullptr, 0);
-    }
-    for (int v = 0; v < 2; ++v) {
-        (void)hipGraphLaunch(gx[v], s0);
-        (void)hipStreamSynchronize(s0);
-        float best = 1e30f;
-        for (int r = 0; r < 5; ++r) {
-            (void)hipEventRecord(ev[0], s0);
-            (void)hipGraphLaunch(gx[v], s0);
-            (void)hipEventRecord(ev[1], s0);
-            (void)hipEventSynchronize(ev[1]);
-            float ms;
-            (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
-            best = ms < best ? ms : best;
-        }
-        printf("graph %s: fwd + bwd + reduce %.2f us per update\n",
-               v ? "bwd || reduce (forked)" : "serial", best * 1e3f / 10);
-    }
     return 0;
 }
