@@ -24,6 +24,10 @@ extern "C" int g2048_conv_targets_launch(const g2048_convnet_params*, const g204
                                          const uint64_t*, float, int, int64_t*, float*, float*,
                                          void*) { return 1; }
 
+__global__ void k_nop(int* p) {
+    if (p && threadIdx.x == 0 && blockIdx.x == 0) *p = 0;
+}
+
 int main(int argc, char** argv) {
     const int B = 8192, C = 1 << 20;
     const int sizes[8] = {256, 64, 16384, 64, 16384, 64, 256, 4};
@@ -76,6 +80,29 @@ int main(int argc, char** argv) {
     A.step = nullptr;
     ReduceAdam R;
     memset(&R, 0, sizeof(R));
+    // argv[1] or argv[2] == "adam": Adam folded into the reduce (the learner's update)
+    bool with_adam = false;
+    for (int a = 1; a < argc; ++a) with_adam |= strcmp(argv[a], "adam") == 0;
+    if (with_adam) {
+        float *m, *v;
+        unsigned long long* stepc;
+        (void)hipMalloc(&m, 33476 * 4);
+        (void)hipMalloc(&v, 33476 * 4);
+        (void)hipMemset(m, 0, 33476 * 4);
+        (void)hipMemset(v, 0, 33476 * 4);
+        (void)hipMalloc(&stepc, 8);
+        const unsigned long long one = 1;
+        (void)hipMemcpy(stepc, &one, 8, hipMemcpyHostToDevice);
+        for (int k = 0; k < 8; ++k) R.p[k] = w[k];
+        R.m = m;
+        R.v = v;
+        R.step = stepc;
+        R.lr = 1e-9;
+        R.b1 = 0.9;
+        R.b2 = 0.999;
+        R.eps = 1e-8;
+        R.on = 1;
+    }
     // the library's choice (train_launch): the four-wave reduce of the pre path, else the
     // 16-wave one over every slab term
     auto reduce = [&]() {
@@ -108,6 +135,7 @@ int main(int argc, char** argv) {
     // the phase ticks of the N timed updates only
     unsigned long long ph[16];
     (void)hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_tphase), sizeof(ph));
+    printf("%s", with_adam ? "(Adam folded in) " : "");
     printf("B=%d grid=%d%s  fwd %.2f us  bwd %.2f us  reduce %.2f us\n", B, grid,
            A.pre ? "" : " (nopre)", tk[0], tk[1], tk[2]);
     {  // the reduce alone, back to back (nothing dirty from the train kernels)
@@ -118,6 +146,29 @@ int main(int argc, char** argv) {
         (void)hipEventSynchronize(ev[1]);
         (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
         printf("reduce alone, back to back: %.2f us\n", ms * 1e3f / N);
+    }
+    {  // the launch after each train kernel: what does the boundary cost the next kernel?
+        auto timed = [&](auto&& before, auto&& after) {
+            float tot = 0.f, ms;
+            for (int it = 0; it < N; ++it) {
+                before();
+                (void)hipEventRecord(ev[2], nullptr);
+                after();
+                (void)hipEventRecord(ev[3], nullptr);
+                (void)hipEventSynchronize(ev[3]);
+                (void)hipEventElapsedTime(&ms, ev[2], ev[3]);
+                tot += ms * 1e3f / N;
+            }
+            return tot;
+        };
+        auto fwd = [&]() { hipLaunchKernelGGL(k_conv_train_fwd, dim3(grid), dim3(NT), 0, nullptr, A); };
+        auto bwd = [&]() { hipLaunchKernelGGL(k_conv_train_bwd, dim3(grid), dim3(NT), 0, nullptr, A); };
+        auto nop = [&]() { hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, nullptr, nullptr); };
+        auto fb = [&]() { fwd(); bwd(); };
+        printf("nop after nop %.2f, after fwd %.2f, after fwd+bwd %.2f us\n", timed(nop, nop),
+               timed(fwd, nop), timed(fb, nop));
+        printf("reduce after nop %.2f, after fwd %.2f, after fwd+bwd %.2f us\n", timed(nop, reduce),
+               timed(fwd, reduce), timed(fb, reduce));
     }
     const char* names[8] = {"stage", "conv1+V", "conv2", "fc1", "loss+df", "dWf1+dY", "dM+dU+st", "slab"};
     const double tiles = (double)N * ((B / 16 + grid - 1) / grid);
