@@ -236,7 +236,7 @@ def test_fused_f64_matches_reference(G, golden_dir, net):
     np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
 
 
-@pytest.mark.parametrize("batch", [1000, 4096])
+@pytest.mark.parametrize("batch", [1000, 3000, 4096])
 @pytest.mark.parametrize("double_dqn", [True, False])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
 def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
