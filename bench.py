@@ -45,7 +45,7 @@ ROLLOUT_BYTES = 38
 #   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
 STEP_BYTES = 37
 STEP_BYTES_BOOKKEEPING = 54
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r04")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
 INFINITY_CACHE_BYTES = 256 << 20  # MI355X_MICROARCH.md: die-level L3, 256 MiB
 RESIDENCY_RULE = ("MI355X_MICROARCH.md, Infinity Cache: a line stays resident while everything "
@@ -285,12 +285,21 @@ def rollout_roofline(r, steps, rec):
     launch_s = r["ev_s"] / steps
     algo = ROLLOUT_BYTES * r["n"] * r["k"]
     achieved = algo / launch_s / 1e9
+    # the same bytes over the wall time per launch that `value` / `ms_per_step` use (host clock
+    # around the whole timed region: graph launch latency and the final sync included)
+    wall_s = r["wall"] / steps
     hbm = r["working_set"] > INFINITY_CACHE_BYTES
     out = {"bound": "hbm" if hbm else "issue",
            "resident": "hbm-streamed" if hbm else "infinity-cache",
            "working_set_bytes": r["working_set"], "residency_rule": RESIDENCY_RULE,
            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": achieved / HBM_PEAK_GBS,
+           "frac_source": ("HIP events on the kernel's stream around the timed launches (the "
+                           "kernel's own duration, as rocprofv3 reports it); `frac_wall` is the "
+                           "same bytes over ms_per_step, the clock `value` uses"),
+           "frac_events": achieved / HBM_PEAK_GBS,
+           "frac_wall": algo / wall_s / 1e9 / HBM_PEAK_GBS,
+           "launch_us_wall": wall_s * 1e6,
            "frac_note": ("of the HBM spec; the bytes stream to HBM" if hbm else
                          "algorithmic bytes over the HBM spec, but the working set stays in the "
                          "Infinity Cache: not an HBM-bandwidth claim (see `issue`)"),

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 3
+#define G2048_ABI_VERSION 4
 
 #ifndef G2048_API
 #define G2048_API __attribute__((visibility("default")))
@@ -318,6 +318,15 @@ G2048_API int g2048_adam_step_sync(float* const* params_dev, const int64_t* nume
                                    double beta1, double beta2, double eps,
                                    float* const* target_params_dev, uint64_t sync_every,
                                    void* stream);
+/* The same with the gradient read as g * grad_scale (> 0): the data-parallel step after a SUM
+ * all-reduce of the gradient bucket (grad_scale = 1 / world), so the collective can sit inside the
+ * same captured graph as the update with no divide launch between them (since ABI v4). */
+G2048_API int g2048_adam_step_scaled(float* const* params_dev, const int64_t* numels, int n_tensors,
+                                     const float* grad_dev, float* exp_avg_dev,
+                                     float* exp_avg_sq_dev, const uint64_t* step_dev, double lr,
+                                     double beta1, double beta2, double eps,
+                                     float* const* target_params_dev, uint64_t sync_every,
+                                     double grad_scale, void* stream);
 
 /* ---- dense 16 -> 64 -> 4 Q-net (BASELINE configs[2]): the same four entry points ---------- */
 typedef struct {
@@ -411,7 +420,9 @@ G2048_API int g2048_dense64_update_f64(const g2048_dense64_params_f64* online,
  * in f64-MFMA operand order.  With Adam folded in (exp_avg and exp_avg_sq given) the update reads
  * those packed operands and re-packs the weights it writes (the online net every update, the
  * target net on a sync), so the caller packs them with g2048_convnet_pack_f64 once after
- * allocating the workspace and again after changing either net's weights any other way.  A
+ * allocating the workspace and again after changing either net's weights any other way (ABI v4:
+ * an Adam-folded update on a workspace that was never packed for these two nets returns
+ * G2048_EINVAL; the library remembers which workspaces it packed, host-side).  A
  * gradient-only update (no Adam state: a data-parallel learner applies Adam after the
  * all-reduce) packs at its start. */
 typedef struct {
@@ -483,6 +494,14 @@ G2048_API int g2048_adam_step_sync_f64(double* const* params_dev, const int64_t*
                                        double beta1, double beta2, double eps,
                                        double* const* target_params_dev, uint64_t sync_every,
                                        void* stream);
+/* g2048_adam_step_scaled in float64 (gradient read as g * grad_scale). */
+G2048_API int g2048_adam_step_scaled_f64(double* const* params_dev, const int64_t* numels,
+                                         int n_tensors, const double* grad_dev,
+                                         double* exp_avg_dev, double* exp_avg_sq_dev,
+                                         const uint64_t* step_dev, double lr, double beta1,
+                                         double beta2, double eps,
+                                         double* const* target_params_dev, uint64_t sync_every,
+                                         double grad_scale, void* stream);
 
 /* g2048_env_step_egreedy_dense64 for a float64 dense 16-64-4 net: Q(s) computed in the step
  * kernel in double, the step as g2048_env_step_egreedy with f64 Q (q_out: f64[n][4] or NULL). */

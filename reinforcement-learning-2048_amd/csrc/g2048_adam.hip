@@ -29,6 +29,7 @@ struct AdamArgs {
     float* v;
     const unsigned long long* step;
     double lr, b1, b2, eps;
+    float gscale;  // the gradient's scale: 1, or 1 / world after a SUM all-reduce
 };
 
 __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
@@ -40,7 +41,7 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     float* p = A.p[k] + (i - A.off[k]);
     const unsigned long long t = *A.step;
     const g2048::AdamCoef c = g2048::adam_coef((double)t, A.lr, A.b1, A.b2, A.eps);
-    const float np = g2048::adam_apply(c, A.g[i], A.m + i, A.v + i, *p);
+    const float np = g2048::adam_apply(c, A.g[i] * A.gscale, A.m + i, A.v + i, *p);
     *p = np;
     // target sync (src/dqn_lib.py:227-228 load_state_dict after the update) on the device
     // counter, so an update that syncs needs no host decision between graph replays
@@ -61,6 +62,7 @@ struct AdamArgs64 {
     double* v;
     const unsigned long long* step;
     double lr, b1, b2, eps;
+    double gscale;
 };
 
 __global__ __launch_bounds__(256) void k_adam64(AdamArgs64 A) {
@@ -72,7 +74,8 @@ __global__ __launch_bounds__(256) void k_adam64(AdamArgs64 A) {
     double* p = A.p[k] + (i - A.off[k]);
     const unsigned long long t = *A.step;
     double m = A.m[i], v = A.v[i];
-    const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, A.g[i], m, v, *p);
+    const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, A.g[i] * A.gscale, m, v,
+                                    *p);
     A.m[i] = m;
     A.v[i] = v;
     *p = np;
@@ -85,10 +88,11 @@ static int adam_launch(float* const* params, const int64_t* numels, int n_tensor
                        const float* grad, float* exp_avg, float* exp_avg_sq,
                        const uint64_t* step_dev, double lr, double beta1, double beta2,
                        double eps, float* const* target_params, uint64_t sync_every,
-                       void* stream) {
+                       double grad_scale, void* stream) {
     if (!params || !numels || n_tensors <= 0 || n_tensors > kMaxTensors || !grad || !exp_avg ||
         !exp_avg_sq || !step_dev)
         return g2048_fail(G2048_EINVAL, "adam_step: bad arguments (n_tensors <= %d)", kMaxTensors);
+    if (!(grad_scale > 0.0)) return g2048_fail(G2048_EINVAL, "adam_step: grad_scale must be > 0");
     if (sync_every && !target_params)
         return g2048_fail(G2048_EINVAL, "adam_step: sync_every > 0 needs target_params");
     AdamArgs A;
@@ -109,6 +113,7 @@ static int adam_launch(float* const* params, const int64_t* numels, int n_tensor
     A.b1 = beta1;
     A.b2 = beta2;
     A.eps = eps;
+    A.gscale = (float)grad_scale;
     const int64_t n = A.off[n_tensors];
     hipLaunchKernelGGL(k_adam, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
@@ -121,7 +126,7 @@ extern "C" G2048_API int g2048_adam_step(float* const* params, const int64_t* nu
                                          float* exp_avg_sq, const uint64_t* step_dev, double lr,
                                          double beta1, double beta2, double eps, void* stream) {
     return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
-                       beta2, eps, nullptr, 0, stream);
+                       beta2, eps, nullptr, 0, 1.0, stream);
 }
 
 extern "C" G2048_API int g2048_adam_step_sync(float* const* params, const int64_t* numels,
@@ -131,16 +136,28 @@ extern "C" G2048_API int g2048_adam_step_sync(float* const* params, const int64_
                                               float* const* target_params, uint64_t sync_every,
                                               void* stream) {
     return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
-                       beta2, eps, target_params, sync_every, stream);
+                       beta2, eps, target_params, sync_every, 1.0, stream);
 }
 
-extern "C" G2048_API int g2048_adam_step_sync_f64(double* const* params, const int64_t* numels,
-                                                  int n_tensors, const double* grad,
-                                                  double* exp_avg, double* exp_avg_sq,
-                                                  const uint64_t* step_dev, double lr,
-                                                  double beta1, double beta2, double eps,
-                                                  double* const* target_params,
-                                                  uint64_t sync_every, void* stream) {
+// Data-parallel form: the gradient bucket holds the SUM over ranks (the all-reduce captured in the
+// same graph, no divide launch) and Adam reads g * grad_scale (grad_scale = 1 / world; exact for
+// power-of-two worlds, so the update equals the divide-then-Adam form bit for bit there).
+extern "C" G2048_API int g2048_adam_step_scaled(float* const* params, const int64_t* numels,
+                                                int n_tensors, const float* grad, float* exp_avg,
+                                                float* exp_avg_sq, const uint64_t* step_dev,
+                                                double lr, double beta1, double beta2, double eps,
+                                                float* const* target_params, uint64_t sync_every,
+                                                double grad_scale, void* stream) {
+    return adam_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
+                       beta2, eps, target_params, sync_every, grad_scale, stream);
+}
+
+static int adam64_launch(double* const* params, const int64_t* numels, int n_tensors,
+                         const double* grad, double* exp_avg, double* exp_avg_sq,
+                         const uint64_t* step_dev, double lr, double beta1, double beta2,
+                         double eps, double* const* target_params, uint64_t sync_every,
+                         double grad_scale, void* stream) {
+    if (!(grad_scale > 0.0)) return g2048_fail(G2048_EINVAL, "adam_step_f64: grad_scale must be > 0");
     if (!params || !numels || n_tensors <= 0 || n_tensors > kMaxTensors || !grad || !exp_avg ||
         !exp_avg_sq || !step_dev)
         return g2048_fail(G2048_EINVAL, "adam_step_f64: bad arguments (n_tensors <= %d)",
@@ -165,10 +182,34 @@ extern "C" G2048_API int g2048_adam_step_sync_f64(double* const* params, const i
     A.b1 = beta1;
     A.b2 = beta2;
     A.eps = eps;
+    A.gscale = grad_scale;
     const int64_t n = A.off[n_tensors];
     hipLaunchKernelGGL(k_adam64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), A);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "adam_step_f64: %s", hipGetErrorString(e));
+}
+
+extern "C" G2048_API int g2048_adam_step_sync_f64(double* const* params, const int64_t* numels,
+                                                  int n_tensors, const double* grad,
+                                                  double* exp_avg, double* exp_avg_sq,
+                                                  const uint64_t* step_dev, double lr,
+                                                  double beta1, double beta2, double eps,
+                                                  double* const* target_params,
+                                                  uint64_t sync_every, void* stream) {
+    return adam64_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
+                         beta2, eps, target_params, sync_every, 1.0, stream);
+}
+
+extern "C" G2048_API int g2048_adam_step_scaled_f64(double* const* params, const int64_t* numels,
+                                                    int n_tensors, const double* grad,
+                                                    double* exp_avg, double* exp_avg_sq,
+                                                    const uint64_t* step_dev, double lr,
+                                                    double beta1, double beta2, double eps,
+                                                    double* const* target_params,
+                                                    uint64_t sync_every, double grad_scale,
+                                                    void* stream) {
+    return adam64_launch(params, numels, n_tensors, grad, exp_avg, exp_avg_sq, step_dev, lr, beta1,
+                         beta2, eps, target_params, sync_every, grad_scale, stream);
 }

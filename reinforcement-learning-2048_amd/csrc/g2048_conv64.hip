@@ -25,6 +25,9 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
 #include "g2048_common.hpp"
@@ -1175,8 +1178,30 @@ static bool params_ok(const g2048_convnet_params_f64* n) {
     return n && n->w1 && n->b1 && n->w2 && n->b2 && n->fc1_w && n->fc1_b && n->fc2_w && n->fc2_b;
 }
 
+// Update workspaces whose head g2048_convnet_pack_f64 has filled, with the conv2 / fc1 weight
+// pointers of the two nets it packed (ABI v4): an Adam-folded update reads the packed operands and
+// refuses a workspace that was never packed for its nets instead of training on uninitialised
+// memory.  Host-side only, so the check is graph-capture safe and costs no launch.
+namespace {
+struct PackKey {
+    const double *w2_on, *f1_on, *w2_tg, *f1_tg;
+    bool operator==(const PackKey& o) const {
+        return w2_on == o.w2_on && f1_on == o.f1_on && w2_tg == o.w2_tg && f1_tg == o.f1_tg;
+    }
+};
+std::mutex g_pack_mu;
+std::unordered_map<const double*, PackKey> g_packed;
+PackKey pack_key(const g2048_convnet_params_f64* on, const g2048_convnet_params_f64* tg) {
+    return PackKey{on->w2, on->fc1_w, tg->w2, tg->fc1_w};
+}
+}  // namespace
+
 static void launch_pack(const g2048_convnet_params_f64* online,
                         const g2048_convnet_params_f64* target, double* pk, hipStream_t st) {
+    {
+        std::lock_guard<std::mutex> lk(g_pack_mu);
+        g_packed[pk] = pack_key(online, target);
+    }
     PackArgs P;
     P.w2_on = online->w2;
     P.f1_on = online->fc1_w;
@@ -1276,7 +1301,16 @@ extern "C" G2048_API int g2048_convnet_update_f64(
 
     // with Adam folded in, the packed operands are current (g2048_convnet_pack_f64 or the
     // previous update's reduce); a gradient-only update packs first (Adam runs elsewhere)
-    if (!adam) launch_pack(online, target, pk, st);
+    if (!adam) {
+        launch_pack(online, target, pk, st);
+    } else {
+        std::lock_guard<std::mutex> lk(g_pack_mu);
+        const auto it = g_packed.find(pk);
+        if (it == g_packed.end() || !(it->second == pack_key(online, target)))
+            return g2048_fail(G2048_EINVAL,
+                              "convnet_update_f64: the workspace holds no packed operands of these "
+                              "nets; call g2048_convnet_pack_f64 after allocating it (ABI v4)");
+    }
 
     Ring R;
     R.s = reinterpret_cast<const uint4*>(s);

@@ -18,7 +18,7 @@ G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOMEM, G2048_EBADINPUT = 0, -1, -2, -
 P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
 ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
-ABI_VERSION = 3  # include/g2048.h G2048_ABI_VERSION
+ABI_VERSION = 4  # include/g2048.h G2048_ABI_VERSION
 REPLAY_SECTION_PAD = 4352  # include/g2048.h G2048_REPLAY_SECTION_PAD
 
 # every symbol include/g2048.h declares, with (restype, argtypes)
@@ -78,6 +78,10 @@ SIGNATURES = {
                                         _u64, _vp]),
     "g2048_adam_step_sync_f64": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
                                         _vp, _u64, _vp]),
+    "g2048_adam_step_scaled": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
+                                      _vp, _u64, _dbl, _vp]),
+    "g2048_adam_step_scaled_f64": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl,
+                                          _dbl, _vp, _u64, _dbl, _vp]),
     "g2048_convnet_update_f64_workspace": (_i64, [_i64]),
     "g2048_convnet_pack_f64": (_int, [_vp, _vp, _vp, _vp]),
     "g2048_convnet_forward_f64": (_int, [_vp, _vp, _vp, _i64, _vp, _vp, _vp]),

@@ -68,9 +68,23 @@ class FlatGradBucket:
             dist.all_reduce(self.flat, group=group)
             self.flat.div_(w)
 
+    def allreduce_sum_(self, group=None) -> None:
+        """The SUM all-reduce alone (also at world 1: the captured data-parallel update is tested
+        on one GPU with a world-1 RCCL group); the caller's Adam applies 1 / world."""
+        if dist.is_available() and dist.is_initialized():
+            dist.all_reduce(self.flat, group=group)
+
     @property
     def nbytes(self) -> int:
         return self.flat.numel() * self.flat.element_size()
+
+
+def captures_collectives(group=None) -> bool:
+    """Whether the gradient all-reduce can be captured into the update's hipGraph: RCCL (the
+    "nccl" backend on ROCm) launches its collective kernels on the caller's stream, so a graph
+    replays them; gloo runs on the host and stays between two graph replays."""
+    return (dist.is_available() and dist.is_initialized()
+            and dist.get_backend(group) == dist.Backend.NCCL)
 
 
 def shard_offset(rank: int, boards_per_rank: int) -> int:

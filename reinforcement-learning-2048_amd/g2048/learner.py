@@ -3,8 +3,9 @@
 DQNLearner.update() is one reference train_step (src/dqn_lib.py:119-164) at batch B:
 sample (torch RNG on device) -> g2048 gather+encode kernel -> online(s'), target(s') -> Bellman
 target -> online(s) -> MSE(sum) -> backward -> [RCCL all_reduce of ONE flat gradient bucket when
-world > 1] -> Adam.  Everything except the collective is captured into hipGraphs, so an update
-costs one (single GPU) or two graph replays plus one all_reduce.
+data-parallel] -> Adam.  The whole update is one hipGraph replay: under RCCL the SUM all-reduce is
+captured with it (Adam reads the gradient times 1 / world, no divide launch); over gloo, which runs
+on the host, the collective sits between two replays.
 
 Trainer is the vectorised training_loop (src/dqn_lib.py:167-244): every iteration steps all N
 boards once with the fused epsilon-greedy kernel (Q from the same online net) and runs
@@ -18,7 +19,7 @@ import copy
 import torch
 
 from . import dqn_lib
-from .dist import FlatGradBucket, broadcast_params, world_size
+from .dist import FlatGradBucket, broadcast_params, captures_collectives, world_size
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, make_net
 from . import qnet
@@ -47,7 +48,8 @@ class DQNLearner:
                  batch_size: int = 8192, discount_factor: float = 0.8, lr: float = 1e-2,
                  use_double_dqn: bool = True, target_sync_every: int = 100, graph: bool = True,
                  seed: int = 0, model: torch.nn.Module | None = None,
-                 process_group=None, sampler=None, loss_fn=None):
+                 process_group=None, sampler=None, loss_fn=None,
+                 data_parallel: bool | None = None):
         self.replay = replay
         self.device = replay.device
         self.dtype = dtype
@@ -64,6 +66,12 @@ class DQNLearner:
         # loss, which the fused kernels implement; any other loss runs the torch path
         self.loss_fn = None if dqn_lib.is_mse_sum(loss_fn) else loss_fn
         self.world = world_size(process_group)
+        # data-parallel: gradient-only updates, the bucket all-reduced, then Adam.  Default: world
+        # > 1; data_parallel=True forces it at world 1 (the captured collective is tested on one
+        # GPU with a world-1 RCCL group)
+        self.dp = self.world > 1 if data_parallel is None else bool(data_parallel)
+        # RCCL: the SUM all-reduce captured into the update's graph, 1 / world folded into Adam
+        self.capture_collective = self.dp and captures_collectives(process_group)
         if model is None:
             torch.manual_seed(seed)
             model = make_net(net, dtype=dtype, device=self.device)
@@ -74,9 +82,31 @@ class DQNLearner:
         self.bucket = FlatGradBucket(self.model)
         self.grad_flat = self.bucket.flat
         self.n_params = self.bucket.numel
+        if self.capture_collective:
+            # RCCL sets a communicator up on its first collective, which must not happen inside
+            # a graph capture: one eager all-reduce of the (zero) bucket now
+            self.bucket.allreduce_sum_(process_group)
         params = self.bucket.params
-        self.opt = torch.optim.Adam(params, lr=lr, capturable=graph, foreach=True)
         self.updates = 0
+        # Adam on the device: torch's Adam update in ONE HIP launch over the flat gradient bucket
+        # (FusedAdam fp32 / Adam64 fp64, csrc/g2048_adam.hip), t and the target sync on the device
+        # update counter -- on the fused paths and on the torch path alike (torch's foreach Adam
+        # is ~8 multi_tensor_apply launches per step: 40-70 us of the dense-ref update).  torch
+        # Adam remains only for models the one-launch kernel cannot take (> 16 tensors, mixed
+        # dtypes, not on a GPU).
+        self.opt = None
+        self._adam = None
+        self.step_dev = None
+        if self.device.type == "cuda" and len(params) <= 16 and all(
+                p.dtype == dtype and p.is_contiguous() for p in params) and dtype in (
+                torch.float32, torch.float64):
+            self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self._adam = (qnet.Adam64(params, lr=lr) if dtype == torch.float64
+                          else FusedAdam(params, lr=lr))
+            if self.target_sync_every:
+                self._adam.attach_target(list(self.target.parameters()), self.target_sync_every)
+        else:
+            self.opt = torch.optim.Adam(params, lr=lr, capturable=graph, foreach=True)
         self.last_loss = torch.zeros((), dtype=dtype, device=self.device)
         self._graphs = None
         self.graph = graph
@@ -111,16 +141,13 @@ class DQNLearner:
             # targets (sampler, both target-side forwards, Bellman), the graded half (forward +
             # MSE + backward) and a fixed-order slab reduction that writes the flat gradient
             # bucket or applies Adam (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip).  The
-            # device update counter is the sampler epoch and Adam's t (bumped by the train launch).
-            self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device)
+            # device update counter is the sampler epoch and Adam's t (bumped by the train launch);
+            # the target sync (every target_sync_every updates) is done by the Adam launch on it:
+            # no host decision between graph replays
+            assert self._adam is not None
             self._idx = torch.zeros(self.B, dtype=torch.int64, device=self.device)
             self._y = torch.zeros(self.B, dtype=torch.float64 if self.f64 else torch.float32,
                                   device=self.device)
-            self._adam = qnet.Adam64(params, lr=lr) if self.f64 else FusedAdam(params, lr=lr)
-            # the target sync (every target_sync_every updates) is done by the Adam launch on
-            # the device update counter: no host decision between graph replays
-            if self.target_sync_every:
-                self._adam.attach_target(list(self.target.parameters()), self.target_sync_every)
             # one whole update per call; single process: Adam (+ target sync) folded into the
             # gradient reduction.  conv: targets (two half-grids, one net each), train forward,
             # train backward, reduce+Adam = 4 launches; dense64: sampler + targets + gradient in
@@ -130,7 +157,7 @@ class DQNLearner:
             else:
                 upd = qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate
             self._upd = upd(self.model, self.target, self.B,
-                            adam=self._adam if self.world == 1 else None)
+                            adam=self._adam if not self.dp else None)
             rank = torch.distributed.get_rank(process_group) if self.world > 1 else 0
             self.sample_seed = (int(seed) * 0x9E3779B9 + 0x2048 + (rank << 40)) & ((1 << 64) - 1)
 
@@ -170,14 +197,27 @@ class DQNLearner:
         self.last_loss.copy_(loss.detach())
 
     def _allreduce(self):
-        self.bucket.allreduce_mean_(self.pg)
+        if not self.dp:
+            return
+        if self.capture_collective:  # SUM; Adam applies 1 / world (grad_scale)
+            self.bucket.allreduce_sum_(self.pg)
+        else:
+            self.bucket.allreduce_mean_(self.pg)
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world if self.capture_collective else 1.0
 
     def _apply(self):
         if self._upd is not None and self._upd.adam is not None:
             return  # applied inside the update's gradient reduction
-        if self.fused:
-            self._adam.step(self.grad_flat, self.step_dev)
+        if self._adam is not None:
+            if not self.fused:  # the fused train launches bump t themselves
+                self.step_dev.add_(1)
+            self._adam.step(self.grad_flat, self.step_dev, self.grad_scale)
         else:
+            if self.grad_scale != 1.0:  # torch's Adam takes no scale: divide (not captured)
+                self.grad_flat.mul_(self.grad_scale)
             self.opt.step()
 
     def _capture(self):
@@ -186,11 +226,12 @@ class DQNLearner:
         snap = [p.detach().clone() for p in params]
         tparams = list(self.target.parameters())  # the fused Adam may sync the target
         tsnap = [p.detach().clone() for p in tparams]
-        step0 = self.step_dev.clone() if self.fused else None
+        dev_adam = self._adam is not None
+        step0 = self.step_dev.clone() if dev_adam else None
         loss0 = self.last_loss.clone()
         rng0 = torch.cuda.get_rng_state(self.device)  # the warm-up draws must not shift the stream
         # optimizer moments too (a resumed learner captures with non-zero Adam state)
-        if self.fused:
+        if dev_adam:
             adam0 = (self._adam.exp_avg.clone(), self._adam.exp_avg_sq.clone())
         else:
             adam0 = {p: {k: v.clone() for k, v in st.items() if torch.is_tensor(v)}
@@ -204,12 +245,13 @@ class DQNLearner:
                 self._apply()
         torch.cuda.current_stream(self.device).wait_stream(side)
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1):
+        with torch.cuda.graph(g1, capture_error_mode=capture_mode(self)):
             self._compute_grads()
-            if self.world == 1:
+            if not self.dp or self.capture_collective:  # the whole update in one graph
+                self._allreduce()
                 self._apply()
         g2 = None
-        if self.world > 1:
+        if self.dp and not self.capture_collective:  # gloo: the collective between two replays
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._apply()
@@ -219,8 +261,8 @@ class DQNLearner:
                 p.copy_(s)
             for p, s in zip(tparams, tsnap):
                 p.copy_(s)
-            for p, st in self.opt.state.items():
-                prev = adam0.get(p, {}) if not self.fused else {}
+            for p, st in (self.opt.state.items() if self.opt is not None else ()):
+                prev = adam0.get(p, {})
                 for k, v in st.items():
                     if torch.is_tensor(v):
                         v.copy_(prev[k]) if k in prev else v.zero_()
@@ -228,7 +270,7 @@ class DQNLearner:
             self.last_loss.copy_(loss0)
         torch.cuda.set_rng_state(rng0, self.device)
         with torch.no_grad():
-            if self.fused:
+            if dev_adam:
                 self._adam.exp_avg.copy_(adam0[0])
                 self._adam.exp_avg_sq.copy_(adam0[1])
                 self.step_dev.copy_(step0)
@@ -260,9 +302,10 @@ class DQNLearner:
         return self.last_loss
 
     def host_target_sync(self) -> None:
-        """The torch path's target sync every target_sync_every updates (src/dqn_lib.py:227-228),
-        after self.updates was counted; the fused paths sync on the device update counter."""
-        if (not self.fused and self.target_sync_every
+        """The target sync every target_sync_every updates (src/dqn_lib.py:227-228) of a learner
+        on torch's Adam, after self.updates was counted; the device Adam (every fused path and the
+        torch path on a GPU) syncs on the device update counter instead."""
+        if (self._adam is None and self.target_sync_every
                 and self.updates % self.target_sync_every == 0):
             dqn_lib.sync_target(self.model, self.target)
 
@@ -287,9 +330,11 @@ class DQNLearner:
               "model": {k: cpu(v) for k, v in self.model.state_dict().items()},
               "target": {k: cpu(v) for k, v in self.target.state_dict().items()},
               "cuda_rng": torch.cuda.get_rng_state(self.device)}
-        if self.fused:
+        if self._adam is not None:
             st.update(adam_exp_avg=cpu(self._adam.exp_avg), adam_exp_avg_sq=cpu(self._adam.exp_avg_sq),
-                      step_dev=cpu(self.step_dev), sample_seed=self.sample_seed)
+                      step_dev=cpu(self.step_dev))
+            if self.fused:
+                st["sample_seed"] = self.sample_seed
         else:
             params = self.bucket.params
             st["adam"] = [{k: cpu(v) for k, v in self.opt.state[p].items() if torch.is_tensor(v)}
@@ -315,11 +360,14 @@ class DQNLearner:
         self.updates = int(st["updates"])
         self.last_loss.copy_(st["last_loss"])
         torch.cuda.set_rng_state(st["cuda_rng"], self.device)
-        if self.fused:
+        if self._adam is not None:
+            if "adam_exp_avg" not in st:
+                st = dict(st, **_flat_adam_state(st.get("adam", []), self.bucket.params))
             self._adam.exp_avg.copy_(st["adam_exp_avg"])
             self._adam.exp_avg_sq.copy_(st["adam_exp_avg_sq"])
             self.step_dev.copy_(st["step_dev"])
-            self.sample_seed = int(st["sample_seed"])
+            if self.fused:
+                self.sample_seed = int(st["sample_seed"])
         else:
             for p, saved in zip(self.bucket.params, st["adam"]):
                 if not saved:
@@ -360,6 +408,11 @@ class Trainer:
         self.graph = (capturable and learner.graph) if graph is None else bool(graph)
         if self.graph and not capturable:
             raise ValueError("the graphed loop needs a fused learner or the reference dense net")
+        if self.graph and not learner.fused and not learner.graph:
+            # the torch path's Adam was built capturable=learner.graph: capturing its step would
+            # fail at capture time, far from the cause
+            raise ValueError("graph=True with a torch-path learner needs DQNLearner(graph=True) "
+                             "(its optimizer must be capturable)")
         # Q of the greedy-branch boards only (False: every board; tests compare the two)
         self.greedy_forward = True
         self._loop_graph = None
@@ -428,19 +481,20 @@ class Trainer:
         (boards, ring position, update counter) from device memory, so replay k equals eager
         iteration k bit for bit."""
         L = self.learner
-        if L.world > 1:
+        if L.dp and not L.capture_collective:
             return self._graphed_iteration_dp()
-        # the torch-path learner syncs its target on the host between updates: one update in the
-        # graph, the others through the learner's own graphed update
-        ups = self.updates_per_step if L.fused else 1
+        # a learner on torch's Adam syncs its target on the host between updates: one update in
+        # the graph, the others through the learner's own graphed update
+        ups = self.updates_per_step if L._adam is not None else 1
         if self._loop_graph is None:
             if not L.fused and L._graphs is None:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, capture_error_mode=capture_mode(L)):
                 self._rollout_step()
                 for _ in range(ups):
                     L._compute_grads()
+                    L._allreduce()  # data-parallel under RCCL: the SUM all-reduce, captured
                     L._apply()
             self._loop_graph = g
         L.before_replay()
@@ -452,9 +506,11 @@ class Trainer:
             L.update()
 
     def _graphed_iteration_dp(self) -> None:
-        """Data-parallel form: graph A = the rollout step + the first update's gradient, the
-        flat-bucket all-reduce (RCCL) between replays, graph B = Adam (+ target sync); further
-        updates of the iteration run the learner's own two-graph update."""
+        """Data-parallel form over a host-side collective (gloo): graph A = the rollout step + the
+        first update's gradient, the flat-bucket all-reduce between replays, graph B = Adam (+
+        target sync); further updates of the iteration run the learner's own two-graph update.
+        (Under RCCL the iteration is ONE graph with the all-reduce captured in it,
+        _graphed_iteration.)"""
         L = self.learner
         if self._loop_graph is None:
             if not L.fused and L._graphs is None:
@@ -625,6 +681,26 @@ class Trainer:
         if self.track:
             self.h_t0 = self.steps
             self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
+
+
+def capture_mode(learner) -> str:
+    """torch.cuda.graph's capture_error_mode for a graph of this learner's update: "thread_local"
+    when it holds the RCCL collective (ProcessGroupNCCL's watchdog thread keeps querying its events
+    while the capturing thread records), else torch's default "global"."""
+    return "thread_local" if learner.capture_collective else "global"
+
+
+def _flat_adam_state(per_param: list, params) -> dict:
+    """A torch-Adam checkpoint of the torch path (round 4: one {step, exp_avg, exp_avg_sq} dict per
+    parameter, or {} before the first step) as the device Adam's flat state."""
+    if not any(per_param):
+        z = torch.zeros(sum(p.numel() for p in params), dtype=params[0].dtype)
+        return {"adam_exp_avg": z, "adam_exp_avg_sq": z.clone(),
+                "step_dev": torch.zeros(1, dtype=torch.int64)}
+    cat = lambda k: torch.cat([d[k].reshape(-1).cpu() for d in per_param])  # noqa: E731
+    step = int(float(per_param[0]["step"]))
+    return {"adam_exp_avg": cat("exp_avg"), "adam_exp_avg_sq": cat("exp_avg_sq"),
+            "step_dev": torch.tensor([step], dtype=torch.int64)}
 
 
 def flops_per_update(net: str, batch: int) -> float:

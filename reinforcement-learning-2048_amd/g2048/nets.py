@@ -21,6 +21,12 @@ from torch.nn import functional as F
 
 
 # ------------------------------------------------------------------ split-K weight gradients
+# "gemm": bias gradients through the chunked GEMMs (the product path); "sum": torch's dim-0 sum over
+# all m rows, the round-3 form -- only tests/test_graph_hazards_gpu.py sets it, to reproduce the
+# captured-update failure that form showed
+BIAS_GRAD_FORM = "gemm"
+
+
 def _splits(m: int) -> int:
     """Row-chunk count for a weight gradient over m rows: ~512 rows per chunk, at most 64 chunks,
     a power of two dividing m (1 = no split)."""
@@ -62,7 +68,10 @@ class _LinearSplitK(torch.autograd.Function):
         # dense-ref update.)
         gb = None
         if ctx.needs_input_grad[2]:
-            gb = torch.bmm(gys.transpose(1, 2), gy.new_ones(s, m // s, 1)).sum(0)[:, 0]
+            if BIAS_GRAD_FORM == "sum":  # round 3's form: diagnostics only
+                gb = gy.sum(0)
+            else:
+                gb = torch.bmm(gys.transpose(1, 2), gy.new_ones(s, m // s, 1)).sum(0)[:, 0]
         # b is None for a bias-free layer: autograd takes no gradient for a non-tensor input
         return gx, gw, gb
 

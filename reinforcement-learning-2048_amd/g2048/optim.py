@@ -43,11 +43,18 @@ class FusedAdam:
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
 
-    def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor):
+    def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor, grad_scale: float = 1.0):
         """grad_flat: fp32 gradients of self.params packed in order; step_counter: device u64
-        holding t (>= 1) for this step's bias correction."""
-        N.check(N.load().g2048_adam_step_sync(
-            self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
-            N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
-            self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0,
-            N.stream_of(grad_flat.device)), "g2048_adam_step_sync")
+        holding t (>= 1) for this step's bias correction; grad_scale: the gradient is read as
+        grad * grad_scale (1 / world after a SUM all-reduce captured in the same graph)."""
+        lib = N.load()
+        args = (self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
+                N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
+                self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0)
+        if grad_scale == 1.0:
+            N.check(lib.g2048_adam_step_sync(*args, N.stream_of(grad_flat.device)),
+                    "g2048_adam_step_sync")
+        else:
+            N.check(lib.g2048_adam_step_scaled(*args, float(grad_scale),
+                                               N.stream_of(grad_flat.device)),
+                    "g2048_adam_step_scaled")

@@ -344,14 +344,21 @@ class Adam64:
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
 
-    def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor):
+    def step(self, grad_flat: torch.Tensor, step_counter: torch.Tensor, grad_scale: float = 1.0):
         """Adam over the flat float64 gradient (the data-parallel path: after the all-reduce);
-        step_counter: device u64 holding t; the target sync as attached."""
-        N.check(N.load().g2048_adam_step_sync_f64(
-            self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
-            N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
-            self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0,
-            N.stream_of(grad_flat.device)), "g2048_adam_step_sync_f64")
+        step_counter: device u64 holding t; the target sync as attached; the gradient read as
+        grad * grad_scale (1 / world after a SUM all-reduce)."""
+        lib = N.load()
+        args = (self._ptrs, self._numel, len(self.params), N.ptr(grad_flat), N.ptr(self.exp_avg),
+                N.ptr(self.exp_avg_sq), N.ptr(step_counter), self.lr, self.betas[0], self.betas[1],
+                self.eps, self._tptrs, self.sync_every if self._tptrs is not None else 0)
+        if grad_scale == 1.0:
+            N.check(lib.g2048_adam_step_sync_f64(*args, N.stream_of(grad_flat.device)),
+                    "g2048_adam_step_sync_f64")
+        else:
+            N.check(lib.g2048_adam_step_scaled_f64(*args, float(grad_scale),
+                                                   N.stream_of(grad_flat.device)),
+                    "g2048_adam_step_scaled_f64")
 
 
 class Dense64Update64:
@@ -424,7 +431,14 @@ class ConvUpdate64:
 
     def ensure_packed(self, force: bool = False) -> bool:
         """Pack both nets into the workspace if torch modified a parameter since the last pack
-        (or force).  Stream-ordered; returns whether it packed."""
+        (or force).  Stream-ordered; returns whether it packed.
+
+        Limit: the check keys on tensor version counters, which only torch's in-place ops bump.
+        A write that bypasses them -- `p.data.copy_(...)` on a detached alias, a c10d collective
+        into parameter storage, another raw-pointer kernel -- leaves the packed operands stale,
+        and the update would train on the old conv2 / fc1 weights: call ensure_packed(force=True)
+        after any such write.  (The fused kernels of this class keep the packs current
+        themselves; the library refuses an Adam update on a workspace never packed, ABI v4.)"""
         v = self._versions()
         if not force and v == self._packed_at:
             return False

@@ -48,11 +48,11 @@ def build_trainer(n_boards: int = 65536, net: str = "conv", dtype=torch.float32,
 def hyperparameters(trainer: Trainer, no_episodes: int, snapshot_game_every_n_episodes: int):
     """The HYPERPARAMS dict of src/configs/double_dqn_conv.py:49-66, for this build's run."""
     L = trainer.learner
-    lr = L._adam.lr if L.fused else L.opt.param_groups[0]["lr"]
+    lr = L._adam.lr if L._adam is not None else L.opt.param_groups[0]["lr"]
     return {"batch_size": L.B, "discount_factor": L.gamma, "model": str(L.model),
             "replay_buffer_length": trainer.replay.capacity, "learning_rate": lr,
             "loss_fn": "MSELoss()" if L.loss_fn is None else str(L.loss_fn),
-            "optimizer": "Adam (fused)" if L.fused else str(L.opt),
+            "optimizer": "Adam (one HIP launch, device t)" if L._adam is not None else str(L.opt),
             "no_episodes": no_episodes, "no_episodes_to_reach_epsilon": trainer.eps_decay,
             "min_epsilon": trainer.min_eps, "use_double_dqn": L.use_double_dqn,
             "snapshot_game_every_n_episodes": snapshot_game_every_n_episodes,

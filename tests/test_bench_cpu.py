@@ -37,13 +37,28 @@ def test_setup_dist_refuses_before_touching_gpu(monkeypatch):
 
 def test_rollout_roofline_residency():
     """bound 'hbm' only for a working set beyond the 256 MiB Infinity Cache."""
-    small = dict(ev_s=20 * 25e-6, n=65536, k=64, settle_ms=60.0,
+    small = dict(ev_s=20 * 25e-6, wall=20 * 26e-6, n=65536, k=64, settle_ms=60.0,
                  working_set=38 * 65536 * 64 + 65536 * 40)
     r = bench.rollout_roofline(small, 20, None)
     assert r["bound"] == "issue" and r["resident"] == "infinity-cache"
     assert abs(r["achieved"] - 38 * 65536 * 64 / 25e-6 / 1e9) < 1e-6
+    # both clocks carried: frac (= frac_events) from the events, frac_wall from ms_per_step's
+    assert r["frac"] == r["frac_events"]
+    assert abs(r["frac_wall"] - 38 * 65536 * 64 / 26e-6 / 1e9 / 8000.0) < 1e-9
     big = dict(small, working_set=8 * 38 * 65536 * 64)
     assert bench.rollout_roofline(big, 20, None)["bound"] == "hbm"
     rec = {"hbm_bytes_per_launch": 2.0e8, "source": "profiles/r04/pmc.json (box)"}
     t = bench.rollout_roofline(big, 20, rec)
     assert t["traffic"] == 2.0e8 and "profiles/r04/pmc.json" in t["traffic_source"]
+
+
+def test_pmc_summary_steps_per_launch():
+    """Issue counters are normalised per env step: K of the rollout key, with or without the
+    ring-launches suffix (round 4 parsed every key as K = 1)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_summary
+    assert pmc_summary.steps_of("k_rollout@65536x64") == 64
+    assert pmc_summary.steps_of("k_rollout@65536x64r8") == 64
+    assert pmc_summary.steps_of("k_rollout_ws@4194304x16") == 16
+    assert pmc_summary.steps_of("k_step@65536") == 1
+    assert pmc_summary.steps_of("k_rollout@65536x0") == 1

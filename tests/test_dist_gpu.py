@@ -152,3 +152,88 @@ def test_bench_two_ranks():
     for leg in ("dense64.fp32", "dense64.fp64", "dense@512.fp32", "dense@512.fp64"):
         assert line["learner"][leg]["ranks_lockstep"] is True, leg
     assert line["learner"]["dense@512.fp64"]["batch"] == 512
+
+
+def _rccl_worker(rank, port, net, dtype, out_dir):
+    """World-1 RCCL group on the one GPU: the data-parallel update with the SUM all-reduce
+    captured in its graph (one replay per update / per loop iteration) against the two-graph
+    form (gradient graph, host-issued collective, Adam graph), bitwise."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "reinforcement-learning-2048_amd")]
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import g2048
+    from g2048.learner import DQNLearner, Trainer
+
+    dt = torch.float64 if dtype == "fp64" else torch.float32
+    n = 1024
+    res = {}
+    # (a) learner updates
+    env = g2048.VecEnv2048(n, seed=9, device=dev)
+    rb = g2048.ReplayBuffer(16 * n, device=dev)
+    env.rollout(16, replay=rb)
+    outs = []
+    for captured in (True, False):
+        L = DQNLearner(rb, net=net, dtype=dt, batch_size=512, target_sync_every=2, seed=5,
+                       data_parallel=True)
+        assert L.dp and L.capture_collective
+        if not captured:
+            L.capture_collective = False  # the two-graph form with a host-issued collective
+        gen = torch.Generator(device=dev).manual_seed(4)
+        if not L.fused:  # the torch path samples with torch's RNG: same rows for both
+            torch.manual_seed(11)
+            torch.cuda.manual_seed(11)
+        grads = []
+        for _ in range(4):
+            L.update()
+            grads.append(L.grad_flat.clone())
+        torch.cuda.synchronize()
+        one_graph = L._graphs[1] is None
+        outs.append((torch.cat([p.detach().reshape(-1) for p in
+                                list(L.model.parameters()) + list(L.target.parameters())]).cpu(),
+                     torch.cat(grads).cpu(), one_graph))
+        del gen
+    res["update_same"] = torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    res["update_graphs"] = (outs[0][2], outs[1][2])
+    # (b) the training loop
+    loops = []
+    for captured in (True, False):
+        env = g2048.VecEnv2048(n, seed=11, device=dev)
+        rb = g2048.ReplayBuffer(16 * n, device=dev)
+        L = DQNLearner(rb, net=net, dtype=dt, batch_size=512, target_sync_every=3, seed=5,
+                       data_parallel=True)
+        if not captured:
+            L.capture_collective = False
+        T = Trainer(env, rb, L, updates_per_step=1, min_fill=0, eps_decay_episodes=20.0)
+        T.prefill(4)
+        for _ in range(7):
+            T.step()
+        torch.cuda.synchronize()
+        loops.append(torch.cat([env.board.reshape(-1).float().cpu(), rb.s.reshape(-1).float().cpu(),
+                                torch.cat([p.detach().reshape(-1) for p in L.model.parameters()]).cpu(),
+                                torch.cat([p.detach().reshape(-1) for p in L.target.parameters()]).cpu()]))
+        res.setdefault("loop_kinds", []).append(
+            type(T._loop_graph).__name__ if T._loop_graph is not None else None)
+    res["loop_same"] = torch.equal(loops[0], loops[1])
+    torch.save(res, os.path.join(out_dir, "res.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "fp64"])
+@pytest.mark.parametrize("net", ["conv", "dense64", "dense"])
+def test_rccl_captured_allreduce_equals_two_graph_form(tmp_path, net, dtype):
+    """under RCCL the data-parallel update -- and the training-loop iteration
+    -- is ONE hipGraph replay with the SUM all-reduce captured in it and 1 / world folded into
+    Adam (g2048_adam_step_scaled); on one GPU with a world-1 RCCL group it must equal the
+    two-graph form (gradient graph, host-issued all-reduce, Adam graph) bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X")
+    mp.spawn(_rccl_worker, args=(_free_port(), net, dtype, str(tmp_path)), nprocs=1, join=True)
+    res = torch.load(os.path.join(tmp_path, "res.pt"), weights_only=True)
+    assert res["update_graphs"] == (True, False), res["update_graphs"]
+    assert res["update_same"], "captured-collective update differs from the two-graph form"
+    assert res["loop_kinds"][0] == "CUDAGraph" and res["loop_kinds"][1] == "tuple"
+    assert res["loop_same"], "captured-collective loop differs from the two-graph loop"

@@ -21,14 +21,41 @@ def test_no_store_data_hazard(tmp_path):
     import store_hazard_audit
 
     out = []
-    for f in sorted(os.listdir(CSRC)):
-        if not f.endswith(".hip"):
-            continue
+    for f in audited_sources():
         s = str(tmp_path / (f + ".s"))
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only",
-                        "-S", os.path.join(CSRC, f), "-o", s], check=True, capture_output=True)
+        subprocess.run(audit_cmd(os.path.join(CSRC, f), s), check=True, capture_output=True)
         out.append(s)
     assert sum(store_hazard_audit.audit(s) for s in out) == 0
+
+
+def audited_sources():
+    """Exactly the sources the shipped library is built from (__graft_entry__.SRCS)."""
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as G
+    return list(G.SRCS)
+
+
+def audit_cmd(src: str, out: str) -> list:
+    """The library's own hipcc flags (__graft_entry__.HIPFLAGS: kernarg preloading changes the
+    kernels' prologues, register allocation and scheduling), minus the link-only ones, plus
+    device-only assembly output: the audit reads the code that ships."""
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as G
+    flags = [f for f in G.HIPFLAGS if f not in ("-shared", "-fPIC")]
+    return [G.HIPCC, *flags, "--cuda-device-only", "-S", src, "-o", out]
+
+
+def test_audit_uses_library_flags():
+    """A change of the library's build flags cannot silently move the audit off the shipped code
+    (kernarg preloading was on in the library but not in the audit)."""
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as G
+    cmd = audit_cmd("x.hip", "x.s")
+    for f in G.HIPFLAGS:
+        if f not in ("-shared", "-fPIC"):
+            assert f in cmd
+    assert "-amdgpu-kernarg-preload-count=16" in cmd
+    assert set(audited_sources()) == set(G.SRCS)
 
 
 def test_audit_sees_loads_and_branches(tmp_path):

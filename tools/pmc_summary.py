@@ -13,6 +13,7 @@ import csv
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 from collections import defaultdict
@@ -28,6 +29,14 @@ def kernel_key(name: str, grid: int):
     if "k_step" in name:
         return f"k_step@{grid}"
     return None
+
+
+def steps_of(key: str) -> int:
+    """Env steps per work-item in one launch of `key`: K of a rollout key "k_rollout@<N>x<K>"
+    (optionally suffixed "r<launches>", e.g. "k_rollout@65536x64r8" -> 64), 1 for k_step.  (Round
+    4 stripped every digit here and always returned 1, so its issue block was per launch.)"""
+    m = re.fullmatch(r"k_rollout(?:_ws)?@\d+x(\d+)(?:r\d+)?", key)
+    return int(m.group(1)) if m and int(m.group(1)) > 0 else 1
 
 
 def load(dirs):
@@ -76,7 +85,7 @@ def main(out_path, *dirs):
             rec.update(fetch_kb_raw=c["FETCH_SIZE"], write_kb=c["WRITE_SIZE"],
                        hbm_bytes_per_launch=(2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
         if "SQ_WAVES" in c and c["SQ_WAVES"] > 0:
-            steps = int(key.split("x")[1].rstrip("r0123456789") or 1) if key.startswith("k_rollout") else 1
+            steps = steps_of(key)
             # (k_rollout_ws: SQ_WAVES counts the compute and the store waves)
             per = lambda n: c.get(n, 0.0) / c["SQ_WAVES"] / steps  # noqa: E731
             rec["issue"] = {
