@@ -223,6 +223,9 @@ def settle(replay, ms: float, max_calls: int = 4000) -> float:
 
 
 def capture(fn, n_steps: int):
+    if dist.is_initialized() and BACKEND == "nccl":  # ProcessGroupNCCL's watchdog (g2048/dist.py)
+        from g2048.dist import quiesce_for_capture
+        quiesce_for_capture()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())

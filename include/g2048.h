@@ -485,6 +485,27 @@ G2048_API int g2048_densenet_forward_greedy(const g2048_densenet_params* params,
                                             double eps_decay_episodes, double eps_min,
                                             void* q_out_dev, void* stream);
 
+/* One whole Double-DQN update of the reference dense net (train_step, src/dqn_lib.py:119-164, +
+ * the target sync of :227-228) in float32 or float64 (dtype; y_out, workspace, grad_out,
+ * loss_out, exp_avg, exp_avg_sq and both nets' tensors of that type): the arguments, step_dev
+ * protocol, Philox sampler (idx_in NULL) or given rows, Bellman target (gamma the float32 torch
+ * uses), MSELoss(sum), gradient order (torch parameter order, grad_out[403716]) and Adam /
+ * target-sync semantics of g2048_convnet_update_f64.  With exp_avg / exp_avg_sq the update
+ * writes the online net's tensors (and the target's on a sync) through the params' pointers.
+ * Six launches: sampler, the two target-side forwards, the row tiles (forward with stored
+ * activations, MSE, the input-gradient GEMMs, dW1 / dW4 / bias terms), the dW2 / dW3 GEMMs
+ * (K = batch, split in row ranges), the fixed-order reduction with Adam.  workspace: dtype
+ * elements, g2048_densenet_update_workspace(batch, dtype) of them (since ABI v4). */
+G2048_API int64_t g2048_densenet_update_workspace(int64_t batch, int dtype);
+G2048_API int g2048_densenet_update(const g2048_densenet_params* online,
+                                    const g2048_densenet_params* target, int dtype,
+                                    g2048_replay* rb, const int64_t* idx_in_dev, int64_t batch,
+                                    uint64_t seed, uint64_t* step_dev, float gamma, int double_dqn,
+                                    int64_t* idx_out_dev, void* y_out_dev, void* workspace_dev,
+                                    void* grad_out_dev, void* loss_out_dev, void* exp_avg_dev,
+                                    void* exp_avg_sq_dev, double lr, double beta1, double beta2,
+                                    double eps, uint64_t sync_every, void* stream);
+
 /* g2048_adam_step_sync in float64: the Adam update of the float64 fused reductions (torch's Adam
  * with its scalars in double) over n_tensors (<= 16) float64 parameter tensors, for a
  * data-parallel float64 learner (gradient -> all-reduce -> this step). */

@@ -78,6 +78,10 @@ SIGNATURES = {
                                         _u64, _vp]),
     "g2048_adam_step_sync_f64": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
                                         _vp, _u64, _vp]),
+    "g2048_densenet_update_workspace": (_i64, [_i64, _int]),
+    "g2048_densenet_update": (_int, [_vp, _vp, _int, _vp, _vp, _i64, _u64, _vp, C.c_float, _int,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
+                                     _u64, _vp]),
     "g2048_adam_step_scaled": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl, _dbl,
                                       _vp, _u64, _dbl, _vp]),
     "g2048_adam_step_scaled_f64": (_int, [_vp, _vp, _int, _vp, _vp, _vp, _vp, _dbl, _dbl, _dbl,

@@ -87,6 +87,24 @@ def captures_collectives(group=None) -> bool:
             and dist.get_backend(group) == dist.Backend.NCCL)
 
 
+# ProcessGroupNCCL's watchdog thread polls the events of every eager collective until it sees them
+# complete (~every 100 ms).  A poll that lands while this thread captures a hipGraph invalidates the
+# capture (hipErrorStreamCaptureUnsupported, then a DistBackendError from the watchdog): seen once
+# in six captures on one GPU with a world-1 RCCL group.  Captures started after the watchdog has
+# retired every eager collective are safe (collectives enqueued DURING a capture are not handed to
+# the watchdog).
+QUIESCE_S = 0.35
+
+
+def quiesce_for_capture(group=None) -> None:
+    """Before a hipGraph capture in an RCCL process: drain the device and give ProcessGroupNCCL's
+    watchdog time to retire the eager collectives it still polls (no-op without RCCL)."""
+    if captures_collectives(group):
+        import time
+        torch.cuda.synchronize()
+        time.sleep(QUIESCE_S)
+
+
 def shard_offset(rank: int, boards_per_rank: int) -> int:
     """Global id of a rank's first board: Philox subsequences never overlap across ranks."""
     return rank * boards_per_rank

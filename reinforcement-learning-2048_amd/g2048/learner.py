@@ -19,7 +19,8 @@ import copy
 import torch
 
 from . import dqn_lib
-from .dist import FlatGradBucket, broadcast_params, captures_collectives, world_size
+from .dist import (FlatGradBucket, broadcast_params, captures_collectives, quiesce_for_capture,
+                   world_size)
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, make_net
 from . import qnet
@@ -112,21 +113,20 @@ class DQNLearner:
         self.graph = graph
         # fused HIP kernels (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip) for the fp32
         # conv and dense 16-64-4 nets; other nets / fp64 run the torch path
-        self.kind = qnet.kind_of(self.model) if self.loss_fn is None else None
         # float64 (the reference's precision): the dense 16-64-4 and conv nets have fused
-        # updates too (g2048_dense64_update_f64, g2048_convnet_update_f64); with world > 1 the
-        # gradient is all-reduced and g2048_adam_step_sync_f64 applies Adam
-        k64 = qnet.kind64_of(self.model)
-        self.f64 = self.kind is None and self.loss_fn is None and k64 is not None
-        if self.f64:
-            self.kind = k64
+        # updates too (g2048_dense64_update_f64, g2048_convnet_update_f64), and the reference
+        # dense net one in both dtypes (g2048_densenet_update); with world > 1 the gradient is
+        # all-reduced and the one-launch Adam follows
+        self.kind = qnet.update_kind(self.model) if self.loss_fn is None else None
+        self.f64 = self.kind is not None and next(self.model.parameters()).dtype == torch.float64
         self.fused = self.kind is not None
         self._upd = None
         # float64 conv: the rollout's Q through the fused forward as well
         self._fwd64 = qnet.ConvForward64(self.model) if self.f64 and self.kind == "conv" else None
         # the reference dense net on the torch path: the rollout's Q through one HIP launch
         # (g2048_densenet_forward[_greedy]) instead of torch's four GEMMs over every board
-        self._dfwd = (qnet.DenseForward(self.model) if not self.fused and self.device.type == "cuda"
+        self._dfwd = (qnet.DenseForward(self.model)
+                      if self.kind in (None, "dense") and self.device.type == "cuda"
                       and qnet.is_dense_ref(self.model) else None)
         # ... and, in float64, the update's two no-grad forwards (Q_online(s'), Q_target(s') of
         # the Bellman target, src/dqn_lib.py:125-144) as the same HIP launch on the sampled s'
@@ -134,10 +134,12 @@ class DQNLearner:
         # update).  Not in float32: its 64-row tiles put B = 8192 rows on 128 of the 256 CUs,
         # slower than torch's two GEMM forwards (0.74 -> 0.80 ms).
         self._dfwd_tg = (qnet.DenseForward(self.target)
-                         if self._dfwd is not None and self.dtype == torch.float64 else None)
+                         if self._dfwd is not None and not self.fused
+                         and self.dtype == torch.float64 else None)
         if self.fused:
-            self._p_on = None if self.f64 else qnet.net_params(self.model)
-            self._p_tgt = None if self.f64 else qnet.net_params(self.target)
+            small = not self.f64 and self.kind in ("conv", "dense64")
+            self._p_on = qnet.net_params(self.model) if small else None
+            self._p_tgt = qnet.net_params(self.target) if small else None
             # targets (sampler, both target-side forwards, Bellman), the graded half (forward +
             # MSE + backward) and a fixed-order slab reduction that writes the flat gradient
             # bucket or applies Adam (csrc/g2048_qnet.hip, g2048_qtrain.hip, g2048_mlp.hip).  The
@@ -152,7 +154,9 @@ class DQNLearner:
             # gradient reduction.  conv: targets (two half-grids, one net each), train forward,
             # train backward, reduce+Adam = 4 launches; dense64: sampler + targets + gradient in
             # ONE launch + reduce+Adam = 2 launches
-            if self.f64:
+            if self.kind == "dense":  # the reference dense net, float32 or float64
+                upd = qnet.DenseRefUpdate
+            elif self.f64:
                 upd = qnet.Dense64Update64 if self.kind == "dense64" else qnet.ConvUpdate64
             else:
                 upd = qnet.Dense64Update if self.kind == "dense64" else qnet.ConvUpdate
@@ -244,6 +248,7 @@ class DQNLearner:
                 self._allreduce()
                 self._apply()
         torch.cuda.current_stream(self.device).wait_stream(side)
+        quiesce_for_capture(self.pg)  # the warm-up's eager collectives retired first
         g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g1, capture_error_mode=capture_mode(self)):
             self._compute_grads()
@@ -311,12 +316,12 @@ class DQNLearner:
 
     @torch.no_grad()
     def q_values(self, env: VecEnv2048) -> torch.Tensor:
+        if self._dfwd is not None:
+            return self._dfwd(env.board)
         if self.fused and not self.f64:
             return qnet.forward(self.model, env.board, params=self._p_on)
         if self._fwd64 is not None:
             return self._fwd64(env.board)
-        if self._dfwd is not None:
-            return self._dfwd(env.board)
         x = env.encode(self.dtype, conv=self.conv_input)
         return self.model(x).reshape(env.n, 4).contiguous()
 
@@ -489,6 +494,7 @@ class Trainer:
         if self._loop_graph is None:
             if not L.fused and L._graphs is None:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
+            quiesce_for_capture(L.pg)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, capture_error_mode=capture_mode(L)):
                 self._rollout_step()
@@ -515,6 +521,7 @@ class Trainer:
         if self._loop_graph is None:
             if not L.fused and L._graphs is None:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
+            quiesce_for_capture(L.pg)
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(ga):
                 self._rollout_step()

@@ -113,6 +113,16 @@ def kind64_of(model) -> str | None:
     return "dense64" if is_dense64(model) else None
 
 
+def update_kind(model) -> str | None:
+    """The fused whole-update kernels that take this model: 'conv' / 'dense64' (float32 or
+    float64), 'dense' (the reference dense net, g2048_densenet_update, float32 or float64)."""
+    k = kind_of(model) or kind64_of(model)
+    if k is None and is_dense_ref(model) and next(model.parameters()).dtype in (torch.float32,
+                                                                                torch.float64):
+        return "dense"
+    return k
+
+
 def _tensors(model, order, dtype=torch.float32):
     sd = dict(model.named_parameters())
     ts = [sd[k] for k in order]
@@ -469,6 +479,52 @@ class ConvUpdate64:
             N.ptr(v), float(lr), float(b1), float(b2), float(eps),
             int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
             "g2048_convnet_update_f64")
+
+
+class DenseRefUpdate:
+    """One whole Double-DQN update of the reference dense net (src/configs/double_dqn_dense.py:
+    7-15) in float32 or float64 (g2048_densenet_update): the Philox sampler, the two target-side
+    forwards, the row tiles (forward with stored activations, MSE, the input-gradient GEMMs on
+    MFMA), the K = B weight-gradient GEMMs and the fixed-order reduction with Adam (FusedAdam /
+    Adam64 state; adam=None leaves the summed gradient in grad_out for a data-parallel
+    all-reduce).  The same call and step_dev protocol as ConvUpdate64."""
+
+    def __init__(self, model, target, batch: int, adam=None):
+        if not (is_dense_ref(model) and is_dense_ref(target)):
+            raise TypeError("DenseRefUpdate needs the reference dense net for online and target")
+        dt = next(model.parameters()).dtype
+        if dt not in (torch.float32, torch.float64):
+            raise TypeError("DenseRefUpdate runs float32 or float64 nets")
+        self.dtype = dt
+        self.code = N.F32 if dt == torch.float32 else N.F64
+        self._params = (_tensors(model, _DENSE_REF_ORDER, dt)
+                        + _tensors(target, _DENSE_REF_ORDER, dt))
+        self.on = N.DenseNetParams(*[t.data_ptr() for t in self._params[:8]])
+        self.tg = N.DenseNetParams(*[t.data_ptr() for t in self._params[8:]])
+        self.batch = int(batch)
+        self.adam = adam
+        dev = next(model.parameters()).device
+        n = N.load().g2048_densenet_update_workspace(self.batch, self.code)
+        self.workspace = torch.empty(n, dtype=dt, device=dev)
+
+    def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
+                 idx_in=None, grad_out=None, loss_out=None):
+        if idx_out.numel() != self.batch or y_out.numel() != self.batch:
+            raise ValueError("idx_out / y_out must have `batch` elements")
+        if y_out.dtype != self.dtype:
+            raise TypeError(f"y_out must be {self.dtype}")
+        if self.adam is None and grad_out is None:
+            raise ValueError("without Adam state the gradient needs a grad_out buffer")
+        a = self.adam
+        m, v = (a.exp_avg, a.exp_avg_sq) if a is not None else (None, None)
+        lr, b1, b2, eps = (a.lr, a.betas[0], a.betas[1], a.eps) if a is not None else (0, 0, 0, 0)
+        N.check(N.load().g2048_densenet_update(
+            C.byref(self.on), C.byref(self.tg), self.code, replay.handle, N.ptr(idx_in),
+            self.batch, int(seed), N.ptr(step_dev), float(gamma), int(bool(double_dqn)),
+            N.ptr(idx_out), N.ptr(y_out), N.ptr(self.workspace), N.ptr(grad_out),
+            N.ptr(loss_out), N.ptr(m), N.ptr(v), float(lr), float(b1), float(b2), float(eps),
+            int(a.sync_every) if a is not None else 0, N.stream_of(y_out.device)),
+            "g2048_densenet_update")
 
 
 class Dense64Update:

@@ -18,7 +18,7 @@ def _declared():
 def test_header_declares_abi():
     names = _declared()
     assert "g2048_env_step" in names and "g2048_replay_sample_encode" in names
-    assert len(names) == 53
+    assert len(names) == 55
 
 
 def test_library_exports_every_declared_symbol():

@@ -97,8 +97,8 @@ def test_dense_forward_rejects_other_nets(G):
 
 @pytest.mark.parametrize("dtype", ["float32", "float64"])
 def test_dense_trainer_graphed_greedy_equals_full_forward(G, dtype):
-    """The reference dense net on the torch path: the Trainer replays ONE captured graph per
-    iteration (HIP greedy-branch forward + fused eps-greedy step + the torch update), and 25
+    """The reference dense net: the Trainer replays ONE captured graph per iteration (HIP
+    greedy-branch forward + fused eps-greedy step + the fused update, g2048_densenet_update), and 25
     iterations are bitwise those of the same loop computing every board's Q (the boards start at
     mixed episode counts, so eps spans 1 .. min_epsilon)."""
     from g2048 import train
@@ -108,7 +108,7 @@ def test_dense_trainer_graphed_greedy_equals_full_forward(G, dtype):
     for greedy in (True, False):
         tr = _small(train, "dense", min_fill=3 * 1024, target_sync_every=3, track_boards=0,
                     dtype=getattr(torch, dtype))
-        assert tr.graph and tr.learner._dfwd is not None and not tr.learner.fused
+        assert tr.graph and tr.learner._dfwd is not None and tr.learner.kind == "dense"
         tr.greedy_forward = greedy
         grp = torch.arange(tr.env.n, device=DEV) % 5
         tr.env.ep[:, 0] = grp.to(torch.int32)
@@ -144,3 +144,115 @@ def test_dense_trainer_graphed_equals_eager(G):
         assert torch.equal(a[k], b[k]), k
     for x, y in zip(a["params"] + a["target"], b["params"] + b["target"]):
         torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5)
+
+
+def _dense_fixture_nets(g, dtype):
+    from g2048.nets import det_init, make_net
+
+    freq = float(g["init_freq"]) if "init_freq" in g else 1.3
+    tph = float(g["tgt_phase"]) if "tgt_phase" in g else 0.2
+    return (det_init(make_net("dense", dtype, DEV), 0.5, freq),
+            det_init(make_net("dense", dtype, DEV), tph, freq))
+
+
+@pytest.mark.parametrize("name", ["learner_dense", "learner_dense_b5000"])
+def test_dense_ref_fused_matches_reference(G, golden_dir, name):
+    """The fused float64 update of the reference dense net (g2048_densenet_update: six launches,
+    DQNLearner(net="dense", dtype=float64)) against the reference train_step fixtures -- B = 512
+    and BASELINE configs[0]'s B = 5000 (src/configs/double_dqn_dense.py:17): the loss within 1e-6
+    absolute, y to 1e-12, the fixture's sampled gradient entries and their sum / sum of squares,
+    and the sampled parameters after one Adam step (intended order) to 1e-10."""
+    import os
+    from g2048.learner import DQNLearner
+
+    g = np.load(os.path.join(golden_dir, name + ".npz"))
+    rb = G.ReplayBuffer(len(g["buf_a"]), device=DEV)
+    rb.load(g["buf_s"], g["buf_a"], g["buf_r"], g["buf_s2"], g["buf_d"])
+    idx = torch.from_numpy(g["idx"]).to(DEV)
+    m, tg = _dense_fixture_nets(g, torch.float64)
+    L = DQNLearner(rb, net="dense", dtype=torch.float64, batch_size=len(idx), lr=float(g["lr"]),
+                   target_sync_every=0, model=m, sampler=lambda B, r: idx)
+    assert L.fused and L.f64 and L.kind == "dense"
+    L.target.load_state_dict(tg.state_dict())
+    L.update()
+    torch.cuda.synchronize()
+    ref = float(g["loss_ref"])
+    assert abs(float(L.last_loss) - ref) <= 1e-6 + 1e-13 * abs(ref), (float(L.last_loss), ref)
+    assert torch.equal(L._idx, idx)
+    np.testing.assert_allclose(L._y.cpu().numpy(), g["y"], rtol=1e-12, atol=1e-9)
+    grad = L.grad_flat.cpu().numpy()
+    sel = g["grad_sel"]
+    gs = g["grads_sampled"]
+    np.testing.assert_allclose(grad[sel], gs, rtol=1e-10, atol=1e-10 * max(1.0, float(np.abs(gs).max())))
+    assert abs(grad.sum() - float(g["grad_sum"])) <= 1e-9 * max(1.0, abs(float(g["grad_sum"])))
+    assert abs((grad ** 2).sum() - float(g["grad_sumsq"])) <= 1e-9 * float(g["grad_sumsq"])
+    after = torch.cat([p.detach().reshape(-1) for p in L.model.parameters()]).cpu().numpy()
+    np.testing.assert_allclose(after[sel], g["params_after_sampled"], rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-9), (torch.float32, 2e-4)])
+@pytest.mark.parametrize("double_dqn", [True, False])
+@pytest.mark.parametrize("batch", [700, 5000, 8192])
+def test_dense_ref_fused_equals_autograd(G, batch, double_dqn, dtype, tol):
+    """Three fused updates of the reference dense net (Philox rows, Adam, target sync every 2)
+    against torch autograd through dqn_lib.dqn_loss on the same rows and the same pre-update
+    weights: loss and every parameter tensor's gradient to `tol` relative (float64 1e-9; float32
+    2e-4 -- fp32 sums over B rows in another order); B = 700 leaves a ragged last tile."""
+    import copy
+
+    from g2048 import dqn_lib
+    from g2048.learner import DQNLearner
+
+    n = 4096
+    env = G.VecEnv2048(n, seed=23, device=DEV)
+    rb = G.ReplayBuffer(4 * n, device=DEV)
+    env.rollout(4, replay=rb)
+    L = DQNLearner(rb, net="dense", dtype=dtype, batch_size=batch, target_sync_every=2, seed=8,
+                   use_double_dqn=double_dqn)
+    assert L.fused and L.kind == "dense"
+    for k in range(3):
+        m0, t0 = copy.deepcopy(L.model), copy.deepcopy(L.target)
+        L.update()
+        torch.cuda.synchronize()
+        rows = L._idx.clone()
+        assert int(rows.min()) >= 0 and int(rows.max()) < 4 * n
+        s, a, r, s2, d = dqn_lib.sample_experiences(batch, rb, DEV, None,
+                                                    dqn_lib.extract_samples_dense, dtype=dtype,
+                                                    idx=rows)
+        loss, _, y = dqn_lib.dqn_loss(m0, t0, s, a, r, s2, d, L.gamma, double_dqn, None)
+        loss.backward()
+        assert abs(float(L.last_loss) - float(loss)) <= tol * abs(float(loss)), k
+        torch.testing.assert_close(L._y, y, rtol=tol, atol=tol * float(y.abs().max()))
+        off = 0
+        for i, p in enumerate(m0.parameters()):
+            gl, gr = L.grad_flat[off:off + p.numel()], p.grad.reshape(-1)
+            assert float((gl - gr).norm()) <= tol * max(float(gr.norm()), 1e-30), (k, i)
+            off += p.numel()
+    assert int(L.step_dev) == 3
+
+
+def test_dense_ref_fused_dp_split_equals_folded(G):
+    """The data-parallel form (gradient only, then Adam64.step on the device counter) moves the
+    online and target weights bitwise like the update with Adam folded into its reduction."""
+    from g2048.learner import DQNLearner
+
+    n = 2048
+    env = G.VecEnv2048(n, seed=5, device=DEV)
+    rb = G.ReplayBuffer(4 * n, device=DEV)
+    env.rollout(4, replay=rb)
+    a = DQNLearner(rb, net="dense", dtype=torch.float64, batch_size=1000, target_sync_every=2,
+                   seed=2, graph=False)
+    b = DQNLearner(rb, net="dense", dtype=torch.float64, batch_size=1000, target_sync_every=2,
+                   seed=2, graph=False)
+    b.model.load_state_dict(a.model.state_dict())
+    b.target.load_state_dict(a.target.state_dict())
+    b._upd.adam = None
+    for _ in range(3):
+        a.update()
+        b._compute_grads()
+        b._adam.step(b.grad_flat, b.step_dev)
+        torch.cuda.synchronize()
+        assert torch.equal(a.grad_flat, b.grad_flat)
+        for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
+                        list(b.model.parameters()) + list(b.target.parameters())):
+            assert torch.equal(p, q)

@@ -39,7 +39,7 @@ def _worker(rank, world, port, net, out_dir, dtype="fp32"):
     L = DQNLearner(rb, net=net, dtype=torch.float64 if dtype == "fp64" else torch.float32,
                    batch_size=1024, target_sync_every=2,
                    seed=100 + rank)  # different seeds: the broadcast must equalise the init
-    fused = net != "dense"  # dense: the torch-ROCm path
+    fused = True  # every net here has a fused update (dense: g2048_densenet_update)
     assert L.world == world and L.fused == fused and L.f64 == (fused and dtype == "fp64")
     init = torch.cat([p.detach().reshape(-1).clone() for p in L.model.parameters()])
     for _ in range(3):

@@ -10,11 +10,15 @@ torch's dim-0 sum (`gy.sum(0)`) then.  Two explanations were open:
   (2) a kernel of the fused update writes outside its buffers, into memory the torch graph's
       private pool owns -- a memory-safety bug on the product path.
 
-test_captured_dim0_sum_replays captures exactly such a reduction and replays it (a) back to back,
-(b) with an unrelated HIP kernel between replays, (c) with the fused fp64 / fp32 conv update
-between replays.  test_fused_learners_stay_in_bounds runs every fused learner with every buffer
-it writes carved from one allocation between sentinel-filled margins and checks the margins.
-test_old_bias_form_in_captured_update re-runs the original failing case on the old form."""
+test_captured_dim0_sum_replays captures such a reduction alone and replays it (a) back to back,
+(b) with an unrelated kernel or torch graph between replays, (c) with the fused fp64 / fp32 conv
+update between replays: all exact.  test_fused_learners_stay_in_bounds runs every fused learner
+with every buffer it writes carved from one allocation between sentinel-filled margins: no margin
+byte changes, so (2) is ruled out.  The original case on the old form fails exactly when another
+GRAPH is replayed between the learner graph's replays (an unrelated torch graph suffices), and
+never with HIP's graph packet capture off (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0): a runtime issue of
+(1)'s kind, in HIP's pre-built graph packets.  The product path keeps torch's global reductions
+out of its captured graphs, and test_torch_path_survives_interleaved_graph_replays guards that."""
 import copy
 
 import numpy as np
@@ -84,7 +88,7 @@ def _between(G, kind):
     return L.update
 
 
-@pytest.mark.parametrize("between", ["none", "fill", "conv64", "conv32"])
+@pytest.mark.parametrize("between", ["none", "fill", "torchcap", "conv64", "conv32"])
 @pytest.mark.parametrize("rows", [16384, 36864, 73728])
 def test_captured_dim0_sum_replays(G, rows, between):
     """x.sum(0) of an f64 [rows, 64] tensor produced inside the graph (the shape of the conv net's
@@ -165,7 +169,8 @@ def _carve_net(arena, base, model, dt):
 
 
 @pytest.mark.parametrize("batch", [700, 3000, 4096, 8192])
-@pytest.mark.parametrize("path", ["conv64", "conv32", "dense64_64", "dense64_32"])
+@pytest.mark.parametrize("path", ["conv64", "conv32", "dense64_64", "dense64_32", "dense_64",
+                                  "dense_32"])
 def test_fused_learners_stay_in_bounds(G, path, batch):
     """Every buffer a fused update writes -- both nets' parameters (Adam, the target sync), Adam's
     moments, the workspace (packed operands, slabs, dZ2 / dM, pre), grad_out, y, idx, the loss and
@@ -176,7 +181,7 @@ def test_fused_learners_stay_in_bounds(G, path, batch):
     from g2048.nets import make_net
     from g2048.optim import FusedAdam
 
-    net = "conv" if path.startswith("conv") else "dense64"
+    net = path.rsplit("_", 1)[0] if path.startswith("dense") else "conv"
     f64 = path.endswith("64")
     dt = torch.float64 if f64 else torch.float32
     n = 2048
@@ -191,7 +196,9 @@ def test_fused_learners_stay_in_bounds(G, path, batch):
     wsn = {"conv64": N.load().g2048_convnet_update_f64_workspace,
            "conv32": N.load().g2048_convnet_train_workspace,
            "dense64_64": N.load().g2048_dense64_update_f64_workspace,
-           "dense64_32": N.load().g2048_dense64_update_workspace}[path](batch)
+           "dense64_32": N.load().g2048_dense64_update_workspace,
+           "dense_64": lambda b: N.load().g2048_densenet_update_workspace(b, N.F64),
+           "dense_32": lambda b: N.load().g2048_densenet_update_workspace(b, N.F32)}[path](batch)
     assert wsn > 0
     words = lambda k: (k * (8 if f64 else 4) + 7) // 8  # noqa: E731  (int64 words of k elements)
     nparam = len(list(model.parameters()))
@@ -211,12 +218,13 @@ def test_fused_learners_stay_in_bounds(G, path, batch):
     step = A.piece(k + 6, torch.int64, 1)
     loss = A.piece(k + 7, dt, 1).view(())
     cls = {"conv64": qnet.ConvUpdate64, "conv32": qnet.ConvUpdate,
-           "dense64_64": qnet.Dense64Update64, "dense64_32": qnet.Dense64Update}[path]
+           "dense64_64": qnet.Dense64Update64, "dense64_32": qnet.Dense64Update,
+           "dense_64": qnet.DenseRefUpdate, "dense_32": qnet.DenseRefUpdate}[path]
     upd = cls(model, target, batch, adam=adam)
     upd.workspace = ws
     if hasattr(upd, "ensure_packed"):
         upd.ensure_packed(force=True)
-    assert nparam == 8 or nparam == 4
+    assert nparam in (4, 8)
     for _ in range(3):
         upd(rb, idx, y, step, 0.8, True, 77, None, grad_out=grad, loss_out=loss)
     bad = A.margins_clean()
@@ -231,13 +239,11 @@ def test_fused_learners_stay_in_bounds(G, path, batch):
     assert torch.isfinite(grad).all() and all(torch.isfinite(p).all() for p in model.parameters())
 
 
-@pytest.mark.parametrize("between", ["none", "fill", "torchcap", "conv64", "conv64_eager",
-                                     "conv64_captureonly", "conv32"])
-def test_old_bias_form_in_captured_update(G, between):
-    """The round-3 bias-gradient form (torch's dim-0 sum over every row) inside the torch-path
-    learner's captured float64 conv update at B = 4096, replays interleaved with other work,
-    against the same learner run eagerly: records whether the form still fails (the test asserts
-    agreement; see DESIGN 4.7 for what it showed)."""
+def _interleaved_errors(G, between, form):
+    """Four updates of a torch-path learner's captured float64 conv update at B = 4096 against the
+    same learner run eagerly (same rows and weights), with `between` run after each update; the
+    bias gradients in `form` ("sum": torch's dim-0 sum, round 3; "gemm": the product path).
+    Returns the per-update, per-tensor relative gradient errors."""
     from g2048 import nets
     from g2048.learner import DQNLearner
 
@@ -248,7 +254,7 @@ def test_old_bias_form_in_captured_update(G, between):
     rows = torch.zeros(B, dtype=torch.int64, device=DEV)
     work = _between(G, between)
     old = nets.BIAS_GRAD_FORM
-    nets.BIAS_GRAD_FORM = "sum"
+    nets.BIAS_GRAD_FORM = form
     try:
         kw = dict(net="conv", dtype=torch.float64, batch_size=B, target_sync_every=2, seed=7,
                   loss_fn=torch.nn.L1Loss(reduction="sum"), sampler=lambda b, r: rows)
@@ -259,7 +265,7 @@ def test_old_bias_form_in_captured_update(G, between):
         b.target.load_state_dict(a.target.state_dict())
         gen = torch.Generator(device=DEV).manual_seed(3)
         sizes = [p.numel() for p in a.model.parameters()]
-        errs, stale, prev = [], [], None
+        errs = []
         for k in range(4):
             rows.copy_(torch.randint(0, 16 * n, (B,), device=DEV, generator=gen))
             a.update()
@@ -271,16 +277,6 @@ def test_old_bias_form_in_captured_update(G, between):
                 e.append(float((ga - gb).norm()) / max(float(gb.norm()), 1e-300))
                 off += sz
             errs.append(e)
-            # is a wrong gradient the previous update's? (distance of each of a's tensors to b's
-            # gradient of the update before)
-            if prev is not None:
-                off, e2 = 0, []
-                for sz in sizes:
-                    ga, gp = a.grad_flat[off:off + sz], prev[off:off + sz]
-                    e2.append(float((ga - gp).norm()) / max(float(gp.norm()), 1e-300))
-                    off += sz
-                stale.append(e2)
-            prev = b.grad_flat.clone()
             with torch.no_grad():
                 for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
                                 list(b.model.parameters()) + list(b.target.parameters())):
@@ -289,8 +285,53 @@ def test_old_bias_form_in_captured_update(G, between):
             torch.cuda.synchronize()
     finally:
         nets.BIAS_GRAD_FORM = old
-    print("per-update, per-tensor relative gradient errors:", errs)
-    print("distance to the previous update's gradient:", stale)
+    return errs
+
+
+# interleavings: nothing, an eager torch kernel, another captured torch graph replayed, the fused
+# conv learner's captured update (fp64 / fp32), the same run eagerly, its capture without replays
+BETWEEN = ["none", "fill", "torchcap", "conv64", "conv64_eager", "conv64_captureonly", "conv32"]
+
+
+@pytest.mark.parametrize("between", BETWEEN)
+def test_torch_path_survives_interleaved_graph_replays(G, between):
+    """The product path (bias gradients through the chunked GEMMs, nets.Linear) is exact in every
+    interleaving -- in particular with other graphs replayed between the captured update's
+    replays, where a torch global reduction inside the graph goes wrong (below).  A global
+    reduction that re-enters the captured learner graph makes this test fail."""
+    errs = _interleaved_errors(G, between, "gemm")
+    assert max(max(e) for e in errs) <= 1e-9, errs
+
+
+@pytest.mark.parametrize("between", ["torchcap", "conv64"])
+def test_old_bias_form_packet_capture_repro(G, between):
+    """Round 4's failure, reproduced on the old form: torch's dim-0 sum over the 36 864 rows of
+    conv1's bias gradient, captured in the update graph, comes out wrong on every replay after
+    ANOTHER graph was replayed in between (a torch graph of unrelated ops does it as well as the
+    fused learner's: `torchcap`), never with eager work in between or without replays, and not
+    with HIP's graph packet capture off (test_old_bias_form_without_packet_capture).  Expected to
+    fail while the runtime has the bug: xfail then, a pass once it is fixed."""
+    errs = _interleaved_errors(G, between, "sum")
+    bad = max(max(e) for e in errs)
+    if bad > 1e-9:
+        assert max(errs[0]) <= 1e-9  # the first replay (before any interleaved graph) is right
+        pytest.xfail(f"HIP graph packet capture: conv1 bias gradient off by {bad:.3g} (relative)")
+
+
+def test_old_bias_form_without_packet_capture(tmp_path):
+    """The same interleaving with DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 (HIP's graph launch without
+    its pre-built AQL packets) is exact: the wrong sums come from the runtime's packet-capture
+    path, not from the kernels of either learner (whose buffers stay in bounds, above)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, DEBUG_CLR_GRAPH_PACKET_CAPTURE="0")
+    out = subprocess.run([sys.executable, __file__, "torchcap"], capture_output=True, text=True,
+                         env=env, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    errs = json.loads(out.stdout.strip().splitlines()[-1])
     assert max(max(e) for e in errs) <= 1e-9, errs
 
 
@@ -326,3 +367,16 @@ def test_unpacked_workspace_refused(G):
     with pytest.raises(N.NativeError, match="packed"):
         other(*args)
     torch.cuda.synchronize()
+
+
+if __name__ == "__main__":  # test_old_bias_form_without_packet_capture's child: one interleaving
+    import json
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "reinforcement-learning-2048_amd")]
+    import g2048
+
+    g2048.load_native()
+    print(json.dumps(_interleaved_errors(g2048, sys.argv[1], "sum")))

@@ -434,7 +434,9 @@ def test_dense_ref_f64_hip_targets(G, double_dqn):
     env.rollout(8, replay=rb)
     rows = torch.zeros(2000, dtype=torch.int64, device=DEV)
     L = DQNLearner(rb, net="dense", dtype=torch.float64, batch_size=2000, target_sync_every=2,
-                   seed=4, use_double_dqn=double_dqn)
+                   seed=4, use_double_dqn=double_dqn,
+                   loss_fn=torch.nn.L1Loss(reduction="sum"))  # the torch path ...
+    L.loss_fn = None  # ... with the MSE(sum) loss
     assert not L.fused and L._dfwd_tg is not None
     L.sampler = lambda B, r: rows
     gen = torch.Generator(device=DEV).manual_seed(1)
@@ -494,3 +496,37 @@ def test_torch_path_graph_replays_match_eager(G, net, dtype):
             for p, q in zip(list(a.model.parameters()) + list(a.target.parameters()),
                             list(b.model.parameters()) + list(b.target.parameters())):
                 p.copy_(q)
+
+
+@pytest.mark.parametrize("double_dqn", [True, False])
+@pytest.mark.parametrize("batch", [700, 4096, 8192])
+def test_conv64_train_a8_equals_four_wave(G, batch, double_dqn):
+    """The eight-wave train A (k_conv64_train_a8, two waves per SIMD) keeps every sum of the
+    four-wave k_conv64_train_a in the same order: three float64 conv updates with each (the
+    eight-wave one selected by G2048_CONV64_TRAIN_A=8) agree bit for bit -- y, loss, the summed
+    gradient (the reduce writes it beside the folded Adam) and both nets' weights."""
+    from g2048.learner import DQNLearner
+
+    n = 2048
+    env = G.VecEnv2048(n, seed=31, device=DEV)
+    rb = G.ReplayBuffer(16 * n, device=DEV)
+    env.rollout(16, replay=rb)
+    outs = []
+    for eight in (False, True):
+        if eight:
+            os.environ["G2048_CONV64_TRAIN_A"] = "8"
+        try:
+            L = DQNLearner(rb, net="conv", dtype=torch.float64, batch_size=batch, seed=6,
+                           target_sync_every=2, graph=False, use_double_dqn=double_dqn)
+            assert L.fused and L.f64
+            res = []
+            for _ in range(3):
+                L.update()
+                torch.cuda.synchronize()
+                res += [L._y.clone(), L.last_loss.reshape(1).clone(), L.grad_flat.clone()]
+            res += [p.detach().reshape(-1).clone() for p in
+                    list(L.model.parameters()) + list(L.target.parameters())]
+            outs.append(torch.cat(res))
+        finally:
+            os.environ.pop("G2048_CONV64_TRAIN_A", None)
+    assert torch.equal(outs[0], outs[1])

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Sweep of the dense-ref update's weight-gradient row splits (G2048_DENSE_NSPLIT): one learner
+per setting and dtype on the same ring, each captured with its setting, timed with HIP events
+after a clock settle; prints us per update."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "reinforcement-learning-2048_amd")]
+import torch  # noqa: E402
+
+import g2048  # noqa: E402
+from g2048.learner import DQNLearner  # noqa: E402
+
+
+def main(batch=8192, reps=100):
+    dev = torch.device("cuda", 0)
+    n = 65536
+    env = g2048.VecEnv2048(n, seed=7, device=dev)
+    rb = g2048.ReplayBuffer(16 * n, device=dev)
+    env.rollout(16, replay=rb)
+    for dt in (torch.float64, torch.float32):
+        for ns in (8, 10, 16, 20, 24):
+            os.environ["G2048_DENSE_NSPLIT"] = str(ns)
+            L = DQNLearner(rb, net="dense", dtype=dt, batch_size=batch, seed=3)
+            L.update()
+            os.environ.pop("G2048_DENSE_NSPLIT", None)
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.1:
+                L.update()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                L.update()
+            e1.record()
+            torch.cuda.synchronize()
+            print(f"{str(dt)[6:]} nsplit {ns}: {e0.elapsed_time(e1) / reps * 1e3:.1f} us per update",
+                  flush=True)
+            del L
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main(*[int(x) for x in sys.argv[1:]])
