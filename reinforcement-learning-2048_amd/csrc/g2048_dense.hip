@@ -337,7 +337,7 @@ constexpr int S_W1 = 0, S_B1 = S_W1 + NP_W1, S_B2 = S_B1 + 512, S_B3 = S_B2 + 51
 constexpr int WG_BLK = 128, WG_KC = 16, WG_TILES = 16 + 8;
 // row ranges of the weight-gradient GEMMs (runtime: G2048_DENSE_NSPLIT for tuning, at most
 // MAX_NSPLIT, which sizes the workspace)
-constexpr int NSPLIT_DEFAULT = 10, MAX_NSPLIT = 32;
+constexpr int NSPLIT_DEFAULT = 10, MAX_NSPLIT = 16;
 constexpr int PART = NP_W2 + NP_W3;  // one split's partial dW2 | dW3
 
 template <typename T>

@@ -21,7 +21,7 @@ def main(batch=8192, reps=100):
     rb = g2048.ReplayBuffer(16 * n, device=dev)
     env.rollout(16, replay=rb)
     for dt in (torch.float64, torch.float32):
-        for ns in (8, 10, 16, 20, 24):
+        for ns in (8, 10, 12, 16):
             os.environ["G2048_DENSE_NSPLIT"] = str(ns)
             L = DQNLearner(rb, net="dense", dtype=dt, batch_size=batch, seed=3)
             L.update()
