@@ -441,6 +441,47 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
     TPHASE(7);
 }
 
+// slab position -> torch flat parameter index
+__device__ __forceinline__ int slab_to_param(int pos) {
+    if (pos < SL_WF1) {  // ((mt*4 + i)*NT + t)*4 + tap: o = 16*wave + l16, c = 16mt + 4g + i
+        const int tap = pos & 3, t = (pos >> 2) & (NT - 1), r = pos >> 10;
+        const int lane = t & 63, o = 16 * (t >> 6) + (lane & 15);
+        const int c = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
+        return P_W2 + o * 256 + c * 4 + tap;
+    }
+    if (pos < SL_SMALL) {  // (jt*16 + e*4 + i)*NT + t: j = 16jt + 4g + i, flat m = 4c' + q with
+                           // c' = 16e + l16, q = wave
+        const int p2 = pos - SL_WF1, t = p2 & (NT - 1), r = p2 >> 8;
+        const int lane = t & 63;
+        const int j = 16 * (r >> 4) + 4 * (lane >> 4) + (r & 3);
+        const int m = 4 * (16 * ((r >> 2) & 3) + (lane & 15)) + (t >> 6);
+        return P_WF1 + j * 256 + m;
+    }
+    const int p3 = pos - SL_SMALL;  // w1 | b1 | b2 | bf1 | wf2 | bf2 in torch order
+    if (p3 < 256) return P_W1 + p3;
+    if (p3 < 320) return P_B1 + p3 - 256;
+    if (p3 < 384) return P_B2 + p3 - 320;
+    if (p3 < 448) return P_BF1 + p3 - 384;
+    if (p3 < 704) return P_WF2 + p3 - 448;
+    return P_BF2 + p3 - 704;
+}
+
+// train bwd's sums of train fwd's slab terms go to `pre` in torch parameter order, so that
+// k_reduce_pre's Adam operands (m, v, the parameters) and its gradient stores are coalesced
+// float4s.  A slab float4 is four contiguous, 16-byte aligned torch positions everywhere except in
+// fc1.weight's block, whose four positions scatter (stride 4); the loss stays at P_TOTAL.
+__device__ __forceinline__ void store_pre_torch(float* pre, int f4, float4 s) {
+    const int pos = f4 * 4;
+    if (pos >= SL_WF1 && pos < SL_SMALL) {
+        pre[slab_to_param(pos)] = s.x;
+        pre[slab_to_param(pos + 1)] = s.y;
+        pre[slab_to_param(pos + 2)] = s.z;
+        pre[slab_to_param(pos + 3)] = s.w;
+    } else {
+        *reinterpret_cast<float4*>(pre + slab_to_param(pos)) = s;
+    }
+}
+
 __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
     __shared__ __attribute__((aligned(16))) float lds[K2_FLOATS];
     const int t = threadIdx.x, lane = t & 63, g = lane >> 4, l16 = lane & 15, wave = t >> 6;
@@ -601,36 +642,11 @@ __global__ __launch_bounds__(NT) void k_conv_train_bwd(TrainArgs A) {
         __syncthreads();
         if (wave == 0 && sh_on) {
             const float4 a = sh.acc, b = part[0][lane], c = part[1][lane], d = part[2][lane];
-            reinterpret_cast<float4*>(A.pre)[f4] =
-                make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
-                            ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w);
+            store_pre_torch(A.pre, f4,
+                            make_float4(((a.x + b.x) + c.x) + d.x, ((a.y + b.y) + c.y) + d.y,
+                                        ((a.z + b.z) + c.z) + d.z, ((a.w + b.w) + c.w) + d.w));
         }
     }
-}
-
-// slab position -> torch flat parameter index
-__device__ __forceinline__ int slab_to_param(int pos) {
-    if (pos < SL_WF1) {  // ((mt*4 + i)*NT + t)*4 + tap: o = 16*wave + l16, c = 16mt + 4g + i
-        const int tap = pos & 3, t = (pos >> 2) & (NT - 1), r = pos >> 10;
-        const int lane = t & 63, o = 16 * (t >> 6) + (lane & 15);
-        const int c = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
-        return P_W2 + o * 256 + c * 4 + tap;
-    }
-    if (pos < SL_SMALL) {  // (jt*16 + e*4 + i)*NT + t: j = 16jt + 4g + i, flat m = 4c' + q with
-                           // c' = 16e + l16, q = wave
-        const int p2 = pos - SL_WF1, t = p2 & (NT - 1), r = p2 >> 8;
-        const int lane = t & 63;
-        const int j = 16 * (r >> 4) + 4 * (lane >> 4) + (r & 3);
-        const int m = 4 * (16 * ((r >> 2) & 3) + (lane & 15)) + (t >> 6);
-        return P_WF1 + j * 256 + m;
-    }
-    const int p3 = pos - SL_SMALL;  // w1 | b1 | b2 | bf1 | wf2 | bf2 in torch order
-    if (p3 < 256) return P_W1 + p3;
-    if (p3 < 320) return P_B1 + p3 - 256;
-    if (p3 < 384) return P_B2 + p3 - 320;
-    if (p3 < 448) return P_BF1 + p3 - 384;
-    if (p3 < 704) return P_WF2 + p3 - 448;
-    return P_BF2 + p3 - 704;
 }
 
 // Optional Adam folded into the reduction (single process): each final gradient element is
@@ -645,6 +661,7 @@ struct ReduceAdam {
     double lr, b1, b2, eps;
     unsigned long long sync_every;
     int on;
+    int vec;  // m, v, every parameter (both nets) and grad_out 16-byte aligned: float4 accesses
 };
 
 // The Adam operands of the four positions of slab float4 p4 (loaded with the slabs: they do not
@@ -654,8 +671,33 @@ struct AdamLane {
     float am[4], av[4], ap[4];
 };
 
+// conv2.weight's slab float4s (positions < SL_WF1) hold the four taps of one (o, c): contiguous and
+// 16-byte aligned in torch order too, so their Adam operands move as float4s (a quarter of the
+// scattered lines per wave).  The test is wave-uniform: a wave's 256 positions never straddle
+// SL_WF1.
+__device__ __forceinline__ bool w2_vec(const ReduceAdam& R, int p4) {
+    return R.vec && p4 * 4 < SL_WF1;
+}
+
 __device__ __forceinline__ void adam_load(const ReduceAdam& R, int p4, AdamLane& L) {
     constexpr int off[9] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2, P_TOTAL};
+    if (w2_vec(R, p4)) {
+        const int pi = slab_to_param(p4 * 4);
+        const float4 m4 = *reinterpret_cast<const float4*>(R.m + pi);
+        const float4 v4 = *reinterpret_cast<const float4*>(R.v + pi);
+        const float4 p4v = *reinterpret_cast<const float4*>(R.p[2] + (pi - P_W2));
+        const float am[4] = {m4.x, m4.y, m4.z, m4.w}, av[4] = {v4.x, v4.y, v4.z, v4.w};
+        const float ap[4] = {p4v.x, p4v.y, p4v.z, p4v.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            L.kt[e] = 2;
+            L.ei[e] = pi - P_W2 + e;
+            L.am[e] = am[e];
+            L.av[e] = av[e];
+            L.ap[e] = ap[e];
+        }
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int pos = p4 * 4 + e;
@@ -678,6 +720,22 @@ __device__ __forceinline__ void finish4(const ReduceAdam& R, bool adam, const g2
                                         unsigned long long t, int p4, float4 sv, AdamLane& L,
                                         float* grad, float* loss) {
     const float se[4] = {sv.x, sv.y, sv.z, sv.w};
+    if (w2_vec(R, p4)) {  // the same per-element update, float4 loads and stores (see adam_load)
+        const int pi = slab_to_param(p4 * 4);
+        if (grad) *reinterpret_cast<float4*>(grad + pi) = sv;
+        if (adam) {
+            float np[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) np[e] = g2048::adam_update(c, se[e], L.am[e], L.av[e], L.ap[e]);
+            *reinterpret_cast<float4*>(R.m + pi) = make_float4(L.am[0], L.am[1], L.am[2], L.am[3]);
+            *reinterpret_cast<float4*>(R.v + pi) = make_float4(L.av[0], L.av[1], L.av[2], L.av[3]);
+            const float4 n4 = make_float4(np[0], np[1], np[2], np[3]);
+            *reinterpret_cast<float4*>(R.p[2] + (pi - P_W2)) = n4;
+            if (R.sync_every && t % R.sync_every == 0ull)
+                *reinterpret_cast<float4*>(R.tp[2] + (pi - P_W2)) = n4;
+        }
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const int pos = p4 * 4 + e;
@@ -699,39 +757,76 @@ __device__ __forceinline__ void finish4(const ReduceAdam& R, bool adam, const g2
     }
 }
 
-// With `pre` (train bwd summed train fwd's slab terms): four waves per block.  Blocks
-// [0, NB_PRE4) take one float4 of `pre` per thread (conv1's float4s skipped); blocks NB_PRE4 + c
-// sum conv1's float4s [C1_F4_LO + 16 c, + 16) over the slabs -- thread (q = t % 16, j = t / 16)
-// the slabs j, j + 16, ... (16 loads in flight), then 16 threads add the 16 partials in j order.
-constexpr int NB_PRE4 = (SL_LOSS / 4 + 256) / 256;
+// With `pre` (train bwd summed train fwd's slab terms into it, in torch order): blocks
+// [0, NB_PRE4) take one torch float4 per thread of their first wave (the other three waves exit
+// at once) -- coalesced loads of `pre`, m, v and the parameter, coalesced stores, spread one wave
+// per CU.  conv1's weight and bias (torch float4s [0, C1_Q4)) are train bwd's own terms: blocks
+// NB_PRE4 + c sum its float4s [16 c, + 16) over the slabs (slab float4 C1_F4_LO + q) -- thread
+// (q = t % 16, j = t / 16) the slabs j, j + 16, ... (16 loads in flight), then 16 threads add the
+// 16 partials in j order.
+constexpr int PRE_F4_PER_BLOCK = 64;
+constexpr int TQ4 = P_TOTAL / 4 + 1;  // torch float4s, the loss's last
+constexpr int C1_Q4 = P_W2 / 4;
+constexpr int NB_PRE4 = (TQ4 + PRE_F4_PER_BLOCK - 1) / PRE_F4_PER_BLOCK;
+static_assert(C1_F4_HI - C1_F4_LO == C1_Q4 && SL_SMALL + P_W2 == C1_F4_HI * 4 &&
+                  P_TOTAL % 4 == 0 && P_B1 % 4 == 0 && P_B2 % 4 == 0 && P_WF1 % 4 == 0 &&
+                  P_BF1 % 4 == 0 && P_WF2 % 4 == 0 && P_BF2 % 4 == 0,
+              "conv1 = torch [0, P_W2) = slab [SL_SMALL, + P_W2); no float4 straddles two tensors");
+
+// four consecutive floats: one float4 access when the operands are 16-byte aligned (R.vec)
+__device__ __forceinline__ float4 ld4(const float* p, bool vec) {
+    if (vec) return *reinterpret_cast<const float4*>(p);
+    return make_float4(p[0], p[1], p[2], p[3]);
+}
+__device__ __forceinline__ void st4(float* p, float4 v, bool vec) {
+    if (vec) {
+        *reinterpret_cast<float4*>(p) = v;
+    } else {
+        p[0] = v.x;
+        p[1] = v.y;
+        p[2] = v.z;
+        p[3] = v.w;
+    }
+}
 
 __global__ __launch_bounds__(256) void k_reduce_pre(const float* slab, int nslab, const float* pre,
                                                     float* grad, float* loss, ReduceAdam R) {
     __shared__ float4 part[16][16];
     const int t = threadIdx.x;
     const bool c1 = (int)blockIdx.x >= NB_PRE4;
-    const int p4 = c1 ? C1_F4_LO + ((int)blockIdx.x - NB_PRE4) * C1_PER_BLOCK + (t & 15)
-                      : (int)blockIdx.x * 256 + t;
-    const bool fin = c1 ? t < C1_PER_BLOCK
-                        : p4 * 4 <= SL_LOSS && !(p4 >= C1_F4_LO && p4 < C1_F4_HI);
-    const bool adam = R.on && fin;
-    AdamLane L;
+    if (!c1 && t >= PRE_F4_PER_BLOCK) return;  // (no barrier in these blocks)
+    const int q = c1 ? ((int)blockIdx.x - NB_PRE4) * C1_PER_BLOCK + (t & 15)
+                     : (int)blockIdx.x * PRE_F4_PER_BLOCK + t;
+    const bool fin = c1 ? t < C1_PER_BLOCK : q >= C1_Q4 && q < TQ4;
+    const bool is_loss = q == TQ4 - 1;
+    const bool adam = R.on && fin && !is_loss;
+    const bool vec = R.vec != 0;
+    // the Adam operands, loaded with the sums (independent of them)
+    constexpr int off[8] = {P_W1, P_B1, P_W2, P_B2, P_WF1, P_BF1, P_WF2, P_BF2};
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < 8; ++j) k += q * 4 >= off[j] ? 1 : 0;
+    const int ei = q * 4 - off[k];
     unsigned long long st = 0;
+    float4 m4 = make_float4(0.f, 0.f, 0.f, 0.f), v4 = m4, p4v = m4;
     if (adam) {
         st = *R.step;
-        adam_load(R, p4, L);
+        m4 = ld4(R.m + q * 4, vec);
+        v4 = ld4(R.v + q * 4, vec);
+        p4v = ld4(R.p[k] + ei, vec);
     }
     float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
     if (!c1) {
-        if (fin) sv = reinterpret_cast<const float4*>(pre)[p4];
+        if (fin) sv = reinterpret_cast<const float4*>(pre)[q];
     } else {
         const int j = t >> 4;
+        const int s4 = C1_F4_LO + q;
         for (int g0 = 0; g0 < nslab; g0 += 256) {
             float4 r[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) {
                 const int g = g0 + j + 16 * u;
-                r[u] = g < nslab ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[p4]
+                r[u] = g < nslab ? reinterpret_cast<const float4*>(slab + (int64_t)g * SLAB)[s4]
                                  : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
@@ -760,7 +855,20 @@ __global__ __launch_bounds__(256) void k_reduce_pre(const float* slab, int nslab
         }
     }
     if (!fin) return;
-    finish4(R, adam, c, st, p4, sv, L, grad, loss);
+    if (is_loss) {
+        if (loss) *loss = sv.x;
+        return;
+    }
+    if (grad) st4(grad + q * 4, sv, vec);
+    if (!adam) return;
+    const float4 n4 = make_float4(g2048::adam_update(c, sv.x, m4.x, v4.x, p4v.x),
+                                  g2048::adam_update(c, sv.y, m4.y, v4.y, p4v.y),
+                                  g2048::adam_update(c, sv.z, m4.z, v4.z, p4v.z),
+                                  g2048::adam_update(c, sv.w, m4.w, v4.w, p4v.w));
+    st4(R.m + q * 4, m4, vec);
+    st4(R.v + q * 4, v4, vec);
+    st4(R.p[k] + ei, n4, vec);
+    if (R.sync_every && st % R.sync_every == 0ull) st4(R.tp[k] + ei, n4, vec);
 }
 
 // Deterministic slab reduction (without `pre`: small batches, grid < SHADOW_MIN_GRID): a block
@@ -849,6 +957,16 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
                         float* workspace, float* grad_out, float* loss_out, uint64_t* step_dev,
                         const ReduceAdam& R, void* stream, const float* split = nullptr,
                         float* y_out = nullptr) {
+    ReduceAdam Rv = R;
+    {
+        auto a16 = [](const void* q) { return ((uintptr_t)q & 15u) == 0u; };
+        bool ok = a16(grad_out);
+        if (R.on) {
+            ok = ok && a16(R.m) && a16(R.v);
+            for (int k = 0; k < 8; ++k) ok = ok && a16(R.p[k]) && (!R.sync_every || a16(R.tp[k]));
+        }
+        Rv.vec = ok;
+    }
     TrainArgs A{};
     A.W = NetW{p->w1, p->b1, p->w2, p->b2, p->fc1_w, p->fc1_b, p->fc2_w, p->fc2_b};
     A.rows = rows;
@@ -874,10 +992,10 @@ static int train_launch(const g2048_convnet_params* p, const uint8_t* rows,
     if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_conv_train_bwd: %s", hipGetErrorString(e));
     if (A.pre)
         hipLaunchKernelGGL(k_reduce_pre, dim3(NB_PRE4 + C1_BLOCKS), dim3(256), 0, st, workspace,
-                           grid, A.pre, grad_out, loss_out, R);
+                           grid, A.pre, grad_out, loss_out, Rv);
     else
         hipLaunchKernelGGL(k_reduce_slabs, dim3((SL_LOSS / 4 + 64) / 64), dim3(64 * RW), 0, st,
-                           workspace, grid, grad_out, loss_out, R);
+                           workspace, grid, grad_out, loss_out, Rv);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "k_reduce_slabs: %s", hipGetErrorString(e));

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Build timing-only variants of the library (tools/variants/, never loaded by the product path):
+#   nophilox  -DG2048_TIMING_NO_PHILOX (Philox replaced by a 2-op mix: its share of k_step)
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p tools/variants
+F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wall -fvisibility=hidden -mllvm -amdgpu-kernarg-preload-count=16"
+C=reinforcement-learning-2048_amd/csrc
+SRCS="$C/g2048.hip $C/g2048_qnet.hip $C/g2048_qtrain.hip $C/g2048_adam.hip $C/g2048_mlp.hip $C/g2048_learn64.hip $C/g2048_conv64.hip $C/g2048_astar.hip $C/g2048_dense.hip"
+/opt/rocm/bin/hipcc $F -DG2048_TIMING_NO_PHILOX -o tools/variants/libg2048_nophilox.so $SRCS
