@@ -288,9 +288,6 @@ __device__ __forceinline__ uint32_t xor3_sk(uint32_t a, uint32_t b, uint32_t k) 
 // (seed, subsequence s, offset 4t) is philox10({t_lo, t_hi, s_lo, s_hi}, {seed_lo, seed_hi}).
 // The key (k0, k1) must be wave-uniform (it is the env / sampler seed everywhere).
 __device__ __forceinline__ uint4 philox10(uint4 c, uint32_t k0, uint32_t k1) {
-#ifdef G2048_TIMING_NO_PHILOX  // timing-only variant builds (tools/stepvariants.sh): a 2-op mix
-    return make_uint4(c.x ^ k0, c.y ^ k1, c.z + c.x, c.w ^ c.x);
-#endif
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         // one v_mad_u64_u32 per product instead of a v_mul_hi_u32 + v_mul_lo_u32 pair

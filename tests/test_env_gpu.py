@@ -188,6 +188,50 @@ def test_random_steps_with_replay_vs_oracle(g2048, n, flags):
     assert ref.ep[:, 0].sum() > 0  # some episodes finished and auto-reset
 
 
+def test_steps_across_clock_moves(g2048):
+    """Single random-policy steps interleaved with rollouts and eps-greedy steps on one env (the
+    three kernels share the group clock and the quad-based draws), and a state restored to an
+    earlier clock (a checkpoint resume), all against the oracle; a partial last group
+    (n % 64 != 0)."""
+    n, seed = 64 * 37 + 21, 0x5EED
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    ref = O.OracleEnv(n, seed=seed)
+    gen = np.random.default_rng(11)
+
+    def check(tag):
+        torch.cuda.synchronize()
+        assert np.array_equal(_np(env.board), ref.board), tag
+        assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta), tag
+        assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock), tag
+
+    def steps(k, tag):
+        for j in range(k):
+            r, d, lg = env.step(None)
+            o = ref.step(O.MODE_RANDOM)
+            assert np.array_equal(_np(r), o["reward"]), (tag, j)
+            assert np.array_equal(_np(d), o["done"]), (tag, j)
+            assert np.array_equal(_np(lg), o["legal"]), (tag, j)
+        check(tag)
+
+    steps(2, "a")
+    env.rollout(3)
+    for _ in range(3):
+        ref.step(O.MODE_RANDOM)
+    steps(5, "b")  # clock 5..9: across a quad boundary
+    q = gen.normal(size=(n, 4)).astype(np.float32)
+    env.step_egreedy(torch.from_numpy(q).to(DEV), 0.5)
+    ref.step(O.MODE_EGREEDY_F32, q=q, eps=0.5)
+    steps(6, "c")
+    saved = [t.clone() for t in (env.board, env.meta, env.ep, env.clock)]
+    ref_saved = [a.copy() for a in (ref.board, ref.meta, ref.ep, ref.clock)]
+    steps(7, "d")
+    for t, v in zip((env.board, env.meta, env.ep, env.clock), saved):
+        t.copy_(v)
+    ref.board[...], ref.meta[...], ref.ep[...], ref.clock[...] = ref_saved
+    steps(7, "e")
+    steps(9, "f")
+
+
 def test_actions_in_vs_oracle(g2048):
     n, seed = 3000, 99
     env = g2048.VecEnv2048(n, seed=seed, device=DEV)

@@ -13,7 +13,3 @@ python -c "
 import json;d=json.loads(open('gpurun_out/h_bench.json').read().strip().splitlines()[-1])
 for k,v in d['learner'].items(): print(k, round(v['update_ms'],4), 'ms', round(v['flop_frac'],4), v['path'], 'loop', round(v['loop_iter_ms'],3), round(v['loop_late_iter_ms'],3))"
 rm -rf /tmp/ph && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/ph -o h -- python bench.py --steps 5 --warmup 2 --step-steps 0 --rollout-k-extra "" --large-n "" --hbm-ring-launches 0 --train conv --no-cpu-baseline > gpurun_out/h_prof.log 2>&1 && cp $(find /tmp/ph -name '*kernel_stats.csv') gpurun_out/h_kernel_stats.csv && grep -E "reduce|train|targets" gpurun_out/h_kernel_stats.csv | cut -d, -f1-4
-# k_step: the in-tree library against the timing-only no-Philox variant (tools/stepvariants.sh)
-for L in "" tools/variants/libg2048_nophilox.so; do
-  timeout -k 10 120 python -u tools/blockbench.py $L || exit 1
-done
