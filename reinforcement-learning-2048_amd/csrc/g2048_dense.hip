@@ -216,6 +216,11 @@ struct FwdArgs {
     const double* eps_dev;
     double eps, eps_decay, eps_min;
     int64_t chunk;
+    // two nets in one launch (the update's Double-DQN target side): workgroups [0, nb1) run `net`
+    // into q, workgroups [nb1, 2 nb1) the same rows through net2 into q2 (nb1 = 0: one net)
+    DenseNet<T> net2;
+    T* q2;
+    int nb1;
 };
 
 template <typename T>
@@ -239,8 +244,11 @@ __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
     __shared__ int32_t qrow[TB];
     __shared__ int32_t wcnt[NW];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int64_t c0 = (int64_t)blockIdx.x * A.chunk;
+    const bool second = A.nb1 > 0 && (int)blockIdx.x >= A.nb1;  // workgroup-uniform
+    const int64_t c0 = (int64_t)(second ? (int)blockIdx.x - A.nb1 : (int)blockIdx.x) * A.chunk;
     const int64_t c1 = c0 + A.chunk < A.n ? c0 + A.chunk : A.n;
+    const DenseNet<T> net = second ? A.net2 : A.net;
+    T* const q = second ? A.q2 : A.q;
     int qn = 0;
     for (int64_t w0 = c0; w0 < c1; w0 += NT) {
         const bool last = w0 + NT >= c1;
@@ -274,7 +282,7 @@ __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
                 put_row(S.x + t * stride_of<T>(16), v);
                 qrow[t] = row;
             }
-            forward_tile<T, TB>(S, A.net, A.q, nb, qrow);
+            forward_tile<T, TB>(S, net, q, nb, qrow);
         }
         // carry the remainder (< TB rows) to the front of the queue
         const int rem = qn - nt * TB;
@@ -934,19 +942,35 @@ int update_launch(const g2048_densenet_params* on, const g2048_densenet_params* 
                   reinterpret_cast<const unsigned long long*>(step_dev), step_next,
                   (uint32_t)seed, (uint32_t)(seed >> 32)};
     hipLaunchKernelGGL(k_dense_sample, dim3((unsigned)((batch + 255) / 256)), dim3(256), 0, st, SA);
-    // the two target-side forwards on the sampled s' rows (the rollout forward kernel)
-    for (int k = 0; k < 2; ++k) {
+    // the target-side forwards on the sampled s' rows (the rollout forward kernel).  Double DQN:
+    // Q_online(s') and Q_target(s') in ONE launch, half the workgroups per net, each on
+    // tile_rows<T>() rows (64 in float32): every workgroup streams one net's weights through L2
+    // for twice the rows of the 32-row tiles two launches needed to fill the CUs, so the weight
+    // traffic per row halves.  Vanilla DQN: Q_target(s') alone, 32-row tiles over every CU.
+    {
         FwdArgs<T> F{};
-        F.net = net_of<T>(k == 0 ? on : tg);
         F.rows = reinterpret_cast<const uint4*>(s2);
         F.idx = idx_out;
         F.n = batch;
-        F.q = k == 0 ? q2on : q2tg;
-        const int64_t ft = (batch + TR - 1) / TR;
-        const int fg = (int)(ft < MAX_WG ? ft : MAX_WG);
-        F.chunk = (batch + fg - 1) / fg;
-        if (k == 0 && !double_dqn) continue;  // vanilla DQN: Q_target(s') alone
-        hipLaunchKernelGGL((k_dense_forward<T, TR>), dim3(fg), dim3(NT), 0, st, F);
+        if (double_dqn) {
+            constexpr int TBM = tile_rows<T>();
+            F.net = net_of<T>(on);
+            F.q = q2on;
+            F.net2 = net_of<T>(tg);
+            F.q2 = q2tg;
+            const int64_t ft = (batch + TBM - 1) / TBM;
+            const int g1 = (int)(ft < MAX_WG ? ft : MAX_WG);
+            F.chunk = (batch + g1 - 1) / g1;
+            F.nb1 = g1;
+            hipLaunchKernelGGL((k_dense_forward<T, TBM>), dim3(2 * g1), dim3(NT), 0, st, F);
+        } else {
+            F.net = net_of<T>(tg);
+            F.q = q2tg;
+            const int64_t ft = (batch + TR - 1) / TR;
+            const int fg = (int)(ft < MAX_WG ? ft : MAX_WG);
+            F.chunk = (batch + fg - 1) / fg;
+            hipLaunchKernelGGL((k_dense_forward<T, TR>), dim3(fg), dim3(NT), 0, st, F);
+        }
     }
     RowArgs<T> R{};
     R.net = net_of<T>(on);
