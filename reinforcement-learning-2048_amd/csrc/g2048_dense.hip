@@ -319,10 +319,11 @@ bool params_ok(const g2048_densenet_params* p) {
 
 // ================================================================== the update (train_step)
 // One Double-DQN update of the reference dense net (src/configs/double_dqn_dense.py:7-15, trained
-// by src/dqn_lib.py:119-164, + the target sync of :227-228) in float32 or float64, six launches:
+// by src/dqn_lib.py:119-164, + the target sync of :227-228) in float32 or float64, five launches:
 //   k_dense_sample   the minibatch rows (Philox, the fused learners' draw, or idx_in) + the next
 //                    update counter
-//   k_dense_forward  x2: Q_online(s'), Q_target(s') of the sampled rows (the rollout forward)
+//   k_dense_forward  Q_online(s') and Q_target(s') of the sampled rows in one launch (the rollout
+//                    forward, half the workgroups per net; vanilla DQN: Q_target(s') alone)
 //   k_dense_rows     per TR-row tile: y (Double / vanilla DQN), Q_online(s) with H1 / H2 stored,
 //                    MSE(sum) -> dq; dW4 / db4 (VALU); dZ3 = dq W4[a] relu'(h3) (stored);
 //                    dZ2 = (dZ3 W3) relu'(h2) (stored) and dZ1 = (dZ2 W2) relu'(h1) on MFMA --
