@@ -88,6 +88,28 @@ __device__ __forceinline__ double adam64(double t, double lr, double b1, double 
     return adam64_apply(adam64_coef(t, lr, b1, b2), b1, b2, eps, g, m, v, p);
 }
 
+// A workgroup's 16-byte slab store: the slab is read only by later launches on other CUs.
+// G2048_SLAB_AUX (build flag, default 0 = a plain global store) selects a buffer store with that
+// cache-policy word instead (gfx950: 1 sc0, 2 nt, 16 sc1) -- a measurement switch.
+#ifndef G2048_SLAB_AUX
+#define G2048_SLAB_AUX 0
+#endif
+typedef uint32_t slab_u32x4 __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ void slab_store16(V* base, int64_t elem, V v) {
+    static_assert(sizeof(V) == 16, "16-byte slab stores");
+#if G2048_SLAB_AUX == 0
+    base[elem] = v;
+#else
+    // base is the workgroup's slab (wave-uniform); a slab fits 2^31 bytes
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7FFFFFFF, 0x00020000);
+    slab_u32x4 u;
+    __builtin_memcpy(&u, &v, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u, rs, (uint32_t)(elem * 16), 0u, G2048_SLAB_AUX);
+#endif
+}
+
 // Fixed-order sum of the previous launch's per-workgroup gradient slabs, run in the shadow of
 // this launch's MFMA phases instead of in a reduction launch of its own.  Wave w of the block sums
 // the slabs w, w + 4, w + 8, ... (ascending) at one vector element per lane; loads go out NB at a

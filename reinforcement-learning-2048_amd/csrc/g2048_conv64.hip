@@ -1311,10 +1311,11 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                double2* dst = reinterpret_cast<double2*>(
-                    sl + P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4);
-                dst[0] = make_double2(gw2[cb][r], gw2[4 + cb][r]);
-                dst[1] = make_double2(gw2[8 + cb][r], gw2[12 + cb][r]);
+                const int64_t e = (P_W2 + (16 * w + 4 * r + lk) * 256 + (16 * cb + lr) * 4) / 2;
+                g2048::slab_store16(reinterpret_cast<double2*>(sl), e,
+                                    make_double2(gw2[cb][r], gw2[4 + cb][r]));
+                g2048::slab_store16(reinterpret_cast<double2*>(sl), e + 1,
+                                    make_double2(gw2[8 + cb][r], gw2[12 + cb][r]));
             }
     }
     if (A.pre) {  // whatever the tiles did not cover

@@ -411,9 +411,10 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
             float u[9];
 #pragma unroll
             for (int xi = 0; xi < 9; ++xi) u[xi] = aU[xi][mt][i];
-            *reinterpret_cast<float4*>(slab + SL_W2 + ((mt * 4 + i) * NT + t) * 4) =
+            g2048::slab_store16(
+                reinterpret_cast<float4*>(slab), SL_W2 / 4 + (mt * 4 + i) * NT + t,
                 make_float4((u[0] + u[1]) + (u[3] + u[4]), (u[1] + u[2]) + (u[4] + u[5]),
-                            (u[3] + u[4]) + (u[6] + u[7]), (u[4] + u[5]) + (u[7] + u[8]));
+                            (u[3] + u[4]) + (u[6] + u[7]), (u[4] + u[5]) + (u[7] + u[8])));
         }
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
