@@ -419,10 +419,8 @@ __global__ __launch_bounds__(NT) void k_conv_train_fwd(TrainArgs A) {
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                slab[SL_WF1 + ((jt * 16 + e * 4 + i) * NT) + t] = aF1[jt][e][i];
+        for (int e = 0; e < 4; ++e)  // the accumulator's four rows i as one 16-byte store
+            *reinterpret_cast<f32x4*>(slab + SL_WF1 + ((jt * 4 + e) * NT + t) * 4) = aF1[jt][e];
     float* red = lds + K1_V;
     red[t] = accB2;
     red[NT + t] = accLoss;
@@ -450,12 +448,12 @@ __device__ __forceinline__ int slab_to_param(int pos) {
         const int c = 16 * (r >> 2) + 4 * (lane >> 4) + (r & 3);
         return P_W2 + o * 256 + c * 4 + tap;
     }
-    if (pos < SL_SMALL) {  // (jt*16 + e*4 + i)*NT + t: j = 16jt + 4g + i, flat m = 4c' + q with
-                           // c' = 16e + l16, q = wave
-        const int p2 = pos - SL_WF1, t = p2 & (NT - 1), r = p2 >> 8;
+    if (pos < SL_SMALL) {  // ((jt*4 + e)*NT + t)*4 + i: j = 16jt + 4g + i, flat m = 4c' + q
+                           // with c' = 16e + l16, q = wave
+        const int p2 = pos - SL_WF1, i = p2 & 3, t = (p2 >> 2) & (NT - 1), je = p2 >> 10;
         const int lane = t & 63;
-        const int j = 16 * (r >> 4) + 4 * (lane >> 4) + (r & 3);
-        const int m = 4 * (16 * ((r >> 2) & 3) + (lane & 15)) + (t >> 6);
+        const int j = 16 * (je >> 2) + 4 * (lane >> 4) + i;
+        const int m = 4 * (16 * (je & 3) + (lane & 15)) + (t >> 6);
         return P_WF1 + j * 256 + m;
     }
     const int p3 = pos - SL_SMALL;  // w1 | b1 | b2 | bf1 | wf2 | bf2 in torch order
