@@ -97,6 +97,10 @@ typedef struct {
  * kernel needs a grid-wide barrier to advance it. */
 #define G2048_CLOCK_GROUP 64
 #define G2048_CLOCK_WORDS(n) (((n) + G2048_CLOCK_GROUP - 1) / G2048_CLOCK_GROUP)
+/* Largest env: 2^31 - 256 boards (80 GB of board / meta / episode state).  A dispatch's grid is
+ * at most 2^32 - 1 work-items per dimension, and the dense-64 fused step gives a board two
+ * threads (the warp-specialised rollout does too, but its < 4 GiB ring window caps it lower). */
+#define G2048_MAX_BOARDS ((int64_t)2147483392)
 
 /* Replaces `Board2048()` x n_boards (src/board.py:10-20): allocates and resets n boards. */
 G2048_API int g2048_env_create(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,

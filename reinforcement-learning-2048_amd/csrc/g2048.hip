@@ -1317,8 +1317,9 @@ int g2048_env_wrap(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_off
                    uint32_t flags, uint8_t* board, uint32_t* meta, uint32_t* ep, uint64_t* clock,
                    int reset, void* stream) {
     if (!out || n <= 0) return fail(G2048_EINVAL, "env_wrap: need out != NULL and n > 0");
-    if (n > ((int64_t)1 << 32) - G2048_CLOCK_GROUP)
-        return fail(G2048_EINVAL, "env_wrap: n = %lld boards exceeds 2^32 - 64", (long long)n);
+    if (n > G2048_MAX_BOARDS)
+        return fail(G2048_EINVAL, "env_wrap: n = %lld boards exceeds G2048_MAX_BOARDS (%lld)",
+                    (long long)n, (long long)G2048_MAX_BOARDS);
     if (!board || !meta || !ep || !clock || !aligned16(board) || !aligned16(ep) ||
         ((uintptr_t)meta & 7u) || ((uintptr_t)clock & 7u))
         return fail(G2048_EINVAL, "env_wrap: board/meta/ep/clock must be non-NULL, board/ep "
@@ -1361,9 +1362,10 @@ int g2048_env_wrap(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_off
 int g2048_env_create(g2048_env** out, int64_t n, uint64_t seed, uint64_t board_offset,
                      int device_id, uint32_t flags, void* stream) {
     if (!out || n <= 0) return fail(G2048_EINVAL, "env_create: need out != NULL and n > 0");
+    if (n > G2048_MAX_BOARDS)
+        return fail(G2048_EINVAL, "env_create: n = %lld boards exceeds G2048_MAX_BOARDS (%lld)",
+                    (long long)n, (long long)G2048_MAX_BOARDS);
     DeviceGuard g(device_id);
-    if (n > ((int64_t)1 << 32) - G2048_CLOCK_GROUP)
-        return fail(G2048_EINVAL, "env_create: n = %lld boards exceeds 2^32 - 64", (long long)n);
     uint8_t* board = nullptr;
     uint32_t *meta = nullptr, *ep = nullptr;
     uint64_t* clock = nullptr;

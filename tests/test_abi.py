@@ -87,3 +87,21 @@ def test_entry_points_reject_bad_arguments():
     rc = lib.g2048_convnet_targets(None, None, None, None, 0, 0, None, 0.8, 1, None, None, None)
     assert rc == N.G2048_EINVAL
     assert lib.g2048_convnet_train_workspace(0) == 0
+
+
+def test_env_size_limit_refused_before_any_hip_call():
+    """n > G2048_MAX_BOARDS (2^31 - 256: a grid stays below 2^32 work-items even where a board
+    has two threads) is refused with G2048_EINVAL before the library touches a device, so this
+    runs on the CPU."""
+    import ctypes as C
+
+    from g2048 import _native as N
+
+    hdr = open(os.path.join(ROOT, "include", "g2048.h")).read()
+    m = re.search(r"#define G2048_MAX_BOARDS \(\(int64_t\)(\d+)\)", hdr)
+    assert m and int(m.group(1)) == (1 << 31) - 256
+    lib = N.load()
+    out = C.c_void_p()
+    rc = lib.g2048_env_create(C.byref(out), (1 << 31) - 255, 1, 0, 0, 0, None)
+    assert rc == -1 and not out.value  # G2048_EINVAL
+    assert b"G2048_MAX_BOARDS" in lib.g2048_last_error()

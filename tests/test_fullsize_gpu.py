@@ -210,3 +210,47 @@ def test_random_step_spawn_uniform(g2048, p4):
     frac4 = (vals == 2).mean()
     assert set(np.unique(vals)) <= {1, 2}
     assert abs(frac4 - p4) < 5 * np.sqrt(p4 * (1 - p4) / len(vals)), frac4
+
+
+def test_max_boards_vs_oracle(g2048):
+    """The ABI's largest env (include/g2048.h: G2048_MAX_BOARDS = 2^31 - 256 boards; 80 GB of
+    board / meta / episode state plus 12 GB of step outputs in HBM): three single steps with
+    every output and a 3-step rollout (the general kernel, no ring), against the oracle on three
+    1 000-board slices -- the first
+    boards, the middle and the last, whose global ids pass 2^30 and byte offsets 2^34.  Every
+    index is 64-bit; this is where a 32-bit one would show.  (A 2^32 - 64 limit, the ABI's
+    before this test, failed at the first launch: a grid of 2^32 work-items.)"""
+    torch.cuda.empty_cache()
+    n_all, seed = 2147483392, 0x5151
+    env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
+    reward = torch.empty(n_all, dtype=torch.int32, device=DEV)
+    done = torch.empty(n_all, dtype=torch.uint8, device=DEV)
+    legal = torch.empty(n_all, dtype=torch.uint8, device=DEV)
+    n = 1000
+    slices = (0, (1 << 30) - 500, n_all - n)
+    refs = {i0: O.OracleEnv(n, seed=seed, board_offset=i0) for i0 in slices}
+    for i0, ref in refs.items():
+        assert np.array_equal(_np(env.board[i0:i0 + n]), ref.board), i0
+    for step in range(3):
+        env.step(None, reward=reward, done=done, legal=legal)
+        torch.cuda.synchronize()
+        for i0, ref in refs.items():
+            o = ref.step(O.MODE_RANDOM)
+            sl = slice(i0, i0 + n)
+            assert np.array_equal(_np(reward[sl]), o["reward"]), (step, i0)
+            assert np.array_equal(_np(done[sl]), o["done"]), (step, i0)
+            assert np.array_equal(_np(legal[sl]), o["legal"]), (step, i0)
+    env.rollout(3)
+    torch.cuda.synchronize()
+    for i0, ref in refs.items():
+        for _ in range(3):
+            ref.step(O.MODE_RANDOM)
+        sl = slice(i0, i0 + n)
+        assert np.array_equal(_np(env.board[sl]), ref.board), i0
+        assert np.array_equal(_np(env.meta[sl]).view(np.uint32), ref.meta), i0
+        assert np.array_equal(_np(env.ep[sl]).view(np.uint32), ref.ep), i0
+    clock = env.clock[-1:]
+    assert int(clock) == 6
+    env.check_errors()
+    del env, reward, done, legal
+    torch.cuda.empty_cache()
