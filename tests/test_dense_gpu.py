@@ -192,7 +192,7 @@ def test_dense_ref_fused_matches_reference(G, golden_dir, name):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-9), (torch.float32, 2e-4)])
 @pytest.mark.parametrize("double_dqn", [True, False])
-@pytest.mark.parametrize("batch", [1, 33, 700, 5000, 8192])
+@pytest.mark.parametrize("batch", [1, 33, 700, 5000, 8192, 20000])
 def test_dense_ref_fused_equals_autograd(G, batch, double_dqn, dtype, tol):
     """Three fused updates of the reference dense net (Philox rows, Adam, target sync every 2)
     against torch autograd through dqn_lib.dqn_loss on the same rows and the same pre-update

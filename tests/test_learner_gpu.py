@@ -236,7 +236,7 @@ def test_fused_f64_matches_reference(G, golden_dir, net):
     np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
 
 
-@pytest.mark.parametrize("batch", [1, 33, 1000, 3000, 4096])
+@pytest.mark.parametrize("batch", [1, 33, 1000, 3000, 4096, 20000])
 @pytest.mark.parametrize("double_dqn", [True, False])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
 def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
@@ -246,7 +246,8 @@ def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
     (|g| ~ eps) moves by a step that depends on g's last bits -- the two paths sum the rows in
     different orders).  B = 1 / 33: ragged single tiles (one and three workgroups).  B = 4096
     puts the conv update on 256 workgroups, where train B sums train A's slab terms itself
-    (SlabShadow) and the reduce reads them summed."""
+    (SlabShadow) and the reduce reads them summed; B = 20 000: 1 250 conv tiles over the 256
+    workgroups, four or five each (the tile loop and its next-tile prefetch past two)."""
     from g2048.learner import DQNLearner
 
     n = 2048
