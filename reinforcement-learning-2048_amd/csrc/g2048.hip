@@ -110,11 +110,17 @@ __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v
 // The step counter of board i's 64-board group as a wave-uniform (SGPR) value.  Every lane of the
 // wave loads the same word; the wave's first lane is always live (groups start at 64-aligned
 // board indices and a wave never straddles two groups).
-__device__ __forceinline__ uint64_t load_clock(const uint64_t* clock, int64_t i) {
-    const uint64_t c = clock[i >> 6];
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)c);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
+// A 64-bit value as the wave's first lane holds it, in SGPRs.  readfirstlane returns an int: each
+// half goes through uint32_t before widening, or a low word >= 2^31 would sign-extend into the
+// high word (the rollout kernels' clocks past 2^31 steps were wrong that way until round 5).
+__device__ __forceinline__ uint64_t first_lane_u64(uint64_t c) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)c);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
     return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ uint64_t load_clock(const uint64_t* clock, int64_t i) {
+    return first_lane_u64(clock[i >> 6]);
 }
 
 // k_step's form: the group index is wave-uniform by construction (a wave never straddles two
@@ -702,8 +708,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
                                      &kDirNet[0][0][0])[(threadIdx.x >> 2) * 2u + (threadIdx.x & 1u)];
     __syncthreads();
     if (!live) return;
-    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    const uint64_t t0 = first_lane_u64(c0);
     Board b = load_board(bv);
     const uint64_t gid = A.board_offset + (uint64_t)i;
     const uint32_t p4 = A.p4_thresh;
@@ -1076,8 +1081,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
         prod[threadIdx.x] = 0u;
         cons[threadIdx.x] = 0u;
     }
-    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    const uint64_t t0 = first_lane_u64(c0);
     const int K = A.k_steps > 0 ? A.k_steps : 0;
     __syncthreads();
     if (storer) {

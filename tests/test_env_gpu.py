@@ -774,3 +774,34 @@ def test_fused_dense64_step_f64(g2048):
     for name in ("s", "s2", "a", "r", "d", "count"):
         assert torch.equal(getattr(rbs[0], name), getattr(rbs[1], name)), name
     assert torch.equal(logs[0].qsum, logs[1].qsum)
+
+
+@pytest.mark.parametrize("rows", [6, 8])
+def test_clock_past_2_32_vs_oracle(g2048, rows):
+    """Step clocks crossing 2^32 (the ring row switches to its 64-bit modulo, the Philox counter
+    to its high word): single steps and rollouts -- rows % 4 == 0 takes the lean kernel's quad-row
+    path, 6 the other -- with a ring of `rows` rows per board, against the oracle on every
+    output, ring row and clock; a partial last clock group."""
+    n, seed = 64 * 20 + 37, 0xC10C
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    rb = g2048.ReplayBuffer(rows * n, device=DEV)
+    ref = O.OracleEnv(n, seed=seed)
+    ref_rb = O.OracleReplay(rows * n)
+    t0 = (1 << 32) - 5
+    env.clock.fill_(t0)
+    ref.clock[:] = t0
+    for step in range(4):
+        r, d, lg = env.step(None, replay=rb)
+        o = ref.step(O.MODE_RANDOM, replay=ref_rb)
+        assert np.array_equal(_np(r), o["reward"]), step
+        assert np.array_equal(_np(lg), o["legal"]), step
+    env.rollout(7, replay=rb)
+    for _ in range(7):
+        ref.step(O.MODE_RANDOM, replay=ref_rb)
+    torch.cuda.synchronize()
+    assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
+    assert int(ref.clock[0]) == t0 + 11 and t0 + 11 > (1 << 32)
+    assert np.array_equal(_np(env.board), ref.board)
+    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    for name in ["s", "s2", "a", "r", "d"]:
+        assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name

@@ -90,8 +90,8 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws_barrier(StepArgs A) {
     uint64_t c0 = 0;
     if (live) c0 = A.clock[i >> 6];
     if (threadIdx.x < 8) s_dir[threadIdx.x] = reinterpret_cast<const uint4*>(&kDirNet[0][0][0])[threadIdx.x];
-    const uint64_t t0 = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
+    const uint64_t t0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)c0) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32);
     const int K = A.k_steps > 0 ? A.k_steps : 0;
     __syncthreads();
     if (storer) {
