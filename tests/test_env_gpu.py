@@ -776,13 +776,14 @@ def test_fused_dense64_step_f64(g2048):
     assert torch.equal(logs[0].qsum, logs[1].qsum)
 
 
-@pytest.mark.parametrize("rows", [6, 8])
-def test_clock_past_2_32_vs_oracle(g2048, rows):
+@pytest.mark.parametrize("n,rows", [(64 * 20 + 37, 6), (64 * 20 + 37, 8), ((1 << 18) + 64, 8)])
+def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     """Step clocks crossing 2^32 (the ring row switches to its 64-bit modulo, the Philox counter
     to its high word): single steps and rollouts -- rows % 4 == 0 takes the lean kernel's quad-row
-    path, 6 the other -- with a ring of `rows` rows per board, against the oracle on every
-    output, ring row and clock; a partial last clock group."""
-    n, seed = 64 * 20 + 37, 0xC10C
+    path, 6 the other, and from 2^18 boards the warp-specialised kernel runs -- with a ring of
+    `rows` rows per board, against the oracle on every output, ring row and clock; a partial last
+    clock group."""
+    seed = 0xC10C
     env = g2048.VecEnv2048(n, seed=seed, device=DEV)
     rb = g2048.ReplayBuffer(rows * n, device=DEV)
     ref = O.OracleEnv(n, seed=seed)
