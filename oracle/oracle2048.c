@@ -359,8 +359,8 @@ int64_t o2048_env_step(o2048_env* e, int mode, const uint8_t* actions, const voi
             rb->a[slot] = (uint8_t)a;
             rb->r[slot] = r;
             rb->d[slot] = (uint8_t)done;
-            uint64_t c = (t + 1) * (uint64_t)e->n;
-            if (c > (uint64_t)rb->capacity) c = (uint64_t)rb->capacity;
+            /* min((t + 1) n, capacity), the product never overflowing */
+            const uint64_t c = t + 1 >= (uint64_t)rows ? (uint64_t)rb->capacity : (t + 1) * (uint64_t)e->n;
             if (c > *rb->count) *rb->count = c;
         }
         if (reward) reward[i] = r;

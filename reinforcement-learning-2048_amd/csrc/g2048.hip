@@ -276,9 +276,10 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
     act_out = act;
 }
 
+// count = min(t_next * n, capacity), without the product overflowing at any clock
 __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
-    uint64_t c = t_next * (uint64_t)A.n;
-    if (c > (uint64_t)A.rb.capacity) c = (uint64_t)A.rb.capacity;
+    const uint64_t c = t_next >= (uint64_t)A.rb.rows ? (uint64_t)A.rb.capacity
+                                                     : t_next * (uint64_t)A.n;
     atomicMax(A.rb.count, (unsigned long long)c);
 }
 

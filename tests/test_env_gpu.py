@@ -802,6 +802,7 @@ def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     torch.cuda.synchronize()
     assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
     assert int(ref.clock[0]) == t0 + 11 and t0 + 11 > (1 << 32)
+    assert int(_np(rb.count)[0]) == int(ref_rb.count[0]) == rows * n
     assert np.array_equal(_np(env.board), ref.board)
     assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
     for name in ["s", "s2", "a", "r", "d"]:
