@@ -161,7 +161,7 @@ def test_trajectories_injected(g2048, golden_dir):
 
 
 # ------------------------------------------------------------------ RNG modes vs oracle
-@pytest.mark.parametrize("n,flags", [(4000, 0), (4096, O.P4_10), (777, 0)])
+@pytest.mark.parametrize("n,flags", [(4000, 0), (4096, O.P4_10), (777, 0), (1, 0), (63, O.P4_10)])
 def test_random_steps_with_replay_vs_oracle(g2048, n, flags):
     seed = 0xC0FFEE + n
     kw = dict(p4=0.1 if flags & O.P4_10 else 0.5)
@@ -185,7 +185,8 @@ def test_random_steps_with_replay_vs_oracle(g2048, n, flags):
     for name in ["s", "s2", "a", "r", "d"]:
         assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
     assert int(_np(rb.count)[0]) == int(ref_rb.count[0]) == 3 * n
-    assert ref.ep[:, 0].sum() > 0  # some episodes finished and auto-reset
+    if n >= 64:
+        assert ref.ep[:, 0].sum() > 0  # some episodes finished and auto-reset
 
 
 def test_steps_across_clock_moves(g2048):
@@ -307,7 +308,7 @@ def test_egreedy_nonfinite_golden_rows(g2048, golden_dir):
         assert np.array_equal(qs[live], g["qmax" + suf][live], equal_nan=True)
 
 
-@pytest.mark.parametrize("n,p4", [(2048, 0.5), (2048 + 77, 0.1)])
+@pytest.mark.parametrize("n,p4", [(2048, 0.5), (2048 + 77, 0.1), (1, 0.5), (65, 0.5)])
 def test_rollout_equals_single_steps(g2048, n, p4):
     """K random steps in one launch == K single steps: odd and even starting clocks (the pair
     block is split across launches), odd and even K, a partial last workgroup, both p4 modes,
@@ -334,7 +335,8 @@ def test_rollout_equals_single_steps(g2048, n, p4):
     for name in ["s", "s2", "a", "r", "d", "count"]:
         assert torch.equal(getattr(r1, name), getattr(r2, name)), name
     g1, g2 = l1.read(), l2.read()
-    assert g1["step"].numel() > 0
+    if n >= 64:
+        assert g1["step"].numel() > 0
     for f in g1:
         assert torch.equal(g1[f], g2[f]), f
     assert torch.equal(l1.qsum, l2.qsum)
