@@ -801,9 +801,13 @@ def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     env.rollout(7, replay=rb)
     for _ in range(7):
         ref.step(O.MODE_RANDOM, replay=ref_rb)
+    q = np.random.default_rng(n).normal(size=(n, 4)).astype(np.float32)
+    a, r, d = env.step_egreedy(torch.from_numpy(q).to(DEV), 0.5, replay=rb)  # DOMAIN_STEP draws
+    o = ref.step(O.MODE_EGREEDY_F32, q=q, eps=0.5, replay=ref_rb)
+    assert np.array_equal(_np(a), o["action"]) and np.array_equal(_np(r), o["reward"])
     torch.cuda.synchronize()
     assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
-    assert int(ref.clock[0]) == t0 + 11 and t0 + 11 > (1 << 32)
+    assert int(ref.clock[0]) == t0 + 12 and t0 + 12 > (1 << 32)
     assert int(_np(rb.count)[0]) == int(ref_rb.count[0]) == rows * n
     assert np.array_equal(_np(env.board), ref.board)
     assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
