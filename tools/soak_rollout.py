@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Soak: many back-to-back rollout launches at a store-bound size (the warp-specialised kernel at
+4M boards, the lean one at 64k), then the boards, counters and the ring rows of the last launches
+checked against the oracle on three 1 000-board slices (Philox keyed by global board id, so a
+slice is exact).  Meant to catch rare store hazards under sustained back-pressure."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "reinforcement-learning-2048_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import g2048  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+def soak(n_all, k, launches, seed):
+    env = g2048.VecEnv2048(n_all, seed=seed, device="cuda:0")
+    rb = g2048.ReplayBuffer(n_all * k * 2, device="cuda:0")
+    t0 = time.perf_counter()
+    for _ in range(launches):
+        env.rollout(k, replay=rb)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    env.check_errors()
+    steps = k * launches
+    rows = 2 * k
+    bad = 0
+    for i0 in (0, n_all // 2 - 500, n_all - 1000):
+        n = 1000
+        ref = O.OracleEnv(n, seed=seed, board_offset=i0)
+        ref_rb = O.OracleReplay(n * rows)
+        for _ in range(steps):
+            ref.step(O.MODE_RANDOM, replay=ref_rb)
+        sl = slice(i0, i0 + n)
+        ok = (np.array_equal(env.board[sl].cpu().numpy(), ref.board) and
+              np.array_equal(env.meta[sl].cpu().numpy().view(np.uint32), ref.meta) and
+              np.array_equal(env.ep[sl].cpu().numpy().view(np.uint32), ref.ep))
+        # ring rows (row r of board i at r * n_all + i) vs the slice ring (r * n + (i - i0))
+        ridx = (np.arange(rows)[:, None] * n_all + np.arange(i0, i0 + n)[None, :]).reshape(-1)
+        ridx_t = torch.from_numpy(ridx).to("cuda:0")
+        for name in ("s", "s2", "a", "r", "d"):
+            got = getattr(rb, name).index_select(0, ridx_t).cpu().numpy()
+            ok = ok and np.array_equal(got, getattr(ref_rb, name))
+        bad += 0 if ok else 1
+        print(f"  slice {i0}: {'ok' if ok else 'MISMATCH'}", flush=True)
+    print(f"{n_all} boards x {steps} steps ({launches} launches of {k}): "
+          f"{n_all * steps / dt / 1e9:.1f} G env steps/s wall, slices bad: {bad}", flush=True)
+    del env, rb
+    torch.cuda.empty_cache()
+    return bad
+
+
+if __name__ == "__main__":
+    bad = soak(1 << 22, 16, 64, 11) + soak(1 << 16, 64, 512, 12)
+    sys.exit(1 if bad else 0)
