@@ -1,0 +1,4 @@
+#!/bin/bash
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -u tools/soak_learner.py
