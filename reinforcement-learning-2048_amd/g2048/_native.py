@@ -19,6 +19,7 @@ P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
 ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
 ABI_VERSION = 4  # include/g2048.h G2048_ABI_VERSION
+MAX_BOARDS = (1 << 31) - 256  # include/g2048.h G2048_MAX_BOARDS
 REPLAY_SECTION_PAD = 4352  # include/g2048.h G2048_REPLAY_SECTION_PAD
 
 # every symbol include/g2048.h declares, with (restype, argtypes)

@@ -101,6 +101,8 @@ class VecEnv2048:
             raise ValueError("p4 must be 0.5 (reference, src/board.py:12) or 0.1")
         if egreedy not in ("compat", "fixed"):
             raise ValueError("egreedy must be 'compat' (src/dqn_lib.py:25-29) or 'fixed'")
+        if not 0 < int(n_boards) <= N.MAX_BOARDS:
+            raise ValueError(f"n_boards must be in [1, {N.MAX_BOARDS}] (G2048_MAX_BOARDS)")
         self.device = N.require_gpu(device)
         self.n = int(n_boards)
         self.seed = int(seed)

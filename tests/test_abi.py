@@ -99,9 +99,18 @@ def test_env_size_limit_refused_before_any_hip_call():
 
     hdr = open(os.path.join(ROOT, "include", "g2048.h")).read()
     m = re.search(r"#define G2048_MAX_BOARDS \(\(int64_t\)(\d+)\)", hdr)
-    assert m and int(m.group(1)) == (1 << 31) - 256
+    assert m and int(m.group(1)) == (1 << 31) - 256 == N.MAX_BOARDS
     lib = N.load()
     out = C.c_void_p()
     rc = lib.g2048_env_create(C.byref(out), (1 << 31) - 255, 1, 0, 0, 0, None)
     assert rc == -1 and not out.value  # G2048_EINVAL
     assert b"G2048_MAX_BOARDS" in lib.g2048_last_error()
+
+
+def test_vecenv_refuses_oversized_env_before_allocating():
+    """VecEnv2048 checks n against G2048_MAX_BOARDS before it allocates or needs a GPU."""
+    import g2048
+
+    for n in (0, (1 << 31) - 255):
+        with pytest.raises(ValueError, match="G2048_MAX_BOARDS"):
+            g2048.VecEnv2048(n, device="cuda:0")
