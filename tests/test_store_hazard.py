@@ -36,12 +36,13 @@ def audited_sources():
 
 
 def audit_cmd(src: str, out: str) -> list:
-    """The library's own hipcc flags (__graft_entry__.HIPFLAGS: kernarg preloading changes the
-    kernels' prologues, register allocation and scheduling), minus the link-only ones, plus
+    """The library's own hipcc flags for this source (__graft_entry__.src_flags: HIPFLAGS --
+    kernarg preloading changes the kernels' prologues, register allocation and scheduling -- and
+    the source's own, e.g. g2048.hip's machine scheduler), minus the link-only ones, plus
     device-only assembly output: the audit reads the code that ships."""
     sys.path.insert(0, ROOT)
     import __graft_entry__ as G
-    flags = [f for f in G.HIPFLAGS if f not in ("-shared", "-fPIC")]
+    flags = [f for f in G.src_flags(src) if f not in ("-shared", "-fPIC")]
     return [G.HIPCC, *flags, "--cuda-device-only", "-S", src, "-o", out]
 
 
@@ -56,6 +57,9 @@ def test_audit_uses_library_flags():
             assert f in cmd
     assert "-amdgpu-kernarg-preload-count=16" in cmd
     assert set(audited_sources()) == set(G.SRCS)
+    for src, extra in G.SRC_FLAGS.items():  # a source's own flags reach its audit too
+        cmd = audit_cmd(os.path.join(CSRC, src), "x.s")
+        assert all(f in cmd for f in extra), src
 
 
 def test_audit_sees_loads_and_branches(tmp_path):
