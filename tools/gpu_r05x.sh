@@ -1,0 +1,13 @@
+#!/bin/bash
+# GPU box: one source's machine-scheduler strategy changed at a time (tools/sched_file_variants.py)
+mkdir -p gpurun_out
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 240 python -u tools/learner_ab.py "" conv,dense64 || exit 1
+for L in tools/variants/libg2048_g2048_qnet_*.so tools/variants/libg2048_g2048_qtrain_*.so tools/variants/libg2048_g2048_conv64_*.so; do
+  timeout -k 10 240 python -u tools/learner_ab.py "$L" conv || exit 1
+done
+for L in tools/variants/libg2048_g2048_mlp_*.so tools/variants/libg2048_g2048_learn64_*.so; do
+  timeout -k 10 240 python -u tools/learner_ab.py "$L" dense64 || exit 1
+done
+timeout -k 10 240 python -u tools/learner_ab.py "" conv,dense64 || exit 1
