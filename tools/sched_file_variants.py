@@ -22,11 +22,14 @@ srcs, strategies = sys.argv[1].split(","), sys.argv[2].split(",")
 def one(pair):
     src, st = pair
     path = os.path.join(G.CSRC, src)
-    flags = [f for f in G.HIPFLAGS if f != "-shared"] + ["-mllvm", f"--amdgpu-sched-strategy={st}"]
-    obj = os.path.join(out, f"{src}.{st}.o")
+    # a strategy name, or "opt:<llvm option>" for any other -mllvm scheduling option
+    knob = st[4:] if st.startswith("opt:") else f"--amdgpu-sched-strategy={st}"
+    flags = [f for f in G.HIPFLAGS if f != "-shared"] + ["-mllvm", knob]
+    obj = os.path.join(out, f"{src}.{st.replace('opt:', '').replace('=', '').replace('-', '')}.o")
     subprocess.run([G.HIPCC, *flags, "-c", path, "-o", obj], check=True)
     objs = [obj if f == src else os.path.join(objdir, f + ".o") for f in G.SRCS]
-    lib = os.path.join(out, f"libg2048_{src.replace('.hip', '')}_{st}.so")
+    tag = st.replace("opt:", "").replace("=", "").replace("-", "")
+    lib = os.path.join(out, f"libg2048_{src.replace('.hip', '')}_{tag}.so")
     link = [f for f in G.HIPFLAGS if f in ("--offload-arch=gfx950", "-shared", "-fPIC")]
     subprocess.run([G.HIPCC, *link, "-o", lib, *objs], check=True)
     return lib
