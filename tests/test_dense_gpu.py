@@ -192,13 +192,14 @@ def test_dense_ref_fused_matches_reference(G, golden_dir, name):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-9), (torch.float32, 2e-4)])
 @pytest.mark.parametrize("double_dqn", [True, False])
-@pytest.mark.parametrize("batch", [1, 33, 700, 5000, 8192, 20000])
+@pytest.mark.parametrize("batch", [1, 33, 700, 5000, 8192, 20000, 65536])
 def test_dense_ref_fused_equals_autograd(G, batch, double_dqn, dtype, tol):
     """Three fused updates of the reference dense net (Philox rows, Adam, target sync every 2)
     against torch autograd through dqn_lib.dqn_loss on the same rows and the same pre-update
     weights: loss and every parameter tensor's gradient to `tol` relative (float64 1e-9; float32
     2e-4 -- fp32 sums over B rows in another order); B = 1 and 33 are ragged single / double
-    tiles (the weight-gradient splits then hold 0-16 rows), B = 700 leaves a ragged last tile."""
+    tiles (the weight-gradient splits then hold 0-16 rows), B = 700 leaves a ragged last tile,
+    B = 65 536 is eight times the bench's batch."""
     import copy
 
     from g2048 import dqn_lib

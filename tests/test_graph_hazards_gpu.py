@@ -168,7 +168,7 @@ def _carve_net(arena, base, model, dt):
     return base + len(list(model.parameters()))
 
 
-@pytest.mark.parametrize("batch", [700, 3000, 4096, 8192])
+@pytest.mark.parametrize("batch", [700, 3000, 4096, 8192, 65536])
 @pytest.mark.parametrize("path", ["conv64", "conv32", "dense64_64", "dense64_32", "dense_64",
                                   "dense_32"])
 def test_fused_learners_stay_in_bounds(G, path, batch):

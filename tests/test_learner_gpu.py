@@ -236,7 +236,7 @@ def test_fused_f64_matches_reference(G, golden_dir, net):
     np.testing.assert_allclose(after, g["params_after"], rtol=1e-10, atol=1e-10)
 
 
-@pytest.mark.parametrize("batch", [1, 33, 1000, 3000, 4096, 20000])
+@pytest.mark.parametrize("batch", [1, 33, 1000, 3000, 4096, 20000, 65536])
 @pytest.mark.parametrize("double_dqn", [True, False])
 @pytest.mark.parametrize("net", ["dense64", "conv"])
 def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
@@ -247,7 +247,8 @@ def test_fused_f64_equals_torch_path(G, net, double_dqn, batch):
     different orders).  B = 1 / 33: ragged single tiles (one and three workgroups).  B = 4096
     puts the conv update on 256 workgroups, where train B sums train A's slab terms itself
     (SlabShadow) and the reduce reads them summed; B = 20 000: 1 250 conv tiles over the 256
-    workgroups, four or five each (the tile loop and its next-tile prefetch past two)."""
+    workgroups, four or five each (the tile loop and its next-tile prefetch past two); B = 65 536:
+    eight times the bench's batch (4 096 conv tiles, 16 per workgroup)."""
     from g2048.learner import DQNLearner
 
     n = 2048

@@ -74,11 +74,12 @@ def test_fused_learner_matches_unfused(G):
     torch.testing.assert_close(res[0][1], res[1][1], rtol=1e-3, atol=1e-3 * float(res[1][1].abs().max()))
 
 
-@pytest.mark.parametrize("B", [1, 17, 32, 1000, 3000, 9000, 20000])
+@pytest.mark.parametrize("B", [1, 17, 32, 1000, 3000, 9000, 20000, 65536])
 def test_conv_train_grad_matches_autograd(G, B):
     """Fused graded half of train_step vs torch autograd in float64 on the same minibatch.
     B = 1 / 17: one ragged tile on one workgroup; B = 1000: 63 workgroups, the reduce sums every slab term; 3000: 188 (train bwd sums train
-    fwd's terms, k_reduce_pre over a partial round of slabs); 20000: 313 (two rounds)."""
+    fwd's terms, k_reduce_pre over a partial round of slabs); 20000: 313 (two rounds); 65536: eight
+    times the bench's batch."""
     from g2048.nets import make_net
     from g2048.qnet import ConvTrainGrad
 
