@@ -61,14 +61,14 @@ def test_bench_rollout_full_size_vs_oracle(g2048):
         assert ref.ep[:, 0].sum() > 0  # episodes ended and auto-reset inside the launch
 
 
-@pytest.mark.parametrize("n_all", [(1 << 18) - 64, (1 << 20) + 4160])
+@pytest.mark.parametrize("n_all", [(1 << 18) - 64, (1 << 18) + 37, (1 << 20) + 4160])
 def test_rollout_large_n_vs_oracle(g2048, n_all):
     """256k / 1 M boards, ring of N*16 rows, one launch of 3 steps and four of 16 -- every clock
     phase -- against the oracle on four 1 000-board slices.  Just below 256k boards
     k_rollout_lean runs (its quad-row path; its first version, under store-queue back-pressure,
     stored some boards with the first word already rewritten by the next instruction: store_board
     in g2048.hip).  From 256k boards on (the second case, ragged: a partly live last workgroup)
-    the warp-specialised k_rollout_ws runs."""
+    the warp-specialised k_rollout_ws runs; 2^18 + 37: its last wave holds 37 live boards."""
     k, seed = 16, 7
     env = g2048.VecEnv2048(n_all, seed=seed, device=DEV)
     rb = g2048.ReplayBuffer(n_all * k, device=DEV)
