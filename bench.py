@@ -24,6 +24,7 @@ import json
 import os
 import sys
 import time
+import traceback
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 for _p in (ROOT, os.path.join(ROOT, "reinforcement-learning-2048_amd")):
@@ -494,11 +495,26 @@ def main():
         torch.cuda.empty_cache()
     step = bench_step(args, world, rank, dev) if args.step_steps > 0 else None
     train = {}
+    failed = False
     for leg in [x for x in args.train.split(",") if x]:
         net, _, b = leg.partition("@")  # "dense@5000": that net at that batch
         for dt in [x for x in args.train_dtypes.split(",") if x]:
-            train[f"{leg}.{dt}"] = bench_train(args, world, rank, dev, net, dt,
-                                               int(b) if b else args.batch)
+            if failed:
+                train[f"{leg}.{dt}"] = {"error": "skipped after an earlier learner leg failed"}
+                continue
+            try:
+                train[f"{leg}.{dt}"] = bench_train(args, world, rank, dev, net, dt,
+                                                   int(b) if b else args.batch)
+            except Exception as e:
+                # one rank per GPU (world > 1): the learner legs are the only ones that capture
+                # RCCL collectives; a failure there is reported in the line and the remaining
+                # learner legs are skipped, so the env-step headline measured above still
+                # prints.  One process (world == 1) fails loudly.
+                if world == 1:
+                    raise
+                traceback.print_exc()
+                train[f"{leg}.{dt}"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                failed = True
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args)
