@@ -8,7 +8,8 @@
 //               of 4*NV ops per iteration, the same iteration count -> ticks per iteration of each
 //   VALU only : the VALU loop alone at one wave per SIMD (the issue cost to compare with)
 //   and the two-wave case with the VALU waves as the older half, or at s_setprio 3, or with the
-//   MFMA waves' loop as one asm block with the accumulators in AGPRs (or VGPRs)
+//   MFMA waves' loop as one asm block with the accumulators in AGPRs (or VGPRs); and the VALU
+//   loop at two waves per SIMD (the SIMD's VALU throughput with a second wave)
 // Kinds: v_add_u32, v_fma_f64, v_pk_fma_f32; the same with v_mfma_f32_16x16x4_f32 (32 cycles).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/mfma64_overlap.hip -o tools/mfma64_overlap
 #include <hip/hip_runtime.h>
@@ -117,12 +118,12 @@ __global__ __launch_bounds__(512) void kmix(double* out, unsigned long long* tic
     // MODE 3: the roles of MODE 1 swapped (the VALU waves are the older half); MODE 4: MODE 1
     // with the VALU waves at s_setprio 3
     const bool do_mfma = MODE == 0 || ((MODE == 1 || MODE == 4) && w < 4) || (MODE == 3 && w >= 4);
-    const bool do_valu = MODE == 0 || MODE == 2 || ((MODE == 1 || MODE == 4) && w >= 4) ||
+    const bool do_valu = MODE == 0 || MODE == 2 || MODE == 7 || ((MODE == 1 || MODE == 4) && w >= 4) ||
                          (MODE == 3 && w < 4);
     if (MODE == 4 && do_valu) __builtin_amdgcn_s_setprio(3);
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     double extra = 0;
-    if (MODE >= 5) {  // MODE 1 with the asm-loop MFMA waves: 5 AGPR, 6 VGPR accumulators
+    if (MODE == 5 || MODE == 6) {  // MODE 1 with the asm-loop MFMA waves: 5 AGPR, 6 VGPR accumulators
         if (w < 4)
             extra = mfma_loop<F32, MODE == 5>(a, b, iters);
         else
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(512) void kmix(double* out, unsigned long long* tic
 
 template <int MODE, int NV, int KIND, bool F32>
 void run(double* d, unsigned long long* tk, int iters, const char* kind) {
-    const int nt = (MODE == 1 || MODE >= 3) ? 512 : 256;
+    const int nt = (MODE == 1 || MODE >= 3) ? 512 : 256;  // MODE 7: VALU only, two waves per SIMD
     kmix<MODE, NV, KIND, F32><<<256, nt>>>(d, tk, iters / 4);  // warm
     kmix<MODE, NV, KIND, F32><<<256, nt>>>(d, tk, iters);
     (void)hipDeviceSynchronize();
@@ -190,6 +191,9 @@ void run(double* d, unsigned long long* tk, int iters, const char* kind) {
         }
         printf("%s two waves  %-12s NV %2d : MFMA wave %6.1f, VALU wave %6.1f ticks per iteration\n",
                F32 ? "f32" : "f64", kind, NV, lo, hi);
+    } else if (MODE == 7) {
+        printf("%s VALU only, two waves per SIMD  %-12s NV %2d : %6.1f / %6.1f ticks per iteration of each wave (%4.2f per op per SIMD)\n",
+               F32 ? "f32" : "f64", kind, NV, lo, hi, 0.5 * (lo + hi) / (2 * 4 * NV));
     } else if (MODE >= 5) {
         printf("%s two waves  %-12s NV %2d : MFMA wave %6.1f, VALU wave %6.1f ticks per iteration (asm loop, acc %s)\n",
                F32 ? "f32" : "f64", kind, NV, lo, hi, MODE == 5 ? "AGPR" : "VGPR");
@@ -228,6 +232,8 @@ void sweep(double* d, unsigned long long* tk, int iters, const char* kind) {
     run<6, 1, KIND, F32>(d, tk, iters, kind);
     run<6, 4, KIND, F32>(d, tk, iters, kind);
     run<6, 8, KIND, F32>(d, tk, iters, kind);
+    run<7, 4, KIND, F32>(d, tk, iters, kind);
+    run<7, 8, KIND, F32>(d, tk, iters, kind);
 }
 
 int main(int argc, char** argv) {
