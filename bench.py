@@ -20,6 +20,7 @@ the env path (weak scaling), the learner's gradients all-reduced over RCCL.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -48,6 +49,21 @@ STEP_BYTES = 37
 STEP_BYTES_BOOKKEEPING = 54
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
+# the learner kernels' PMC passes (tools/gpu_pmc_learner.sh -> tools/pmc_learner.py)
+PMC_LEARNER_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_learner.json")
+# the kernels of one update of each fused learner (the per-update launches; k_pack / k_adam run
+# only at setup or on the data-parallel path)
+UPDATE_KERNELS = {
+    ("conv", "fp64"): ("k_conv64_train_a", "k_conv64_train_b", "k_conv64_reduce"),
+    ("conv", "fp32"): ("k_conv_targets_persist", "k_conv_train_fwd", "k_conv_train_bwd",
+                       "k_reduce_pre"),
+    ("dense", "fp64"): ("k_dense_sample", "k_dense_forward", "k_dense_rows", "k_dense_wgrad",
+                        "k_dense_reduce"),
+    ("dense", "fp32"): ("k_dense_sample", "k_dense_forward", "k_dense_rows", "k_dense_wgrad",
+                        "k_dense_reduce"),
+    ("dense64", "fp32"): ("k_mlp_update1",),
+    ("dense64", "fp64"): ("k_dense64_update1_f64",),
+}
 INFINITY_CACHE_BYTES = 256 << 20  # MI355X_MICROARCH.md: die-level L3, 256 MiB
 RESIDENCY_RULE = ("MI355X_MICROARCH.md, Infinity Cache: a line stays resident while everything "
                   "loaded or stored between two uses of it fits in about 256 MiB")
@@ -76,6 +92,48 @@ def traffic_fields(rec, algorithmic: float) -> dict:
     return {"traffic": t, "traffic_over_algorithmic": t / algorithmic,
             "traffic_source": rec["source"] + "; FETCH_SIZE + WRITE_SIZE at the memory side of "
                               "L2 (Infinity-Cache hits included), per launch"}
+
+
+def learner_algorithmic_bytes(batch: int, params: int, elt: int) -> int:
+    """Bytes one update must move (learner): the B sampled transitions (s, s' 16 + 16,
+    a 1, r 4, d 1 = 38 B each), both nets' weights read once, Adam's moments and the parameters
+    read and written (m, v, p: 6 x params), and the rows / targets written (8 + elt per sample)."""
+    return batch * (38 + 8 + elt) + params * elt * (2 + 6)
+
+
+def learner_roofline(net: str, dtype: str, batch: int, update_s: float, params: int,
+                     algo_flop: float, peak_tf: float) -> dict:
+    """The roofline object of one learner leg: bound "mfma" (the update is GEMM-shaped work on
+    f32 / f64 MFMA); achieved = the ALGORITHMIC FLOPs (5 forward-equivalents of the direct net,
+    SURVEY 8d) over the event-timed update; executed_flop = the matrix FLOPs the kernels really
+    issue (Winograd conv2 issues fewer), and traffic = FETCH + WRITE bytes of the update's kernels,
+    both from the committed PMC passes (profiles/r06/pmc_learner.json, a separate rocprofv3 run)."""
+    elt = 4 if dtype == "fp32" else 8
+    algo_b = learner_algorithmic_bytes(batch, params, elt)
+    out = {"bound": "mfma", "achieved": algo_flop / update_s / 1e12, "peak": peak_tf,
+           "unit": "TFLOP/s", "frac": algo_flop / update_s / 1e12 / peak_tf,
+           "algorithmic_flop": algo_flop, "algorithmic_bytes": algo_b, "update_us": update_s * 1e6,
+           "executed_flop": None, "traffic": None}
+    try:
+        with open(PMC_LEARNER_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return out
+    tag = f"{net}.{dtype}@{batch}"
+    recs = {k: d.get(f"{k}@{tag}") for k in UPDATE_KERNELS.get((net, dtype), ())}
+    if not recs or any(r is None for r in recs.values()):
+        return out
+    if all("hbm_bytes_per_launch" in r for r in recs.values()):
+        t = sum(r["hbm_bytes_per_launch"] for r in recs.values())
+        out.update(traffic=t, traffic_over_algorithmic=t / algo_b,
+                   traffic_per_kernel={k: r["hbm_bytes_per_launch"] for k, r in recs.items()})
+    if all("mfma_flop" in r for r in recs.values()):
+        ex = sum(r["mfma_flop"] for r in recs.values())
+        out.update(executed_flop=ex, executed_tflops=ex / update_s / 1e12,
+                   executed_frac=ex / update_s / 1e12 / peak_tf)
+    out["traffic_source"] = (f"{os.path.relpath(PMC_LEARNER_FILE, ROOT)} "
+                             f"({d.get('_provenance', '')}); kernels {', '.join(recs)}")
+    return out
 
 
 def parse():
@@ -114,6 +172,8 @@ def parse():
 
 # RCCL ("nccl") in production; G2048_BENCH_BACKEND=gloo rehearses several ranks on one GPU
 BACKEND = os.environ.get("G2048_BENCH_BACKEND", "nccl")
+CTRL = None  # gloo side group (setup_dist): the ranks' agreement on a failed learner leg
+CTRL_TIMEOUT_S = float(os.environ.get("G2048_BENCH_CTRL_TIMEOUT_S", "600"))
 
 
 def launch_ranks(args) -> int:
@@ -148,6 +208,13 @@ def pick_device(local: int, world: int, backend: str, n_dev: int) -> int:
 
 
 def setup_dist(args):
+    """One process per GPU.  world > 1: an RCCL ("nccl") process group (gloo in the one-GPU
+    rehearsal), plus a gloo side group for the ranks' agreement on a failed leg.  G2048_BENCH_DIST=1
+    at world 1 builds the same groups around ONE rank, so every distributed path of this file --
+    the RCCL barrier, max-over-ranks, thread-local captures, the learner's captured SUM all-reduce
+    with 1 / world in Adam, the fixed-count settle and the GPU all_gather of the lockstep check --
+    runs on a one-GPU box before the driver's multi-GPU run (tests/test_bench_rccl_gpu.py)."""
+    global CTRL
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
@@ -155,16 +222,36 @@ def setup_dist(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", pick_device(local, world, BACKEND, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 or os.environ.get("G2048_BENCH_DIST") == "1":
+        if world == 1:  # a one-rank group: a local rendezvous of its own
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if BACKEND == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(BACKEND)
+        # control plane on the host: a rank whose learner leg failed may have left the RCCL
+        # communicator unusable (or its peers blocked in a replayed collective)
+        CTRL = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=CTRL_TIMEOUT_S))
     return world, rank, dev
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def distributed() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world, dev):
-    if world > 1:
+    if distributed():
         if BACKEND == "nccl":
             dist.barrier(device_ids=[dev.index])
         else:
@@ -172,7 +259,7 @@ def barrier(world, dev):
 
 
 def max_over_ranks(x: float, world: int, dev) -> float:
-    if world == 1:
+    if not distributed():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -180,11 +267,28 @@ def max_over_ranks(x: float, world: int, dev) -> float:
 
 
 def sum_over_ranks(x: float, world: int, dev) -> float:
-    if world == 1:
+    if not distributed():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t)
     return float(t.item())
+
+
+def any_rank_failed(failed: bool) -> bool:
+    """The ranks' agreement after a learner leg, over the gloo side group: True if ANY rank
+    failed it.  A rank whose peers never arrive (one of them failed and the others are blocked in
+    a collective it will not join) times out here after CTRL_TIMEOUT_S and exits non-zero, which
+    makes torch.distributed.run stop every rank: the job fails loudly instead of hanging."""
+    if CTRL is None:
+        return failed
+    t = torch.tensor([1 if failed else 0], dtype=torch.int32)
+    try:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=CTRL)
+    except Exception as e:  # noqa: BLE001 -- a timeout or a dead peer
+        print(f"bench.py rank {dist.get_rank()}: no agreement on the learner leg ({e}); "
+              "exiting non-zero", file=sys.stderr, flush=True)
+        os._exit(3)
+    return bool(t.item())
 
 
 def timed(world, dev, fn, reps: int):
@@ -224,16 +328,19 @@ def settle(replay, ms: float, max_calls: int = 4000) -> float:
 
 
 def capture(fn, n_steps: int):
-    if dist.is_initialized() and BACKEND == "nccl":  # ProcessGroupNCCL's watchdog (g2048/dist.py)
-        from g2048.dist import quiesce_for_capture
-        quiesce_for_capture()
+    """A hipGraph of n_steps calls of fn.  In a process holding an RCCL group the capture is
+    thread-local: ProcessGroupNCCL's watchdog thread queries events while this thread records
+    (g2048/dist.py: capture_error_mode)."""
+    from g2048.dist import capture_error_mode, quiesce_for_capture
+
+    quiesce_for_capture()
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         fn()  # one eager call on the side stream before capture
     torch.cuda.current_stream().wait_stream(s)
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode=capture_error_mode()):
         for _ in range(n_steps):
             fn()
     return g
@@ -378,7 +485,10 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
     env = g2048.VecEnv2048(n, seed=args.seed + 7, device=dev, board_offset=rank * n)
     rb = g2048.ReplayBuffer(C, device=dev)
     tdt = torch.float32 if dtype == "fp32" else torch.float64
-    L = DQNLearner(rb, net=net, dtype=tdt, batch_size=batch, target_sync_every=100)
+    # in a process group (also a one-rank one, G2048_BENCH_DIST=1): the data-parallel update, with
+    # the gradient SUM all-reduce captured in the update's graph under RCCL
+    L = DQNLearner(rb, net=net, dtype=tdt, batch_size=batch, target_sync_every=100,
+                   data_parallel=True if distributed() else None)
     T = Trainer(env, rb, L, updates_per_step=1, min_fill=0)
     T.prefill(C // n)  # replay pre-filled by random-policy rollout steps (one launch)
     for _ in range(5):
@@ -388,7 +498,7 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
     K = args.train_updates if dtype == "fp32" else max(args.train_updates // 4, 10)
     # untimed updates for --settle-ms (the clock ramp, as for the rollout legs: a fp64 conv update
     # timed right after a short warm-up reads ~160 us, sustained ~151 us)
-    if world == 1:
+    if not distributed():
         settle_ms = settle(L.update, args.settle_ms, max_calls=2000)
     else:  # every rank must run the same number of updates (each holds a collective)
         t0 = time.perf_counter()
@@ -408,7 +518,7 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
     loss = float(L.last_loss)
     env.check_errors()
     lockstep = None
-    if world > 1:  # the replicas (online + target nets) must agree bit for bit on every rank
+    if distributed():  # the replicas (online + target nets) must agree bit for bit on every rank
         flat = torch.cat([p.detach().reshape(-1) for p in
                           list(L.model.parameters()) + list(L.target.parameters())])
         flat = flat if BACKEND == "nccl" else flat.cpu()
@@ -429,7 +539,10 @@ def bench_train(args, world, rank, dev, net, dtype, batch):
             "loop_late_env_steps_per_s": sum_over_ranks(n * K2 / late_wall, world, dev),
             "loop_late_epsilon_mean": eps_late,
             "batch": batch, "replay": C, "dtype": dtype, "loss": loss, "settle_ms": settle_ms,
-            "params": L.n_params, "graphed_loop": T.graph, "ranks_lockstep": lockstep}
+            "params": L.n_params, "graphed_loop": T.graph, "ranks_lockstep": lockstep,
+            "data_parallel": L.dp, "captured_allreduce": L.capture_collective,
+            "grad_scale": L.grad_scale,
+            "roofline": learner_roofline(net, dtype, batch, upd_ev / K, L.n_params, fl, peak)}
 
 
 # ------------------------------------------------------------------ CPU baselines
@@ -454,7 +567,7 @@ def main():
     n, k = ro["n"], ro["k"]
     value = n * k * world * args.steps / ro["wall"]
     ranges = [[ro["board_offset"], n]]
-    if world > 1:  # every rank's global board range: disjoint Philox subsequences
+    if distributed():  # every rank's global board range: disjoint Philox subsequences
         got = [None] * world
         dist.all_gather_object(got, ranges[0])
         ranges = got
@@ -502,19 +615,25 @@ def main():
             if failed:
                 train[f"{leg}.{dt}"] = {"error": "skipped after an earlier learner leg failed"}
                 continue
+            mine = False
             try:
                 train[f"{leg}.{dt}"] = bench_train(args, world, rank, dev, net, dt,
                                                    int(b) if b else args.batch)
             except Exception as e:
-                # one rank per GPU (world > 1): the learner legs are the only ones that capture
-                # RCCL collectives; a failure there is reported in the line and the remaining
-                # learner legs are skipped, so the env-step headline measured above still
-                # prints.  One process (world == 1) fails loudly.
-                if world == 1:
+                # one process without a group fails loudly.  In a process group the learner legs
+                # are the only ones that capture RCCL collectives: the failing leg is reported in
+                # the line and the remaining learner legs are skipped on EVERY rank (agreed over
+                # the gloo side group), so the env-step headline measured above still prints
+                if not distributed():
                     raise
                 traceback.print_exc()
                 train[f"{leg}.{dt}"] = {"error": f"{type(e).__name__}: {e}"[:400]}
+                mine = True
+            if any_rank_failed(mine):
                 failed = True
+                if not mine:
+                    train[f"{leg}.{dt}"] = {"error": "failed on another rank",
+                                            "this_rank": train[f"{leg}.{dt}"]}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baselines(args)
@@ -544,6 +663,9 @@ def main():
                        "parallelism": f"dp{world} (boards sharded, no collective)"},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "dist": {"process_group": distributed(),
+                     "backend": dist.get_backend() if distributed() else None,
+                     "capture_error_mode": _capture_mode_name()},
         }
         if hbm64:
             line["rollout_64k_hbm"] = hbm64
@@ -556,8 +678,13 @@ def main():
         if train:
             line["learner"] = train
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed():
         dist.destroy_process_group()
+
+
+def _capture_mode_name() -> str:
+    from g2048.dist import capture_error_mode
+    return capture_error_mode()
 
 
 if __name__ == "__main__":

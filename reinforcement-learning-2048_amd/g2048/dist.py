@@ -87,22 +87,33 @@ def captures_collectives(group=None) -> bool:
             and dist.get_backend(group) == dist.Backend.NCCL)
 
 
-# ProcessGroupNCCL's watchdog thread polls the events of every eager collective until it sees them
-# complete (~every 100 ms).  A poll that lands while this thread captures a hipGraph invalidates the
-# capture (hipErrorStreamCaptureUnsupported, then a DistBackendError from the watchdog): seen once
-# in six captures on one GPU with a world-1 RCCL group.  Captures started after the watchdog has
-# retired every eager collective are safe (collectives enqueued DURING a capture are not handed to
-# the watchdog).
-QUIESCE_S = 0.35
+def nccl_group_exists() -> bool:
+    """Whether this process holds a ProcessGroupNCCL (RCCL) default group."""
+    return (dist.is_available() and dist.is_initialized()
+            and dist.get_backend() == dist.Backend.NCCL)
+
+
+def capture_error_mode(group=None) -> str:
+    """torch.cuda.graph's capture_error_mode for ANY hipGraph captured in this process.
+
+    ProcessGroupNCCL's watchdog thread polls the events of every eager collective
+    (hipEventQuery, ~every 100 ms) until it sees them complete.  Under a "global"-mode capture
+    that query, made by another thread, is an unsafe call: it invalidates the capture
+    (hipErrorStreamCaptureInvalidated) and fails in the watchdog ("operation not permitted when
+    stream is capturing"), which then tears the process group down -- seen in round 5 on a
+    global-mode capture next to a world-1 RCCL group.  "thread_local" confines the capture's
+    rules to the capturing thread, so the watchdog's queries are legal whenever they land.  So
+    every capture in a process that holds an NCCL group is thread-local; elsewhere torch's
+    default "global" (which also catches an unsafe call from a helper thread of ours)."""
+    return "thread_local" if (captures_collectives(group) or nccl_group_exists()) else "global"
 
 
 def quiesce_for_capture(group=None) -> None:
-    """Before a hipGraph capture in an RCCL process: drain the device and give ProcessGroupNCCL's
-    watchdog time to retire the eager collectives it still polls (no-op without RCCL)."""
-    if captures_collectives(group):
-        import time
+    """Before a hipGraph capture in an RCCL process: drain the device, so the side-stream warm-up
+    (and its eager collectives) are complete when the capture starts.  The watchdog race itself
+    is closed by the thread-local capture mode (capture_error_mode), not by waiting."""
+    if captures_collectives(group) or nccl_group_exists():
         torch.cuda.synchronize()
-        time.sleep(QUIESCE_S)
 
 
 def shard_offset(rank: int, boards_per_rank: int) -> int:

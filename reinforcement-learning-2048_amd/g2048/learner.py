@@ -19,8 +19,8 @@ import copy
 import torch
 
 from . import dqn_lib
-from .dist import (FlatGradBucket, broadcast_params, captures_collectives, quiesce_for_capture,
-                   world_size)
+from .dist import (FlatGradBucket, broadcast_params, capture_error_mode, captures_collectives,
+                   quiesce_for_capture, world_size)
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, make_net
 from . import qnet
@@ -258,7 +258,7 @@ class DQNLearner:
         g2 = None
         if self.dp and not self.capture_collective:  # gloo: the collective between two replays
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2):
+            with torch.cuda.graph(g2, capture_error_mode=capture_mode(self)):
                 self._apply()
         self._graphs = (g1, g2)
         with torch.no_grad():  # restore in place (the graphs hold these addresses)
@@ -350,7 +350,14 @@ class DQNLearner:
     def load_state_dict(self, st: dict) -> None:
         """Restore in place: parameter, optimizer and counter tensors keep their addresses, so
         already-captured graphs stay valid."""
-        if bool(st["fused"]) != self.fused or st["kind"] != (self.kind or ""):
+        # the reference dense net trained on the torch path up to round 4 (fused False, kind ''):
+        # the same parameters and Adam (torch's per-parameter state, converted below), so its
+        # checkpoints resume on the fused update; they hold no sampler seed (the torch path drew
+        # minibatches with torch's RNG), so this learner's own seed is kept
+        torch_path_dense = (not bool(st["fused"]) and st["kind"] == "" and self.kind == "dense"
+                            and self.fused)
+        if not torch_path_dense and (bool(st["fused"]) != self.fused
+                                     or st["kind"] != (self.kind or "")):
             raise ValueError("checkpoint was written by a learner of another net / path")
         for k, v in (("batch_size", self.B), ("gamma", self.gamma), ("double_dqn", self.use_double_dqn),
                      ("dtype", str(self.dtype))):
@@ -371,7 +378,7 @@ class DQNLearner:
             self._adam.exp_avg.copy_(st["adam_exp_avg"])
             self._adam.exp_avg_sq.copy_(st["adam_exp_avg_sq"])
             self.step_dev.copy_(st["step_dev"])
-            if self.fused:
+            if self.fused and not torch_path_dense:
                 self.sample_seed = int(st["sample_seed"])
         else:
             for p, saved in zip(self.bucket.params, st["adam"]):
@@ -523,10 +530,10 @@ class Trainer:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
             quiesce_for_capture(L.pg)
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga):
+            with torch.cuda.graph(ga, capture_error_mode=capture_mode(L)):
                 self._rollout_step()
                 L._compute_grads()
-            with torch.cuda.graph(gb):
+            with torch.cuda.graph(gb, capture_error_mode=capture_mode(L)):
                 L._apply()
             self._loop_graph = (ga, gb)
         ga, gb = self._loop_graph
@@ -691,10 +698,12 @@ class Trainer:
 
 
 def capture_mode(learner) -> str:
-    """torch.cuda.graph's capture_error_mode for a graph of this learner's update: "thread_local"
-    when it holds the RCCL collective (ProcessGroupNCCL's watchdog thread keeps querying its events
-    while the capturing thread records), else torch's default "global"."""
-    return "thread_local" if learner.capture_collective else "global"
+    """torch.cuda.graph's capture_error_mode for every graph of this learner (update, loop
+    iteration, the gloo form's two graphs): "thread_local" whenever the process holds an RCCL
+    group -- ProcessGroupNCCL's watchdog thread queries events while the capturing thread records,
+    which a global-mode capture treats as an unsafe call (g2048/dist.py: capture_error_mode) --
+    else torch's default "global"."""
+    return capture_error_mode(learner.pg)
 
 
 def _flat_adam_state(per_param: list, params) -> dict:

@@ -69,6 +69,49 @@ def test_resume_is_bit_exact(G, net, tmp_path):
     assert b.learner.updates == a.learner.updates and b.steps == a.steps
 
 
+def test_resume_round4_dense_checkpoint(G):
+    """the reference dense net trained on the torch path up to round 4; its checkpoints
+    (learner fused=False, kind '', torch Adam state per parameter, no sampler seed) resume on the
+    fused dense-ref update: same weights, Adam moments and step, and -- the sampler seed being the
+    learner's own -- the same next updates, bit for bit."""
+    a = _small(G, "dense")
+    assert a.learner.fused and a.learner.kind == "dense"
+    for _ in range(12):
+        a.step()
+    st = a.state_dict()
+    L = dict(st["learner"])
+    flat_m, flat_v = L.pop("adam_exp_avg"), L.pop("adam_exp_avg_sq")
+    step = L.pop("step_dev")
+    L.pop("sample_seed")
+    per, off = [], 0
+    for p in a.learner.bucket.params:  # round 4: torch.optim.Adam(capturable=True) state
+        n = p.numel()
+        per.append({"step": step.to(torch.float32).reshape(()),
+                    "exp_avg": flat_m[off:off + n].view_as(p).clone(),
+                    "exp_avg_sq": flat_v[off:off + n].view_as(p).clone()})
+        off += n
+    L.update(fused=False, kind="", adam=per)
+    old = dict(st, learner=L)
+    for _ in range(5):
+        a.step()
+    want = _fingerprint(a)
+    b = _small(G, "dense")
+    b.load_state_dict(old)
+    assert torch.equal(b.learner._adam.exp_avg.cpu(), flat_m)
+    assert torch.equal(b.learner.step_dev.cpu(), step)
+    for _ in range(5):
+        b.step()
+    got = _fingerprint(b)
+    for k in ("board", "replay_s", "loss"):
+        assert torch.equal(got[k], want[k]), k
+    for x, y in zip(got["params"] + got["target"], want["params"] + want["target"]):
+        assert torch.equal(x, y)
+    c = _small(G, "conv")  # another net's torch-path checkpoint is still refused
+    with pytest.raises(ValueError, match="another net"):
+        c.load_state_dict(dict(c.state_dict(), learner=dict(c.state_dict()["learner"],
+                                                            fused=False, kind="")))
+
+
 def test_load_rejects_mismatch(G):
     a = _small(G, "conv")
     st = a.state_dict()
