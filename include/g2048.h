@@ -377,7 +377,10 @@ G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* params,
  * and call g2048_adam_step afterwards.  idx_out / y_out receive the rows and targets; loss_out the
  * loss (nullable).  With Adam and sync_every > 0, the updated parameters are also written to the
  * TARGET net when t % sync_every == 0 (the target sync of training_loop, decided on the device).
- * workspace: f32[g2048_dense64_update_workspace(batch)]. */
+ * G2048_DENSE64_ONE_LAUNCH=1 in the environment selects a one-launch form, bitwise the same
+ * update (the last workgroups to finish their tiles reduce, synchronised through arrival counters
+ * at the workspace's tail, which every update leaves at zero); measured slower, not the default.
+ * workspace: f32[g2048_dense64_update_workspace(batch)], zero-filled before its first use. */
 G2048_API int64_t g2048_dense64_update_workspace(int64_t batch);
 G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
                                    const g2048_dense64_params* target, g2048_replay* rb,
@@ -396,7 +399,8 @@ G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
  * reduction that writes grad_out / loss_out and -- with exp_avg / exp_avg_sq -- applies torch's
  * Adam in float64 to the ONLINE parameters in place (+ the target sync when t % sync_every ==
  * 0).  Same step_dev protocol as g2048_dense64_update.  Parameters are device float64 tensors in
- * torch's layouts (Linear [out][in]).  workspace: f64[g2048_dense64_update_f64_workspace(B)]. */
+ * torch's layouts (Linear [out][in]).  G2048_DENSE64_ONE_LAUNCH as for g2048_dense64_update.
+ * workspace: f64[g2048_dense64_update_f64_workspace(B)], zero-filled before its first use. */
 typedef struct {
     double *w1, *b1; /* Linear(16, 64) */
     double *w2, *b2; /* Linear(64, 4)  */

@@ -41,9 +41,15 @@ __global__ __launch_bounds__(256) void k_adam(AdamArgs A) {
     float* p = A.p[k] + (i - A.off[k]);
     const unsigned long long t = *A.step;
     const g2048::AdamCoef c = g2048::adam_coef((double)t, A.lr, A.b1, A.b2, A.eps);
-    // the scaled gradient is rounded on its own (no contraction into Adam's first fma), so a
-    // scaled step is bitwise the unscaled step on the pre-scaled gradient for ANY scale
-    const float np = g2048::adam_apply(c, __fmul_rn(A.g[i], A.gscale), A.m + i, A.v + i, *p);
+    // the scaled gradient is rounded on its own (contraction off: HIP's __fmul_rn is a plain
+    // multiply, which the compiler fused into Adam's g - m), so a scaled step is bitwise the
+    // unscaled step on the pre-scaled gradient for ANY scale
+    float gs;
+    {
+#pragma clang fp contract(off)
+        gs = A.g[i] * A.gscale;
+    }
+    const float np = g2048::adam_apply(c, gs, A.m + i, A.v + i, *p);
     *p = np;
     // target sync (src/dqn_lib.py:227-228 load_state_dict after the update) on the device
     // counter, so an update that syncs needs no host decision between graph replays
@@ -76,8 +82,12 @@ __global__ __launch_bounds__(256) void k_adam64(AdamArgs64 A) {
     double* p = A.p[k] + (i - A.off[k]);
     const unsigned long long t = *A.step;
     double m = A.m[i], v = A.v[i];
-    const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps,
-                                    __dmul_rn(A.g[i], A.gscale), m, v, *p);
+    double gs;
+    {
+#pragma clang fp contract(off)
+        gs = A.g[i] * A.gscale;
+    }
+    const double np = g2048::adam64((double)t, A.lr, A.b1, A.b2, A.eps, gs, m, v, *p);
     A.m[i] = m;
     A.v[i] = v;
     *p = np;

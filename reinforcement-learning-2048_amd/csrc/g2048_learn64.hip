@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
@@ -117,7 +118,29 @@ struct UpdArgs64 {
     unsigned long long* step_next;
 };
 
-__global__ __launch_bounds__(NT) void k_dense64_update_f64(UpdArgs64 A) {
+// A slab element: a plain store, or (COH) a device-scope sc1 store through the XCD's L2 to the
+// coherent level, read back by the same launch's reducers with sc1 loads (as g2048_mlp.hip's
+// slab_put: buffer forms, so the reducers' loads batch).
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr int AUX_SC1 = 16;  // gfx950 buffer cache-policy word: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const double* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+// sl: the workgroup's slab (wave-uniform: the resource stays in SGPRs; a per-lane base would
+// need a waterfall loop over the lanes' resources); e: the element
+template <bool COH>
+__device__ __forceinline__ void slab_put(double* sl, int e, double v) {
+    if constexpr (COH)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), slab_rsrc(sl),
+                                              (uint32_t)e * 8u, 0u, AUX_SC1);
+    else
+        sl[e] = v;
+}
+
+// a workgroup's tiles and its gradient slab (k_dense64_update_f64, and the first half of
+// k_dense64_update1_f64; COH: the slab written through to the coherent level)
+template <bool COH>
+__device__ __forceinline__ void update_tiles64(const UpdArgs64& A) {
     __shared__ Smem M;
     const int t = threadIdx.x, j = t & 63, qd = t >> 6;
     const unsigned long long ep = A.idx_in ? 0ull : *A.step;
@@ -246,12 +269,14 @@ __global__ __launch_bounds__(NT) void k_dense64_update_f64(UpdArgs64 A) {
     // slab in torch order: 0.weight [64][16], 0.bias [64], 2.weight [4][64], 2.bias [4], loss
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sl[P_W1 + j * 16 + 4 * qd + i] = g_w1[i];
-    if (qd == 0) sl[P_B1 + j] = g_b1;
-    sl[P_W2 + qd * 64 + j] = g_w2;
-    if (j == 0) sl[P_B2 + qd] = g_b2;
-    if (t == 0) sl[P_N] = g_loss;
+    for (int i = 0; i < 4; ++i) slab_put<COH>(sl, P_W1 + j * 16 + 4 * qd + i, g_w1[i]);
+    if (qd == 0) slab_put<COH>(sl, P_B1 + j, g_b1);
+    slab_put<COH>(sl, P_W2 + qd * 64 + j, g_w2);
+    if (j == 0) slab_put<COH>(sl, P_B2 + qd, g_b2);
+    if (t == 0) slab_put<COH>(sl, P_N, g_loss);
 }
+
+__global__ __launch_bounds__(NT) void k_dense64_update_f64(UpdArgs64 A) { update_tiles64<false>(A); }
 
 constexpr int RW = 16;  // waves per reduction block
 static_assert(MAX_SLABS <= RW * 16, "reduction covers at most RW*16 slabs");
@@ -272,34 +297,53 @@ struct RedArgs64 {
     int adam;
 };
 
-// block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... in order (all of its
-// loads in flight at once), then wave 0 combines the 16 partials in order and (adam) applies the
-// update to the parameter in place; wave 0's Adam operands are loaded with the slabs.
-__global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
-    __shared__ double part[RW][64];
+// The fixed-order sum of slab position chunk*64 + lane: partials p_w = 0 + slab[w] + slab[w + 16]
+// + ... (w = 0 .. 15, all of a wave's loads in flight at once), then p_0 + ... + p_15 by wave 0,
+// which writes the gradient / loss and (adam) applies the update (step t) to the parameter in
+// place; wave 0's Adam operands are loaded with the slabs.  The calling block's NW waves take the
+// partials w = wave, wave + NW, ...: k_dense64_reduce_f64 (16 waves) and k_dense64_update1_f64's
+// reducers (4 waves, COH: sc1 loads of slabs written in the same launch) sum in exactly this order.
+template <int NW, bool COH>
+__device__ __forceinline__ void reduce_positions64(const RedArgs64& A, int chunk,
+                                                   unsigned long long t, double (*part)[64]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pos = blockIdx.x * 64 + lane;
+    const int pos = chunk * 64 + lane;
     const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
     const int base[4] = {P_W1, P_B1, P_W2, P_B2};
     const bool adam = A.adam && wave == 0 && pos < P_N;
     double am = 0.0, av = 0.0, ap = 0.0;
-    unsigned long long t = 0;
     if (adam) {
-        t = *A.step_next;
         am = A.m[pos];
         av = A.v[pos];
         ap = A.p[k][pos - base[k]];
     }
-    double v[16];
+    constexpr int PW = RW / NW;
+    // unconditional loads from clamped (valid) addresses, zeroed after (batched, not branched)
+    const bool okp = pos <= P_N;
+    const int pc = okp ? pos : P_N;
+    double v[PW][16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int g = wave + RW * u;
-        v[u] = (pos <= P_N && g < A.nslab) ? A.slab[(int64_t)g * SLAB + pos] : 0.0;
+    for (int i = 0; i < PW; ++i)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int g = wave + NW * i + RW * u;
+            const bool ok = okp && g < A.nslab;
+            const int64_t e = (int64_t)(g < A.nslab ? g : 0) * SLAB + pc;
+            double x;
+            if constexpr (COH)
+                x = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                                   slab_rsrc(A.slab), (uint32_t)(e * 8), 0u, AUX_SC1));
+            else
+                x = A.slab[e];
+            v[i][u] = ok ? x : 0.0;
+        }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        double r = 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) r += v[i][u];
+        part[wave + NW * i][lane] = r;
     }
-    double r = 0.0;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) r += v[u];
-    part[wave][lane] = r;
     __syncthreads();
     if (wave == 0 && pos <= P_N) {
         double sum = part[0][lane];
@@ -317,16 +361,80 @@ __global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
             }
         }
     }
+}
+
+constexpr int RCHUNKS = (P_N + 1 + 63) / 64;  // 64-position chunks of the slab (loss included)
+
+__global__ __launch_bounds__(64 * RW) void k_dense64_reduce_f64(RedArgs64 A) {
+    __shared__ double part[RW][64];
+    reduce_positions64<RW, false>(A, blockIdx.x, A.adam ? *A.step_next : 0ull, part);
     if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
+}
+
+// The whole float64 update in ONE launch, as k_mlp_update1 (g2048_mlp.hip): every workgroup
+// writes its slab with sc1 stores, waits for them and counts its arrival; the last
+// min(RCHUNKS, grid) to arrive reduce (after every arrival, sc1 loads) in k_dense64_reduce_f64's
+// order with t = *step + 1; the last reducer returns the counters (workspace tail, zeroed before
+// first use) to 0.
+struct Upd1Args64 {
+    UpdArgs64 U;
+    RedArgs64 R;
+    unsigned int* arrive;  // [0] arrivals, [1] reducers done, [2] error count
+};
+
+__global__ __launch_bounds__(NT) void k_dense64_update1_f64(Upd1Args64 A) {
+    const unsigned long long t_next = *A.U.step + 1ull;
+    update_tiles64<true>(A.U);
+    __shared__ unsigned int s_arrival;
+    __shared__ double part[RW][64];
+    const unsigned grid = gridDim.x;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's slab stores are complete
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_arrival = __hip_atomic_fetch_add(&A.arrive[0], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned a = s_arrival;
+    const unsigned nred = grid < (unsigned)RCHUNKS ? grid : (unsigned)RCHUNKS;
+    if (a >= grid) {  // a workspace that was not zeroed
+        if (threadIdx.x == 0) atomicAdd(&A.arrive[2], 1u);
+        return;
+    }
+    if (a < grid - nred) return;
+    const unsigned me = a - (grid - nred);
+    if (threadIdx.x == 0) {
+        unsigned it = 0;
+        while (__hip_atomic_load(&A.arrive[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < grid) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++it == (1u << 24)) {
+                atomicAdd(&A.arrive[2], 1u);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    for (unsigned c = me; c < (unsigned)RCHUNKS; c += nred) {
+        reduce_positions64<NT / 64, true>(A.R, (int)c, t_next, part);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        if (me == 0 && A.R.step) *A.R.step = t_next;
+        if (__hip_atomic_fetch_add(&A.arrive[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            nred - 1) {
+            __hip_atomic_store(&A.arrive[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&A.arrive[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace
 
 extern "C" G2048_API int64_t g2048_dense64_update_f64_workspace(int64_t batch) {
-    // slabs (<= 256 workgroups) + the next-step word, in doubles
+    // slabs (<= 256 workgroups) + the next-step word + the one-launch form's u32 counters
+    // (arrivals, reducers done, errors, pad), in doubles
     const int64_t tiles = (batch + S - 1) / S;
     const int64_t grid = tiles < MAX_SLABS ? tiles : MAX_SLABS;
-    return grid * SLAB + 2;
+    return grid * SLAB + 1 + 2;
 }
 
 extern "C" G2048_API int g2048_dense64_update_f64(
@@ -371,7 +479,6 @@ extern "C" G2048_API int g2048_dense64_update_f64(
     U.slab = workspace;
     U.step_next = reinterpret_cast<unsigned long long*>(workspace + (int64_t)grid * SLAB);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(k_dense64_update_f64, dim3(grid), dim3(NT), 0, st, U);
     RedArgs64 R;
     R.slab = workspace;
     R.nslab = grid;
@@ -393,7 +500,18 @@ extern "C" G2048_API int g2048_dense64_update_f64(
     R.b2 = beta2;
     R.eps = eps;
     R.adam = adam ? 1 : 0;
-    hipLaunchKernelGGL(k_dense64_reduce_f64, dim3((P_N + 1 + 63) / 64), dim3(64 * RW), 0, st, R);
+    // G2048_DENSE64_ONE_LAUNCH=1: the one-launch form (measured slower, as in g2048_mlp.hip)
+    const char* one = getenv("G2048_DENSE64_ONE_LAUNCH");
+    if (one && one[0] == '1') {
+        Upd1Args64 A1;
+        A1.U = U;
+        A1.R = R;
+        A1.arrive = reinterpret_cast<unsigned int*>(U.step_next + 1);
+        hipLaunchKernelGGL(k_dense64_update1_f64, dim3(grid), dim3(NT), 0, st, A1);
+    } else {
+        hipLaunchKernelGGL(k_dense64_update_f64, dim3(grid), dim3(NT), 0, st, U);
+        hipLaunchKernelGGL(k_dense64_reduce_f64, dim3(RCHUNKS), dim3(64 * RW), 0, st, R);
+    }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK
                            : g2048_fail(G2048_EHIP, "dense64_update_f64: %s", hipGetErrorString(e));

@@ -12,6 +12,7 @@
 // once per workgroup in torch's parameter order; a deterministic reduction sums the slabs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/g2048.h"
 #include "g2048_board.hpp"
@@ -255,25 +256,46 @@ __device__ __forceinline__ void grad_tile(Tile<S>& T, const LW& W, float4 w1v, G
     }
 }
 
+// A slab element: a plain store, or (COH) a device-scope store -- the sc1 cache policy (the bits
+// the compiler gives an agent-scope atomic store on gfx950) writes it through the XCD's L2 to the
+// coherent level, so a workgroup of the same launch on another XCD can read it (with sc1 loads)
+// without an L2 write-back or invalidate (k_mlp_update1).  Buffer forms, not atomics: relaxed
+// atomic loads are each followed by a vmcnt(0) wait, which would serialise the reduction's loads.
+constexpr int AUX_SC1 = 16;  // gfx950 buffer cache-policy word: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(const float* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, 0x7FFFFFFF, 0x00020000);
+}
+// slab: the workgroup's slab (wave-uniform, so the resource is built in SGPRs once; a per-lane
+// base would need a waterfall loop over the lanes' resources); e: the element
+template <bool COH>
+__device__ __forceinline__ void slab_put(float* slab, int e, float v) {
+    if constexpr (COH)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), slab_rsrc(slab),
+                                              (uint32_t)e * 4u, 0u, AUX_SC1);
+    else
+        slab[e] = v;
+}
+
 // the workgroup's gradient slab in torch parameter order + its loss (scratch: S*4 >= 64 floats)
-template <int S>
+template <int S, bool COH = false>
 __device__ __forceinline__ void write_slab(const GradAcc& G, Tile<S>& T, float* slab) {
     const int t = threadIdx.x;
     {  // dW1[16w + 4g + i][l16]
         const int lane = t & 63, wave = t >> 6, g = lane >> 4, l16 = lane & 15;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) slab[P_W1 + (16 * wave + 4 * g + i) * 16 + l16] = G.w1a[i] + G.w1b[i];
+        for (int i = 0; i < 4; ++i)
+            slab_put<COH>(slab, P_W1 + (16 * wave + 4 * g + i) * 16 + l16, G.w1a[i] + G.w1b[i]);
     }
-    if (t < H) slab[P_B1 + t] = G.b1;
-    slab[P_W2 + t] = G.w2;  // t = a*64 + j
-    if ((t & 63) == 0) slab[P_B2 + (t >> 6)] = G.b2;
+    if (t < H) slab_put<COH>(slab, P_B1 + t, G.b1);
+    slab_put<COH>(slab, P_W2 + t, G.w2);  // t = a*64 + j
+    if ((t & 63) == 0) slab_put<COH>(slab, P_B2 + (t >> 6), G.b2);
     __syncthreads();
     if (t < S) T.q[t] = G.loss;  // threads >= S hold 0
     __syncthreads();
     if (t == 0) {
         float v = 0.f;
         for (int i = 0; i < S; ++i) v += T.q[i];
-        slab[P_N] = v;
+        slab_put<COH>(slab, P_N, v);
     }
 }
 
@@ -417,7 +439,10 @@ struct UpdateArgs {
 #define MPHASE(k)
 #endif
 
-__global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
+// the update's per-workgroup work (k_mlp_update, and the first half of k_mlp_update1): every
+// tile of the workgroup, then its gradient slab (COH: written through to the coherent level)
+template <bool COH>
+__device__ __forceinline__ void update_tiles(const UpdateArgs& A) {
     constexpr int S = S_UPD;
     MPHASE(0);
     __shared__ LW Won, Wtg;
@@ -484,9 +509,11 @@ __global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) {
 #endif
         MPHASE(5);
     }
-    write_slab<S>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
+    write_slab<S, COH>(G, T, A.slab + (int64_t)blockIdx.x * SLAB);
     MPHASE(6);
 }
+
+__global__ __launch_bounds__(NT) void k_mlp_update(UpdateArgs A) { update_tiles<false>(A); }
 
 // block = 64 slab positions x 16 waves: wave w sums slabs w, w+16, ... (<= 16 loads, all in
 // flight at once), then a fixed-order combine of the 16 partials.  With `adam`, the summed
@@ -511,37 +538,61 @@ struct ReduceArgs {
     int adam;
 };
 
-__global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
-    __shared__ float part[RW][64];
+// The fixed-order sum of slab position `pos` (partials p_w = slab[w] + slab[w + 16] + ... for
+// w = 0 .. 15, then p_0 + ... + p_15) and what follows it: the gradient / loss written and, with
+// `adam`, torch Adam applied (step t) + the target sync.  `part` is LDS [RW][64]; the calling
+// block's NW waves compute the partials w = wave, wave + NW, ... (all of a wave's slab loads in
+// flight at once); wave 0 finishes.  k_mlp_reduce (16 waves) and k_mlp_update1's reducers (4
+// waves, COH: agent-scope loads of the slabs other XCDs wrote in the same launch) run it, so both
+// sum in exactly this order (bitwise the same update).
+template <int NW, bool COH>
+__device__ __forceinline__ void reduce_positions(const ReduceArgs& A, int chunk,
+                                                 unsigned long long t, float (*part)[64]) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int pos = blockIdx.x * 64 + lane;
+    const int pos = chunk * 64 + lane;
     // Adam operands (wave 0) loaded with the slabs: independent of the sums
     const bool adam = A.adam && wave == 0 && pos < P_N;
     const int k = pos < P_B1 ? 0 : pos < P_W2 ? 1 : pos < P_B2 ? 2 : 3;
     const int base[4] = {P_W1, P_B1, P_W2, P_B2};
     float am = 0.f, av = 0.f, ap = 0.f;
-    unsigned long long t = 0;
     if (adam) {
-        t = *A.step_next;
         am = A.m[pos];
         av = A.v[pos];
         ap = A.p[k][pos - base[k]];
     }
-    float r[16];
+    constexpr int PW = RW / NW;  // partials per wave
+    // unconditional loads from clamped (valid) addresses, zeroed after: a load under a per-slab
+    // branch is issued alone (the compiler cannot batch loads across the branches)
+    const bool okp = pos <= P_N;
+    const int pc = okp ? pos : P_N;
+    float r[PW][16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int g = wave + RW * u;
-        r[u] = (pos <= P_N && g < A.nslab) ? A.slab[(int64_t)g * SLAB + pos] : 0.f;
+    for (int i = 0; i < PW; ++i)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int g = wave + NW * i + RW * u;
+            const bool ok = okp && g < A.nslab;
+            const int64_t e = (int64_t)(g < A.nslab ? g : 0) * SLAB + pc;
+            float x;
+            if constexpr (COH)
+                x = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  slab_rsrc(A.slab), (uint32_t)(e * 4), 0u, AUX_SC1));
+            else
+                x = A.slab[e];
+            r[i][u] = ok ? x : 0.f;
+        }
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+        float v = r[i][0];
+#pragma unroll
+        for (int u = 1; u < 16; ++u) v += r[i][u];
+        part[wave + NW * i][lane] = v;
     }
-    float v = r[0];
-#pragma unroll
-    for (int u = 1; u < 16; ++u) v += r[u];
-    part[wave][lane] = v;
     __syncthreads();
     if (wave == 0 && pos <= P_N) {
         float sum = part[0][lane];
 #pragma unroll
-        for (int k = 1; k < RW; ++k) sum += part[k][lane];
+        for (int k2 = 1; k2 < RW; ++k2) sum += part[k2][lane];
         if (pos == P_N) {
             if (A.loss) *A.loss = sum;
         } else {
@@ -556,7 +607,76 @@ __global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
             }
         }
     }
+}
+
+constexpr int RCHUNKS = (P_N + 64) / 64;  // 64-position chunks of the slab (loss included)
+
+__global__ __launch_bounds__(64 * RW) void k_mlp_reduce(ReduceArgs A) {
+    __shared__ float part[RW][64];
+    reduce_positions<RW, false>(A, blockIdx.x, A.adam ? *A.step_next : 0ull, part);
     if (A.step && blockIdx.x == 0 && threadIdx.x == 0) *A.step = *A.step_next;
+}
+
+// The whole dense-64 update in ONE launch: every workgroup runs its tiles and writes its slab
+// (k_mlp_update's work) with agent-scope stores (through the XCD's L2 to the coherent level, no
+// L2 write-back needed), waits for them and counts its arrival; the last min(RCHUNKS, grid)
+// workgroups to arrive become the reducers -- each waits until every workgroup has arrived, then
+// sums its 64-position chunks with agent-scope loads exactly as k_mlp_reduce does and applies
+// Adam with t = *step + 1 (read by every workgroup before it counts itself; reducer 0 commits the
+// counter last).  The workgroups a reducer waits for have all started or are next in line for the
+// CUs the early finishers freed, so the wait always ends; it is capped anyway (an error count in
+// the workspace; the tests check it stays 0).  The last reducer to finish returns both counters
+// to 0 for the next launch (the workspace must be zeroed before its first use).  Replaces the
+// k_mlp_update -> k_mlp_reduce kernel boundary.
+struct Update1Args {
+    UpdateArgs U;
+    ReduceArgs R;
+    unsigned int* arrive;  // [0] arrivals, [1] reducers done, [2] error count
+};
+
+__global__ __launch_bounds__(NT) void k_mlp_update1(Update1Args A) {
+    const unsigned long long t_next = *A.U.step + 1ull;
+    update_tiles<true>(A.U);
+    __shared__ unsigned int s_arrival;
+    __shared__ float part[RW][64];
+    const unsigned grid = gridDim.x;
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's slab stores are complete
+    __syncthreads();
+    if (threadIdx.x == 0)
+        s_arrival = __hip_atomic_fetch_add(&A.arrive[0], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const unsigned a = s_arrival;
+    const unsigned nred = grid < (unsigned)RCHUNKS ? grid : (unsigned)RCHUNKS;
+    if (a >= grid) {  // a workspace that was not zeroed: nothing here can be trusted
+        if (threadIdx.x == 0) atomicAdd(&A.arrive[2], 1u);
+        return;
+    }
+    if (a < grid - nred) return;
+    const unsigned me = a - (grid - nred);  // this reducer's index
+    if (threadIdx.x == 0) {
+        unsigned it = 0;
+        while (__hip_atomic_load(&A.arrive[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < grid) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++it == (1u << 24)) {
+                atomicAdd(&A.arrive[2], 1u);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    for (unsigned c = me; c < (unsigned)RCHUNKS; c += nred) {
+        reduce_positions<NT / 64, true>(A.R, (int)c, t_next, part);
+        __syncthreads();  // part is reused by the next chunk
+    }
+    if (threadIdx.x == 0) {
+        if (me == 0 && A.R.step) *A.R.step = t_next;
+        if (__hip_atomic_fetch_add(&A.arrive[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            nred - 1) {
+            __hip_atomic_store(&A.arrive[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&A.arrive[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 }
 
 }  // namespace
@@ -649,12 +769,26 @@ extern "C" G2048_API int g2048_dense64_train_grad(const g2048_dense64_params* p,
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
 }
 
+// workspace: slabs | u64 step_next | u32 arrivals, reducers done, errors, pad (k_mlp_update1)
+constexpr int WS_TAIL = 2 + 4;
+
 extern "C" G2048_API int64_t g2048_dense64_update_workspace(int64_t batch) {
     const int64_t ntiles = (batch + S_UPD - 1) / S_UPD;
 #ifdef G2048_MLP_PHASE
-    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + 2 + 2 * 8 * MAX_SLABS;
+    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + WS_TAIL + 2 * 8 * MAX_SLABS;
 #endif
-    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + 2;  // + the u64 step_next word
+    return (ntiles < MAX_SLABS ? ntiles : MAX_SLABS) * SLAB + WS_TAIL;
+}
+
+// G2048_DENSE64_ONE_LAUNCH=1 selects the one-launch update (k_mlp_update1; read per call, so the
+// tests compare the two forms bitwise in one process).  Measured and not the default
+// (tools/dense64_onelaunch_ab.py, profiles/r06/dense64_onelaunch_ab.txt): 23.7 us per update against
+// 19.4 us for the two launches -- a workgroup's wait for its slab stores to be acknowledged at
+// the coherent level plus the arrival atomic cost ~5.8 us, more than the kernel boundary it
+// replaces.
+static bool dense64_one_launch() {
+    const char* e = getenv("G2048_DENSE64_ONE_LAUNCH");
+    return e && e[0] == '1';
 }
 
 extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online,
@@ -701,12 +835,9 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
     U.slab = workspace;
     U.step_next = step_next;
 #ifdef G2048_MLP_PHASE
-    U.phase = reinterpret_cast<long long*>(step_next + 1);
+    U.phase = reinterpret_cast<long long*>(workspace + (int64_t)grid * SLAB + WS_TAIL);
 #endif
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    hipLaunchKernelGGL(k_mlp_update, dim3(grid), dim3(NT), 0, st, U);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_mlp_update: %s", hipGetErrorString(e));
     ReduceArgs R{};
     R.slab = workspace;
     R.nslab = grid;
@@ -730,7 +861,20 @@ extern "C" G2048_API int g2048_dense64_update(const g2048_dense64_params* online
     R.b1 = beta1;
     R.b2 = beta2;
     R.eps = eps;
-    hipLaunchKernelGGL(k_mlp_reduce, dim3((P_N + 64) / 64), dim3(64 * RW), 0, st, R);
+    if (dense64_one_launch()) {
+        Update1Args A1;
+        A1.U = U;
+        A1.R = R;
+        A1.arrive = reinterpret_cast<unsigned int*>(step_next + 1);
+        hipLaunchKernelGGL(k_mlp_update1, dim3(grid), dim3(NT), 0, st, A1);
+        const hipError_t e = hipGetLastError();
+        return e == hipSuccess ? G2048_OK
+                               : g2048_fail(G2048_EHIP, "k_mlp_update1: %s", hipGetErrorString(e));
+    }
+    hipLaunchKernelGGL(k_mlp_update, dim3(grid), dim3(NT), 0, st, U);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return g2048_fail(G2048_EHIP, "k_mlp_update: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(k_mlp_reduce, dim3(RCHUNKS), dim3(64 * RW), 0, st, R);
     e = hipGetLastError();
     return e == hipSuccess ? G2048_OK : g2048_fail(G2048_EHIP, "k_mlp_reduce: %s", hipGetErrorString(e));
 }

@@ -387,7 +387,13 @@ class Dense64Update64:
         self.adam = adam
         dev = next(model.parameters()).device
         n = N.load().g2048_dense64_update_f64_workspace(self.batch)
-        self.workspace = torch.empty(n, dtype=torch.float64, device=dev)
+        # zeroed: its tail holds the one-launch update's arrival counters (include/g2048.h)
+        self.workspace = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._grid = min((self.batch + 63) // 64, 256)
+
+    def sync_errors(self) -> int:
+        """As Dense64Update.sync_errors (host sync)."""
+        return int(self.workspace[self._grid * 1352 + 1:].view(torch.int32)[2])
 
     def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
                  idx_in=None, grad_out=None, loss_out=None):
@@ -543,7 +549,15 @@ class Dense64Update:
         self.adam = adam
         dev = next(model.parameters()).device
         n = N.load().g2048_dense64_update_workspace(self.batch)
-        self.workspace = torch.empty(n, dtype=torch.float32, device=dev)
+        # zeroed: its tail holds the one-launch update's arrival counters (include/g2048.h)
+        self.workspace = torch.zeros(n, dtype=torch.float32, device=dev)
+        self._grid = min((self.batch + 31) // 32, 256)
+
+    def sync_errors(self) -> int:
+        """Capped waits of the one-launch update's reducers, or launches on a workspace that was
+        not zeroed (the tail's error word; host sync).  0 on a healthy device."""
+        tail = self.workspace[self._grid * 1352 + 2:].view(torch.int32)
+        return int(tail[2])
 
     def __call__(self, replay, idx_out, y_out, step_dev, gamma=0.8, double_dqn=True, seed=0,
                  idx_in=None, grad_out=None, loss_out=None):

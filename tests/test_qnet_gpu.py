@@ -592,3 +592,98 @@ def test_f64_trainer_graphed_equals_eager(G, net):
     assert torch.equal(outs[0][0], outs[1][0])
     assert outs[0][1] == outs[1][1]
     assert torch.equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("B", [45, 1000, 8192, 20000])
+@pytest.mark.parametrize("with_adam", [True, False])
+def test_dense64_one_launch_equals_two_launches(G, B, with_adam, monkeypatch):
+    """g2048_dense64_update as ONE launch (G2048_DENSE64_ONE_LAUNCH=1: the last
+    workgroups to finish their tiles reduce the slabs, k_mlp_update1) against the two-launch form
+    (k_mlp_update ->
+    k_mlp_reduce, the default): bitwise the same rows, targets, gradient, loss,
+    parameters, Adam moments, target sync and update counter over 5 updates, at grids of 2 (each
+    reducer takes several 64-position chunks), 32, 256 and 256 x 3 tiles.  The arrival counters
+    are back at zero after every launch and no reducer's wait was capped."""
+    import copy
+
+    from g2048.nets import det_init, make_net
+    from g2048.optim import FusedAdam
+    from g2048.qnet import Dense64Update
+
+    rb = _filled_ring(G, 3 + B % 13)
+    on = det_init(make_net("dense64", torch.float32, DEV), 0.4)
+    tg0 = det_init(make_net("dense64", torch.float32, DEV), 0.9)
+    runs = []
+    for two in (False, True):
+        if two:
+            monkeypatch.delenv("G2048_DENSE64_ONE_LAUNCH", raising=False)
+        else:
+            monkeypatch.setenv("G2048_DENSE64_ONE_LAUNCH", "1")
+        m, tg = copy.deepcopy(on), copy.deepcopy(tg0)
+        adam = FusedAdam(list(m.parameters()), lr=1e-2)
+        adam.attach_target(list(tg.parameters()), 2)
+        upd = Dense64Update(m, tg, B, adam=adam if with_adam else None)
+        step = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+        got = []
+        for _ in range(5):
+            io = torch.empty(B, dtype=torch.int64, device=DEV)
+            y = torch.empty(B, device=DEV)
+            g = torch.full((1348,), float("nan"), device=DEV)
+            loss = torch.zeros((), device=DEV)
+            upd(rb, io, y, step, 0.8, True, 0x1234, None, grad_out=g, loss_out=loss)
+            if not with_adam:
+                adam.step(g, step)
+            got += [io, y, g, loss]
+        torch.cuda.synchronize()
+        tail = upd.workspace[upd._grid * 1352 + 2:].view(torch.int32)[:3].cpu()
+        assert upd.sync_errors() == 0
+        assert tail.tolist() == [0, 0, 0], tail
+        got += [torch.cat([p.reshape(-1) for p in m.parameters()]),
+                torch.cat([p.reshape(-1) for p in tg.parameters()]),
+                adam.exp_avg.clone(), adam.exp_avg_sq.clone(), step.clone()]
+        runs.append(got)
+    assert int(runs[0][-1]) == 10
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [45, 1000, 8192, 20000])
+def test_dense64_f64_one_launch_equals_two_launches(G, B, monkeypatch):
+    """The float64 dense-64 update in one launch (G2048_DENSE64_ONE_LAUNCH=1,
+    k_dense64_update1_f64) against its two launches: bitwise over 5 Adam-folded updates with target syncs, grids of 1 .. 256 x 2 tiles."""
+    import copy
+
+    from g2048.nets import det_init, make_net
+    from g2048.qnet import Adam64, Dense64Update64
+
+    rb = _filled_ring(G, 7 + B % 11)
+    on = det_init(make_net("dense64", torch.float64, DEV), 0.4)
+    tg0 = det_init(make_net("dense64", torch.float64, DEV), 0.9)
+    runs = []
+    for two in (False, True):
+        if two:
+            monkeypatch.delenv("G2048_DENSE64_ONE_LAUNCH", raising=False)
+        else:
+            monkeypatch.setenv("G2048_DENSE64_ONE_LAUNCH", "1")
+        m, tg = copy.deepcopy(on), copy.deepcopy(tg0)
+        adam = Adam64(list(m.parameters()), lr=1e-2)
+        adam.attach_target(list(tg.parameters()), 2)
+        upd = Dense64Update64(m, tg, B, adam=adam)
+        step = torch.full((1,), 5, dtype=torch.int64, device=DEV)
+        got = []
+        for _ in range(5):
+            io = torch.empty(B, dtype=torch.int64, device=DEV)
+            y = torch.empty(B, dtype=torch.float64, device=DEV)
+            loss = torch.zeros((), dtype=torch.float64, device=DEV)
+            upd(rb, io, y, step, 0.8, True, 0x1234, None, loss_out=loss)
+            got += [io, y, loss]
+        torch.cuda.synchronize()
+        assert upd.sync_errors() == 0
+        assert upd.workspace[upd._grid * 1352 + 1:].view(torch.int32)[:3].tolist() == [0, 0, 0]
+        got += [torch.cat([p.reshape(-1) for p in m.parameters()]),
+                torch.cat([p.reshape(-1) for p in tg.parameters()]),
+                adam.exp_avg.clone(), adam.exp_avg_sq.clone(), step.clone()]
+        runs.append(got)
+    assert int(runs[0][-1]) == 10
+    for a, b in zip(*runs):
+        assert torch.equal(a, b)

@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes over tools/prof_learner.py (tools/gpu_pmc_learner.sh) into
+profiles/<round>/pmc_learner.json: per learner kernel and workload (net, dtype, batch), per launch
+
+  fetch / write bytes   FETCH_SIZE x 2 (gfx950: FETCH_SIZE reads 1/2 of a wide coalesced read
+                        stream, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, in bytes;
+                        memory side of L2 (Infinity-Cache hits included)
+  mfma_flop             executed matrix FLOPs: SQ_INSTS_VALU_MFMA_MOPS_F64 / _F32 x 512
+                        (the counters count 512-FLOP units)
+  valu / mfma / lds     instructions per wave (SQ_INSTS_VALU includes the MFMAs on gfx9)
+  mfma_busy_frac        SQ_VALU_MFMA_BUSY_CYCLES / (SQ_BUSY_CU_CYCLES x 4 SIMDs) when present
+
+Usage: pmc_learner.py <out.json> <pass-dir>:<workload-tag> [...]
+       (the tag is "<net>.<dtype>@<batch>", e.g. conv.fp64@8192)."""
+import csv
+import glob
+import json
+import os
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+KERNELS = {"k_conv64_train_a8", "k_conv64_train_a", "k_conv64_train_b", "k_conv64_reduce", "k_pack",
+           "k_conv_targets_persist", "k_conv_train_fwd", "k_conv_train_bwd", "k_reduce_pre",
+           "k_reduce_slabs", "k_dense_sample", "k_dense_forward", "k_dense_rows", "k_dense_wgrad",
+           "k_dense_reduce", "k_mlp_update1", "k_mlp_update", "k_mlp_reduce",
+           "k_dense64_update1_f64", "k_dense64_update_f64", "k_dense64_reduce_f64", "k_adam64",
+           "k_adam"}
+
+
+def kernel_of(name: str):
+    """The kernel's own identifier in a rocprofv3 name such as
+    "(anonymous namespace)::k_dense_forward<double>(FwdArgs<double>)"."""
+    for tok in re.findall(r"\bk_[A-Za-z0-9_]+", name):
+        if tok in KERNELS:
+            return tok
+    return None
+
+
+def load(specs):
+    vals = defaultdict(lambda: defaultdict(list))
+    for spec in specs:
+        d, _, tag = spec.partition(":")
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            per = defaultdict(float)
+            meta = {}
+            for r in csv.DictReader(open(f)):
+                k = kernel_of(r["Kernel_Name"])
+                if k is None:
+                    continue
+                did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                per[(did, r["Counter_Name"])] += float(r["Counter_Value"])
+                meta[did] = f"{k}@{tag}"
+            for (did, cn), v in per.items():
+                vals[meta[did]][cn].append(v)
+    return vals
+
+
+def main(out_path, *specs):
+    vals = load(specs)
+    res = {"_provenance": "rocprofv3 --pmc passes (tools/gpu_pmc_learner.sh), one counter group "
+                          "per run, --kernel-trace only; medians over the dispatches"}
+    for key in sorted(vals):
+        c = {cn: statistics.median(v) for cn, v in vals[key].items()}
+        rec = {"dispatches": max(len(v) for v in vals[key].values())}
+        if "FETCH_SIZE" in c:
+            rec["fetch_bytes"] = 2 * c["FETCH_SIZE"] * 1024
+        if "WRITE_SIZE" in c:
+            rec["write_bytes"] = c["WRITE_SIZE"] * 1024
+        if "fetch_bytes" in rec and "write_bytes" in rec:
+            rec["hbm_bytes_per_launch"] = rec["fetch_bytes"] + rec["write_bytes"]
+        mops = c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) + c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
+        if mops:
+            rec["mfma_flop"] = mops * 512
+        waves = c.get("SQ_WAVES", 0.0)
+        if waves:
+            for cn, name in (("SQ_INSTS_VALU", "valu_insts_per_wave"),
+                             ("SQ_INSTS_MFMA", "mfma_insts_per_wave"),
+                             ("SQ_INSTS_LDS", "lds_insts_per_wave"),
+                             ("SQ_INSTS_SALU", "salu_insts_per_wave")):
+                if cn in c:
+                    rec[name] = c[cn] / waves
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in c and c.get("SQ_BUSY_CU_CYCLES"):
+            rec["mfma_busy_frac"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * c["SQ_BUSY_CU_CYCLES"])
+        rec["counters"] = c
+        res[key] = rec
+    os.makedirs(os.path.dirname(out_path) or ".", exist_ok=True)
+    json.dump(res, open(out_path, "w"), indent=1)
+    print(json.dumps({k: {kk: vv for kk, vv in v.items() if kk != "counters"}
+                      for k, v in res.items() if k[0] != "_"}, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], *sys.argv[2:])
