@@ -430,7 +430,10 @@ G2048_API int g2048_dense64_update_f64(const g2048_dense64_params_f64* online,
  * target net on a sync), so the caller packs them with g2048_convnet_pack_f64 once after
  * allocating the workspace and again after changing either net's weights any other way (ABI v4:
  * an Adam-folded update on a workspace that was never packed for these two nets returns
- * G2048_EINVAL; the library remembers which workspaces it packed, host-side).  A
+ * G2048_EINVAL; the library remembers which workspaces it packed, host-side, by the workspace
+ * and weight ADDRESSES -- a best-effort guard: a workspace freed and reallocated at the same
+ * address for the same nets passes it without holding packed operands, so a caller that
+ * reallocates a workspace packs it again, as after any other change of the weights).  A
  * gradient-only update (no Adam state: a data-parallel learner applies Adam after the
  * all-reduce) packs at its start. */
 typedef struct {

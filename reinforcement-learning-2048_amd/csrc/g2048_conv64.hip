@@ -1607,7 +1607,10 @@ static bool params_ok(const g2048_convnet_params_f64* n) {
 // Update workspaces whose head g2048_convnet_pack_f64 has filled, with the conv2 / fc1 weight
 // pointers of the two nets it packed (ABI v4): an Adam-folded update reads the packed operands and
 // refuses a workspace that was never packed for its nets instead of training on uninitialised
-// memory.  Host-side only, so the check is graph-capture safe and costs no launch.
+// memory.  Host-side only, so the check is graph-capture safe and costs no launch.  Keyed by
+// addresses, so best-effort (include/g2048.h): a workspace reallocated at a packed one's address
+// for the same nets passes; the Python side (qnet.ConvUpdate64) allocates its workspace once per
+// learner and packs it at construction.
 namespace {
 struct PackKey {
     const double *w2_on, *f1_on, *w2_tg, *f1_tg;

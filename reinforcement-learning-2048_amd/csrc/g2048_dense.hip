@@ -174,20 +174,26 @@ __device__ __forceinline__ void layer(const T* in, T* out, const T* __restrict__
     __syncthreads();
 }
 
-// The tile's TB rows (in S.x) through the net; Q of row b -> q[qrow[b] * 4 + a] for b < nb.
-template <typename T, int TB>
-__device__ __forceinline__ void forward_tile(Smem<T, TB>& S, const DenseNet<T>& P, T* q, int nb,
+// The tile's TB rows (in x, row stride SX) through the net (activations in h, row stride SH);
+// Q of row b -> q[qrow[b] * 4 + a] for b < nb.  A row's Q does not depend on TB (every output
+// element sums its k in one fixed order), so a 16-row tile run in a 32-row tile's buffers
+// (k_dense_forward's remainder tiles) gives the rows the same bits.
+// TBL: the tile size whose thread layout the last (VALU) layer uses -- a 16-row remainder tile
+// in a 32-row kernel keeps the 32-row tile's split of the k-sum (PARTS), so its rows' Q are
+// bitwise those of a full tile.
+template <typename T, int TB, int TBL = TB>
+__device__ __forceinline__ void forward_tile(T* x, T* h, const DenseNet<T>& P, T* q, int nb,
                                              const int32_t* qrow) {
     constexpr int SX = stride_of<T>(16), SH = stride_of<T>(H1);
-    __syncthreads();  // S.x written
-    layer<T, 16, H1, SX, SH, false, TB>(S.x, S.h, P.w1, P.b1);
-    layer<T, H1, H2, SH, SH, true, TB>(S.h, S.h, P.w2, P.b2);
-    layer<T, H2, H3, SH, SH, true, TB>(S.h, S.h, P.w3, P.b3);
+    __syncthreads();  // x written
+    layer<T, 16, H1, SX, SH, false, TB>(x, h, P.w1, P.b1);
+    layer<T, H1, H2, SH, SH, true, TB>(h, h, P.w2, P.b2);
+    layer<T, H2, H3, SH, SH, true, TB>(h, h, P.w3, P.b3);
     // Linear(256, 4) on VALU: thread (row b, action a, part p) sums NP consecutive k in two
     // chains; the parts are combined in a fixed order through lane shuffles
-    constexpr int PARTS = NT / (TB * 4), NP = H3 / PARTS;
+    constexpr int PARTS = NT / (TBL * 4), NP = H3 / PARTS;
     const int t = threadIdx.x, part = t % PARTS, a = (t / PARTS) & 3, b = t / (4 * PARTS);
-    const T* hr = S.h + b * SH + NP * part;
+    const T* hr = h + b * SH + NP * part;
     const T* wr = P.w4 + a * H3 + NP * part;
     T e = T(0), o = T(0);
 #pragma unroll 8
@@ -199,7 +205,7 @@ __device__ __forceinline__ void forward_tile(Smem<T, TB>& S, const DenseNet<T>& 
 #pragma unroll
     for (int m = 1; m < PARTS; m *= 2) v = v + __shfl_xor(v, m);
     if (part == 0 && b < nb) q[(int64_t)qrow[b] * 4 + a] = v + P.b4[a];
-    __syncthreads();  // S.h / S.x free for the next tile
+    __syncthreads();  // h / x free for the next tile
 }
 
 template <typename T>
@@ -282,7 +288,16 @@ __global__ __launch_bounds__(NT) void k_dense_forward(FwdArgs<T> A) {
                 put_row(S.x + t * stride_of<T>(16), v);
                 qrow[t] = row;
             }
-            forward_tile<T, TB>(S, net, q, nb, qrow);
+            // a remainder of <= 16 rows in a 32-row kernel runs as a 16-row tile: half the
+            // MFMAs for the same weight stream (the update's target-side forwards at batches
+            // whose 32-row tiles would spill into a partial second round, e.g. B = 5000)
+            if constexpr (TB == 32) {
+                if (nb <= 16) {
+                    forward_tile<T, 16, 32>(S.x, S.h, net, q, nb, qrow);
+                    continue;
+                }
+            }
+            forward_tile<T, TB>(S.x, S.h, net, q, nb, qrow);
         }
         // carry the remainder (< TB rows) to the front of the queue
         const int rem = qn - nt * TB;
@@ -960,8 +975,20 @@ int update_launch(const g2048_densenet_params* on, const g2048_densenet_params* 
             F.net2 = net_of<T>(tg);
             F.q2 = q2tg;
             const int64_t ft = (batch + TBM - 1) / TBM;
-            const int g1 = (int)(ft < MAX_WG ? ft : MAX_WG);
+            int g1 = (int)(ft < MAX_WG ? ft : MAX_WG);
             F.chunk = (batch + g1 - 1) / g1;
+            // 2 g1 workgroups of one TBM-row tile each would fill the CUs one and a fraction
+            // times (f64, 4096 < B <= 6144; B = 5000: 314 tiles on 256 CUs, the second round 58
+            // tiles deep): half the CUs per net instead, each on a TBM-row tile plus a <= 16-row
+            // remainder tile (k_dense_forward), one round
+            const char* nos = getenv("G2048_DENSE_FWD_ONE_TILE");  // 1: round 5's layout (A/B)
+            if (TBM == 32 && 2 * ft > MAX_WG && 2 * ft < 2 * MAX_WG && !(nos && nos[0] == '1')) {
+                const int64_t ch = (batch + MAX_WG / 2 - 1) / (MAX_WG / 2);
+                if (ch <= TBM + 16) {
+                    g1 = MAX_WG / 2;
+                    F.chunk = ch;
+                }
+            }
             F.nb1 = g1;
             hipLaunchKernelGGL((k_dense_forward<T, TBM>), dim3(2 * g1), dim3(NT), 0, st, F);
         } else {

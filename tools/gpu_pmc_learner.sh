@@ -2,12 +2,11 @@
 # GPU box: PMC passes over the learner updates (tools/prof_learner.py <net> <dtype> <updates>
 # <batch>), one counter group per rocprofv3 run, kernel-trace only (no sys/runtime trace);
 # summary -> gpurun_out/pmc_learner.json.  Usage: gpu_pmc_learner.sh [workload ...]
-#   workload = net:dtype:batch (default: conv:fp64:8192 conv:fp32:8192 dense:fp64:8192
-#              dense:fp64:5000 dense64:fp32:8192)
+#   workload = net:dtype:batch (default: every learner leg of bench.py)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-WL=${*:-"conv:fp64:8192 conv:fp32:8192 dense:fp64:8192 dense:fp64:5000 dense64:fp32:8192"}
+WL=${*:-"conv:fp64:8192 conv:fp32:8192 dense:fp64:8192 dense:fp32:8192 dense:fp64:5000 dense:fp32:5000 dense64:fp32:8192 dense64:fp64:8192"}
 timeout -s KILL 60 rocprofv3 -L > gpurun_out/pmc_counter_list.txt 2>&1 || true
 have() { grep -qw "$1" gpurun_out/pmc_counter_list.txt; }
 SQ=""
