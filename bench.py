@@ -328,10 +328,10 @@ def settle(replay, ms: float, max_calls: int = 4000) -> float:
 
 
 def capture(fn, n_steps: int):
-    """A hipGraph of n_steps calls of fn.  In a process holding an RCCL group the capture is
-    thread-local: ProcessGroupNCCL's watchdog thread queries events while this thread records
-    (g2048/dist.py: capture_error_mode)."""
-    from g2048.dist import capture_error_mode, quiesce_for_capture
+    """A hipGraph of n_steps calls of fn (g2048/dist.py: graph_capture -- thread-local in a
+    process holding an RCCL group, whose watchdog thread queries events while this thread
+    records; no garbage collection during the capture)."""
+    from g2048.dist import graph_capture, quiesce_for_capture
 
     quiesce_for_capture()
     g = torch.cuda.CUDAGraph()
@@ -340,7 +340,7 @@ def capture(fn, n_steps: int):
     with torch.cuda.stream(s):
         fn()  # one eager call on the side stream before capture
     torch.cuda.current_stream().wait_stream(s)
-    with torch.cuda.graph(g, capture_error_mode=capture_error_mode()):
+    with graph_capture(g):
         for _ in range(n_steps):
             fn()
     return g

@@ -9,6 +9,8 @@ Backend-agnostic: the CPU tests run it over gloo.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 
 import torch
@@ -106,6 +108,26 @@ def capture_error_mode(group=None) -> str:
     every capture in a process that holds an NCCL group is thread-local; elsewhere torch's
     default "global" (which also catches an unsafe call from a helper thread of ours)."""
     return "thread_local" if (captures_collectives(group) or nccl_group_exists()) else "global"
+
+
+@contextlib.contextmanager
+def graph_capture(graph: "torch.cuda.CUDAGraph", group=None, **kw):
+    """torch.cuda.graph(graph) for every capture of this package: the capture-error mode of
+    capture_error_mode(), and no garbage collection while it records.  A collection that runs in
+    the middle of a capture can free an OLD graph (an earlier learner's, a bench leg's) whose
+    destructor calls hipGraphExecDestroy -- an unsafe call in any capture mode on the capturing
+    thread, which invalidates the capture ("operation failed due to a previous error during
+    capture"; seen once in the round-6 driver command's conv leg).  So: collect first, then keep
+    the collector off until the capture ends."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(graph, capture_error_mode=capture_error_mode(group), **kw):
+            yield graph
+    finally:
+        if was:
+            gc.enable()
 
 
 def quiesce_for_capture(group=None) -> None:

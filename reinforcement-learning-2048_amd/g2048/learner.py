@@ -19,7 +19,7 @@ import copy
 import torch
 
 from . import dqn_lib
-from .dist import (FlatGradBucket, broadcast_params, capture_error_mode, captures_collectives,
+from .dist import (FlatGradBucket, broadcast_params, captures_collectives, graph_capture,
                    quiesce_for_capture, world_size)
 from .env import ReplayBuffer, VecEnv2048
 from .nets import NETS, make_net
@@ -248,9 +248,9 @@ class DQNLearner:
                 self._allreduce()
                 self._apply()
         torch.cuda.current_stream(self.device).wait_stream(side)
-        quiesce_for_capture(self.pg)  # the warm-up's eager collectives retired first
+        quiesce_for_capture(self.pg)  # the side-stream warm-up (and its collectives) done first
         g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, capture_error_mode=capture_mode(self)):
+        with graph_capture(g1, self.pg):
             self._compute_grads()
             if not self.dp or self.capture_collective:  # the whole update in one graph
                 self._allreduce()
@@ -258,7 +258,7 @@ class DQNLearner:
         g2 = None
         if self.dp and not self.capture_collective:  # gloo: the collective between two replays
             g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g2, capture_error_mode=capture_mode(self)):
+            with graph_capture(g2, self.pg):
                 self._apply()
         self._graphs = (g1, g2)
         with torch.no_grad():  # restore in place (the graphs hold these addresses)
@@ -503,7 +503,7 @@ class Trainer:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
             quiesce_for_capture(L.pg)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, capture_error_mode=capture_mode(L)):
+            with graph_capture(g, L.pg):
                 self._rollout_step()
                 for _ in range(ups):
                     L._compute_grads()
@@ -530,10 +530,10 @@ class Trainer:
                 L._capture()  # autograd warm-up on a side stream (leaves no trace)
             quiesce_for_capture(L.pg)
             ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(ga, capture_error_mode=capture_mode(L)):
+            with graph_capture(ga, L.pg):
                 self._rollout_step()
                 L._compute_grads()
-            with torch.cuda.graph(gb, capture_error_mode=capture_mode(L)):
+            with graph_capture(gb, L.pg):
                 L._apply()
             self._loop_graph = (ga, gb)
         ga, gb = self._loop_graph
@@ -695,15 +695,6 @@ class Trainer:
         if self.track:
             self.h_t0 = self.steps
             self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
-
-
-def capture_mode(learner) -> str:
-    """torch.cuda.graph's capture_error_mode for every graph of this learner (update, loop
-    iteration, the gloo form's two graphs): "thread_local" whenever the process holds an RCCL
-    group -- ProcessGroupNCCL's watchdog thread queries events while the capturing thread records,
-    which a global-mode capture treats as an unsafe call (g2048/dist.py: capture_error_mode) --
-    else torch's default "global"."""
-    return capture_error_mode(learner.pg)
 
 
 def _flat_adam_state(per_param: list, params) -> dict:
