@@ -628,6 +628,10 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
         CPHASE(10);
         // dWf1 += dZ3^T H2: wave w -> rows j = 16w .., 16 column blocks, K = 16 boards.  A
         // step's 17 LDS operands are read together (one wait per 16 MFMAs, not one per two)
+        // (G2048_TIMING_NO_WGRAD: a timing-only build without the weight-gradient MFMAs and
+        // slabs of conv2 / fc1, tools/conv64_wgrad_bound.sh -- the bound on what moving them
+        // to K = B GEMMs can save; its results are wrong by construction)
+#ifndef G2048_TIMING_NO_WGRAD
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             double op[17];
@@ -639,6 +643,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
             for (int cb = 0; cb < 16; ++cb) gf1[cb] = mfma(op[0], op[1 + cb], gf1[cb]);
             __builtin_amdgcn_sched_barrier(0);
         }
+#endif
         CPHASE(11);
         // dH2 = dZ3 Wf1 (masked by relu'(H2)) -> dZ2: wave w -> columns 64w .. 64w+63
         {
@@ -681,10 +686,12 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     // slab: fc1.weight [64][256], fc1.bias, fc2.weight [4][64], fc2.bias, loss.  (Issued inside
     // the last tile, before dH2, these stores made the kernel spill: 312 B of scratch.)
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#ifndef G2048_TIMING_NO_WGRAD
 #pragma unroll
     for (int cb = 0; cb < 16; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sl[P_F1 + (16 * w + 4 * r + lk) * 256 + 16 * cb + lr] = gf1[cb][r];
+#endif
     if (t < 64) sl[P_FB1 + t] = gfb1;
     sl[P_F2 + w * 64 + l] = gf2;
     if (l == 0) sl[P_FB2 + w] = gfb2;
@@ -1220,6 +1227,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         // slab batches: four per tile, all inside dW2, whose operands all come from LDS -- vmcnt
         // counts in order, so a batch in flight across dV's B-fragment loads would make every
         // wait for them wait for the slab loads too
+#ifndef G2048_TIMING_NO_WGRAD
 #pragma unroll 4
         for (int s = 0; s < 16; ++s) {
             if (A.pre && (s & 3) == 0) sh.issue<0>();
@@ -1231,6 +1239,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             __builtin_amdgcn_sched_barrier(0);
             if (A.pre && (s & 3) == 3) sh.consume<0>();
         }
+#endif
         CPHASE(16);
         // dV_xi: wave w -> channels c = 16w .., K = 64 o in 16 k-steps, nine chains; B two
         // steps ahead
@@ -1307,6 +1316,9 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         // of one (o, c) are 32 contiguous bytes (torch order o, c, tap), two 16-byte stores, so
         // 16 lanes write 512 B in a row
         double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
+#ifdef G2048_TIMING_NO_WGRAD
+        if (A.batch < 0)  // never: the timing-only build stores no conv2.weight terms
+#endif
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
@@ -1318,7 +1330,11 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
                                     make_double2(gw2[8 + cb][r], gw2[12 + cb][r]));
             }
     }
+#ifndef G2048_TIMING_NO_WGRAD
     if (A.pre) {  // whatever the tiles did not cover
+#else
+    if (A.pre && A.batch < 0) {  // the timing-only build sums no fc slab terms
+#endif
         while (sh.pending()) {
             sh.issue<0>();
             sh.consume<0>();
@@ -1416,7 +1432,13 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
                            ? *reinterpret_cast<const double2*>(A.pre + pos)
                            : make_double2(0.0, 0.0);
     double2 r = make_double2(0.0, 0.0);
+#ifdef G2048_TIMING_NO_WGRAD
+    // the timing-only build reads no conv2.weight slab terms (a K = B GEMM leaves a handful of
+    // partials for them, not 256 slabs)
+    if (pos <= P_N && !summed && !(pos >= P_W2 && pos < P_B2)) {
+#else
     if (pos <= P_N && !summed) {
+#endif
         double2 v[MAX_WG / RW];
         // (wave 0: Adam's step scalars are formed while its slab loads are in flight)
 #pragma unroll
