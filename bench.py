@@ -47,7 +47,7 @@ ROLLOUT_BYTES = 38
 #   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
 STEP_BYTES = 37
 STEP_BYTES_BOOKKEEPING = 54
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
 # the learner kernels' PMC passes (tools/gpu_pmc_learner.sh -> tools/pmc_learner.py)
 PMC_LEARNER_FILE = os.path.join(ROOT, "profiles", "r06", "pmc_learner.json")
