@@ -105,15 +105,16 @@ def learner_roofline(net: str, dtype: str, batch: int, update_s: float, params: 
                      algo_flop: float, peak_tf: float) -> dict:
     """The roofline object of one learner leg: bound "mfma" (the update is GEMM-shaped work on
     f32 / f64 MFMA); achieved = the ALGORITHMIC FLOPs (5 forward-equivalents of the direct net,
-    SURVEY 8d) over the event-timed update; executed_flop = the matrix FLOPs the kernels really
-    issue (Winograd conv2 issues fewer), and traffic = FETCH + WRITE bytes of the update's kernels,
-    both from the committed PMC passes (profiles/r06/pmc_learner.json, a separate rocprofv3 run)."""
+    SURVEY 8d) over the event-timed update; executed_mfma_flop = the matrix FLOPs the kernels
+    really issue (Winograd conv2 issues fewer; 0 for the dense-64 f64 update, which runs on VALU),
+    and traffic = FETCH + WRITE bytes of the update's kernels, both from the committed PMC passes
+    (profiles/r06/pmc_learner.json, a separate rocprofv3 run)."""
     elt = 4 if dtype == "fp32" else 8
     algo_b = learner_algorithmic_bytes(batch, params, elt)
     out = {"bound": "mfma", "achieved": algo_flop / update_s / 1e12, "peak": peak_tf,
            "unit": "TFLOP/s", "frac": algo_flop / update_s / 1e12 / peak_tf,
            "algorithmic_flop": algo_flop, "algorithmic_bytes": algo_b, "update_us": update_s * 1e6,
-           "executed_flop": None, "traffic": None}
+           "executed_mfma_flop": None, "traffic": None}
     try:
         with open(PMC_LEARNER_FILE) as f:
             d = json.load(f)
@@ -129,8 +130,8 @@ def learner_roofline(net: str, dtype: str, batch: int, update_s: float, params: 
                    traffic_per_kernel={k: r["hbm_bytes_per_launch"] for k, r in recs.items()})
     if all("mfma_flop" in r for r in recs.values()):
         ex = sum(r["mfma_flop"] for r in recs.values())
-        out.update(executed_flop=ex, executed_tflops=ex / update_s / 1e12,
-                   executed_frac=ex / update_s / 1e12 / peak_tf)
+        out.update(executed_mfma_flop=ex, executed_mfma_tflops=ex / update_s / 1e12,
+                   executed_mfma_frac=ex / update_s / 1e12 / peak_tf)
     out["traffic_source"] = (f"{os.path.relpath(PMC_LEARNER_FILE, ROOT)} "
                              f"({d.get('_provenance', '')}); kernels {', '.join(recs)}")
     return out

@@ -70,9 +70,9 @@ def main(out_path, *specs):
             rec["write_bytes"] = c["WRITE_SIZE"] * 1024
         if "fetch_bytes" in rec and "write_bytes" in rec:
             rec["hbm_bytes_per_launch"] = rec["fetch_bytes"] + rec["write_bytes"]
-        mops = c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0) + c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
-        if mops:
-            rec["mfma_flop"] = mops * 512
+        if "SQ_INSTS_VALU_MFMA_MOPS_F64" in c or "SQ_INSTS_VALU_MFMA_MOPS_F32" in c:
+            rec["mfma_flop"] = 512 * (c.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)
+                                      + c.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0))
         waves = c.get("SQ_WAVES", 0.0)
         if waves:
             for cn, name in (("SQ_INSTS_VALU", "valu_insts_per_wave"),
