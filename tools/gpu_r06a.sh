@@ -1,6 +1,8 @@
 #!/bin/bash
 # round 6 (a): RCCL capture mode + bench RCCL branch (world-1 group), scaled Adam, round-4 dense
-# resume, one-launch dense-64 update (bitwise vs two launches, A/B timing)
+# resume, one-launch dense-64 update (bitwise vs two launches, A/B timing).  Run while the
+# one-launch form was the default and G2048_DENSE64_TWO_LAUNCH=1 selected the two launches (since
+# reversed: G2048_DENSE64_ONE_LAUNCH=1 selects the one-launch form)
 set -o pipefail
 export PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
