@@ -484,6 +484,8 @@ struct TrainArgs {
     double* dz2;   // [ntiles * TB][256]
     double* slab;  // [grid][SLAB]
     double* pre;   // [SLAB] train A's slab terms summed by train B (null: the reduce sums them)
+    double* h2g;   // [ntiles * TB][256] H2 of Q_online(s) (GEMM weight gradients only)
+    double* dz3g;  // [ntiles * TB][64] dZ3 (GEMM weight gradients only)
 };
 
 // Targets and the graded forward of the same tile in one launch (2 + 3 above): per tile the
@@ -495,6 +497,10 @@ struct FusedArgs {
     TrainArgs A;
 };
 
+// GW: the weight gradients of conv2 / fc1 leave the train launches for k_conv64_wgrad (K = B
+// GEMMs over stored operands): train A stores H2 and dZ3 instead of accumulating dWf1 and writes
+// no fc1.weight slab terms; train B skips dW2 and its conv2.weight slab terms.
+template <bool GW>
 __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     __shared__ Smem M;
     const TgtArgs& T = F.T;
@@ -631,9 +637,28 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
         // (G2048_TIMING_NO_WGRAD: a timing-only build without the weight-gradient MFMAs and
         // slabs of conv2 / fc1, tools/conv64_wgrad_bound.sh -- the bound on what moving them
         // to K = B GEMMs can save; its results are wrong by construction)
+        if constexpr (GW) {
+            // the operands of k_conv64_wgrad's dWf1 = dZ3^T H2: this tile's H2 rows (16 x 256)
+            // and dZ3 rows (16 x 64), batch-indexed, 16-byte stores
+            const int64_t rb0 = b0 * 256;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int e = 2 * (t + NT * k);  // element pair e, e + 1 of the 16 x 256 block
+                const int bq = e >> 8, col = e & 255;
+                *reinterpret_cast<double2*>(A.h2g + rb0 + e) =
+                    make_double2(M.h2[bq * HS + col], M.h2[bq * HS + col + 1]);
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int e = 2 * (t + NT * k);  // of the 16 x 64 block
+                const int bq = e >> 6, col = e & 63;
+                *reinterpret_cast<double2*>(A.dz3g + b0 * 64 + e) =
+                    make_double2(M.h3[bq * H3S + col], M.h3[bq * H3S + col + 1]);
+            }
+        }
 #ifndef G2048_TIMING_NO_WGRAD
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < 4 && !GW; ++s) {
             double op[17];
             op[0] = M.h3[(4 * s + lk) * H3S + 16 * w + lr];
 #pragma unroll
@@ -687,10 +712,13 @@ __global__ __launch_bounds__(NT) void k_conv64_train_a(FusedArgs F) {
     // the last tile, before dH2, these stores made the kernel spill: 312 B of scratch.)
     double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
 #ifndef G2048_TIMING_NO_WGRAD
+    if constexpr (!GW) {
 #pragma unroll
-    for (int cb = 0; cb < 16; ++cb)
+        for (int cb = 0; cb < 16; ++cb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sl[P_F1 + (16 * w + 4 * r + lk) * 256 + 16 * cb + lr] = gf1[cb][r];
+            for (int r = 0; r < 4; ++r)
+                sl[P_F1 + (16 * w + 4 * r + lk) * 256 + 16 * cb + lr] = gf1[cb][r];
+    }
 #endif
     if (t < 64) sl[P_FB1 + t] = gfb1;
     sl[P_F2 + w * 64 + l] = gf2;
@@ -1140,6 +1168,7 @@ struct alignas(16) SmemB {
     SmallW sw;
 };
 
+template <bool GW>
 __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     __shared__ SmemB M;
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -1229,7 +1258,7 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         // wait for them wait for the slab loads too
 #ifndef G2048_TIMING_NO_WGRAD
 #pragma unroll 4
-        for (int s = 0; s < 16; ++s) {
+        for (int s = 0; s < 16 && !GW; ++s) {
             if (A.pre && (s & 3) == 0) sh.issue<0>();
             double op[17];
             lds17(op, s);
@@ -1318,6 +1347,8 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
         double* sl = A.slab + (int64_t)blockIdx.x * SLAB;
 #ifdef G2048_TIMING_NO_WGRAD
         if (A.batch < 0)  // never: the timing-only build stores no conv2.weight terms
+#else
+        if (!GW)  // GW: k_conv64_wgrad computes conv2.weight's gradient
 #endif
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb)
@@ -1378,6 +1409,212 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
     CPHASE_FLUSH();
 }
 
+// ------------------------------------------------------------------ 3'. the weight gradients as K = B GEMMs
+// (GW mode) conv2.weight's and fc1.weight's gradients over the whole minibatch, from operands the
+// train launches left in the workspace instead of per-workgroup slabs:
+//   conv2 directly, one GEMM per tap: dW2[o][c][tap] = sum_{b, p} dY[b][o][p] d[b][pos(p, tap)][c]
+//     (K = 4 B rows (b, p); dY = the stored dZ2, d = conv1's relu output recomputed from the
+//     boards on MFMA, only the four positions the tap reads).  (The Winograd-domain form,
+//     dU_xi = sum_b V_xi^T dM_xi with G^T dU G in the reduce, issues 44 % fewer MFMAs but its
+//     transforms cancel: it missed the reference fixture's 1e-10 on 10 conv2 weights, 4.7e-10
+//     absolute; not kept);
+//   fc1: dWf1[j][k] = sum_b dZ3[b][j] H2[b][k] (stored by train A), four 64-column blocks.
+// Eight output blocks of 64 x 64, each split over the batch (the four conv2 taps into S2 ranges,
+// the fc1 blocks into S1 = S2 / 4: equal MFMA work per workgroup): workgroup (unit, split) runs one
+// block over one range in stages of 64 K-rows (16 samples x 4 positions, or 64 samples), operands
+// fetched into registers a stage ahead and staged in LDS; eight waves, two per SIMD (one's MFMAs
+// cover the other's LDS reads): wave w owns rows 16 (w & 3) .. + 15, all 64 columns, over half
+// of every stage's K (8 k-steps x 4 MFMAs); the halves are added through LDS and the workgroup
+// writes its 64 x 64 partial, and the reduce sums a block's partials in split order.  Every sum has a fixed order: bitwise run to run.
+constexpr int WKR = 64;       // K-rows per stage
+constexpr int WAS = 66;       // LDS row stride (doubles) of the staged operands
+constexpr int WG_MAX_SPLIT = 48;
+constexpr int WG_BLOCK = 4096;  // doubles per 64 x 64 partial
+
+struct WgSplit {
+    int s1, s2;  // splits of an fc1 block / of a conv2 tap
+};
+WgSplit wgrad_splits(int64_t batch) {
+    const int64_t st_f = (batch + 63) / 64, st_w = (batch + 15) / 16;  // stages of each unit
+    const int s1 = (int)(st_f < 12 ? st_f : 12);
+    const int64_t s2 = 4 * (int64_t)s1 < st_w ? 4 * s1 : st_w;
+    return WgSplit{s1, (int)s2};
+}
+int64_t wgrad_part_doubles(int64_t batch) {
+    const WgSplit sp = wgrad_splits(batch);
+    return (int64_t)4 * (sp.s1 + sp.s2) * WG_BLOCK;
+}
+
+struct WgArgs {
+    const double *w1, *b1;  // the online net's conv1 (the weights the train launches used)
+    const uint4* s;         // replay s rows
+    const int64_t* idx;     // [B] the minibatch's ring rows
+    const double* dz2;      // [ntiles * TB][256]
+    const double* h2;       // [ntiles * TB][256]
+    const double* dz3;      // [ntiles * TB][64]
+    int64_t batch;
+    int s1, s2;
+    int64_t chunk1, chunk2;  // samples per split (fc1 blocks / conv2 taps)
+    double* part;            // conv2 taps: [4][s2][64 o x 64 c]; then fc1: [4][s1][64 j x 64 k]
+};
+
+constexpr int NTW = 512;  // k_conv64_wgrad: eight waves, two per SIMD
+using WgTile = double[WKR][WAS];
+
+// One workgroup of k_conv64_wgrad: CW a conv2 tap (unit = tap), else an fc1 column block.
+// Waves 0 .. 3 multiply, waves 4 .. 7 stage: operands are double-buffered in LDS, and while the
+// multiplying waves run stage i's GEMM (one per SIMD, 16 k-steps x 4 MFMAs, rows 16 w), the
+// staging waves (one per SIMD beside it) write stage i + 1 into the other buffer -- global
+// operands fetched into their registers a stage earlier, the taps' conv1 on MFMA -- and fetch
+// stage i + 2; one barrier per stage.
+template <bool CW>
+__device__ __forceinline__ void wgrad_block(const WgArgs& A, WgTile* As, WgTile* Bs, int unit,
+                                            int split) {
+    const int t = threadIdx.x, l = t & 63, w = t >> 6, lr = l & 15, lk = l >> 4;
+    const bool stager = w >= 4;  // wave-uniform role
+    const int wr = w & 3, pt = t & 255;
+    const int64_t chunk = CW ? A.chunk2 : A.chunk1;
+    const int64_t k0 = (int64_t)split * chunk;
+    const int64_t k1 = k0 + chunk < A.batch ? k0 + chunk : A.batch;
+    constexpr int SPB = CW ? 16 : 64;  // samples per stage
+    // conv1 (CW, staging waves): this lane's weights for channel c = 16 wr + lr, tap lk; its input
+    // cells come from board lr of the stage, held in registers
+    const int c = 16 * wr + lr;
+    const double wb = CW && stager ? A.w1[c * 4 + lk] : 0.0, bc = CW && stager ? A.b1[c] : 0.0;
+    // a stage's global operands in the staging waves' registers.  CW: thread pt -> (b = (pt >> 6)
+    // + 4k, o = pt & 63), k < 4, its four dY (p = 0 .. 3), and board lr (ring rows two stages
+    // ahead, since the board load depends on them); fc1: (b = (pt >> 6) + 4k, col pt & 63), k < 16
+    const int col = pt & 63;
+    uint64_t blo = 0, bhi = 0;  // board lr of the fetched stage (two halves of the 128-bit row)
+    int64_t ridx = -1;          // its ring row for the stage after (-1: none)
+    double ga[16], gb[16];
+#define WG_FETCH(st0_)                                                                        \
+    do {                                                                                      \
+        const int64_t st0f = (st0_);                                                          \
+        if (CW) {                                                                             \
+            blo = 0, bhi = 0;                                                                 \
+            if (ridx >= 0) {                                                                  \
+                const uint4 v = A.s[ridx];                                                    \
+                blo = (uint64_t)v.x | ((uint64_t)v.y << 32);                                  \
+                bhi = (uint64_t)v.z | ((uint64_t)v.w << 32);                                  \
+            }                                                                                 \
+            const int64_t nb0 = st0f + SPB + lr;                                              \
+            ridx = nb0 < k1 ? A.idx[nb0] : -1;                                                \
+            _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                   \
+                const int64_t b = st0f + (pt >> 6) + 4 * k;                                   \
+                double2 p0 = make_double2(0.0, 0.0), p1 = p0;                                 \
+                if (b < k1) {                                                                 \
+                    const double2* src =                                                      \
+                        reinterpret_cast<const double2*>(A.dz2 + b * 256 + col * 4);          \
+                    p0 = src[0];                                                              \
+                    p1 = src[1];                                                              \
+                }                                                                             \
+                ga[4 * k] = p0.x, ga[4 * k + 1] = p0.y, ga[4 * k + 2] = p1.x,                 \
+                ga[4 * k + 3] = p1.y;                                                         \
+            }                                                                                 \
+        } else {                                                                              \
+            _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                  \
+                const int64_t b = st0f + (pt >> 6) + 4 * k;                                   \
+                const bool ok = b < k1;                                                       \
+                ga[k] = ok ? A.dz3[b * 64 + col] : 0.0;                                       \
+                gb[k] = ok ? A.h2[b * 256 + 64 * unit + col] : 0.0;                           \
+            }                                                                                 \
+        }                                                                                     \
+    } while (0)
+    // the fetched stage -> LDS buffer bf_; CW: conv1 at the tap's positions pos(p, tap) on MFMA
+    // (lane: boards 4r + lk, channel c), bias + relu -> Bs[(b, p)][c] -- conv1_mfma's arithmetic,
+    // so the values (and the relu mask) are train B's.  Cell (r, c) of a board is byte c of word r:
+    // bits 8 (4r + c) of the 128-bit row
+#define WG_PUT(bf_)                                                                           \
+    do {                                                                                      \
+        WgTile& At = As[(bf_)];                                                               \
+        WgTile& Bt = Bs[(bf_)];                                                               \
+        if (CW) {                                                                             \
+            _Pragma("unroll") for (int k = 0; k < 4; ++k)                                     \
+                _Pragma("unroll") for (int p = 0; p < 4; ++p)                                 \
+                    At[((pt >> 6) + 4 * k) * 4 + p][col] = ga[4 * k + p];                     \
+            _Pragma("unroll") for (int p = 0; p < 4; ++p) {                                   \
+                const int q = pos_of(p, unit);                                                \
+                const int rr = q / 3 + (lk >> 1), cc = q % 3 + (lk & 1);                      \
+                const uint64_t half = rr >= 2 ? bhi : blo;                                    \
+                const double xv =                                                             \
+                    (double)((uint32_t)(half >> (8 * (4 * (rr & 1) + cc))) & 0xFFu);          \
+                const d4 dq = mfma(xv, wb, d4{0.0, 0.0, 0.0, 0.0});                           \
+                _Pragma("unroll") for (int r = 0; r < 4; ++r) {                               \
+                    const double a = dq[r] + bc;                                              \
+                    Bt[(4 * r + lk) * 4 + p][c] = a > 0.0 ? a : 0.0;                          \
+                }                                                                             \
+            }                                                                                 \
+        } else {                                                                              \
+            _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                  \
+                At[(pt >> 6) + 4 * k][col] = ga[k];                                           \
+                Bt[(pt >> 6) + 4 * k][col] = gb[k];                                           \
+            }                                                                                 \
+        }                                                                                     \
+    } while (0)
+    if (stager && k0 < k1) {
+        if (CW) ridx = k0 + lr < k1 ? A.idx[k0 + lr] : -1;
+        WG_FETCH(k0);
+        WG_PUT(0);
+        if (k0 + SPB < k1) WG_FETCH(k0 + SPB);
+    }
+    __syncthreads();
+    d4 acc[4];
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) acc[nb] = d4{0.0, 0.0, 0.0, 0.0};
+    int bf = 0;
+    for (int64_t st0 = k0; st0 < k1; st0 += SPB, bf ^= 1) {
+        if (!stager) {
+            // the GEMM: 16 k-steps of 4 K-rows, rows 16 w, 4 column blocks
+            const WgTile& At = As[bf];
+            const WgTile& Bt = Bs[bf];
+#pragma unroll
+            for (int s4 = 0; s4 < WKR / 4; ++s4) {
+                const int kr = 4 * s4 + lk;
+                const double av = At[kr][16 * wr + lr];
+                double bv[4];
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) bv[nb] = Bt[kr][16 * nb + lr];
+#ifndef G2048_TIMING_WG_NOGEMM
+#pragma unroll
+                for (int nb = 0; nb < 4; ++nb) acc[nb] = mfma(av, bv[nb], acc[nb]);
+#else
+                acc[0][0] += av + bv[0] + bv[1] + bv[2] + bv[3];
+#endif
+            }
+        }
+#ifndef G2048_TIMING_WG_NOPUT
+        else if (st0 + SPB < k1) {  // the next stage into the other buffer (last read before
+            WG_PUT(bf ^ 1);         // the previous barrier), the one after it into registers
+            if (st0 + 2 * SPB < k1) WG_FETCH(st0 + 2 * SPB);
+        }
+#endif
+        __syncthreads();
+    }
+#undef WG_FETCH
+#undef WG_PUT
+    if (stager) return;
+    // the partial: row 16 w + 4r + lk, column 16nb + lr
+    const int64_t slot =
+        CW ? (int64_t)unit * A.s2 + split : (int64_t)4 * A.s2 + unit * A.s1 + split;
+    double* out = A.part + slot * WG_BLOCK;
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(16 * wr + 4 * r + lk) * 64 + 16 * nb + lr] = acc[nb][r];
+}
+
+__global__ __launch_bounds__(NTW) void k_conv64_wgrad(WgArgs A) {
+    __shared__ WgTile As[2];  // A operand, [K-row][row]: dY [(b, p)][o] / dZ3 [b][j]
+    __shared__ WgTile Bs[2];  // B operand, [K-row][col]: d [(b, p)][c] / H2 [b][k]
+    const int nw2 = 4 * A.s2;
+    if ((int)blockIdx.x < nw2)
+        wgrad_block<true>(A, As, Bs, (int)blockIdx.x / A.s2, (int)blockIdx.x % A.s2);
+    else
+        wgrad_block<false>(A, As, Bs, ((int)blockIdx.x - nw2) / A.s1,
+                           ((int)blockIdx.x - nw2) % A.s1);
+}
+
 constexpr int RW = 16;
 static_assert(MAX_WG % RW == 0 && SLAB % 2 == 0, "reduction: MAX_WG / RW slabs per wave, pairs");
 
@@ -1396,6 +1633,10 @@ struct RedArgs {
     double lr, b1, b2, eps;
     int adam;
     double* pk;  // the packed operands to re-pack after Adam (null: none)
+    // GW mode: conv2.weight's and fc1.weight's gradients from k_conv64_wgrad's partials
+    // (null: from the slabs)
+    const double* part;
+    int nsplit1, nsplit2;
 };
 
 // Block = 128 positions (two per lane, 16-byte loads) x RW waves: wave w sums slabs w, w + RW,
@@ -1432,6 +1673,33 @@ __global__ __launch_bounds__(64 * RW) void k_conv64_reduce(RedArgs A) {
                            ? *reinterpret_cast<const double2*>(A.pre + pos)
                            : make_double2(0.0, 0.0);
     double2 r = make_double2(0.0, 0.0);
+    // GW mode: conv2.weight (o, c, tap) = the tap-unit's partials at (o, c) summed in split
+    // order; fc1.weight (j, k) = the block k >> 6's.  Wave w takes the splits w, w + RW, ... and
+    // the waves are added below, as for the slabs
+    const bool gw_w2 = A.part != nullptr && pos >= P_W2 && pos < P_B2;
+    const bool gw_f1 = A.part != nullptr && pos >= P_F1 && pos < P_FB1;
+    if (gw_w2) {  // pos even: (o, c, tap), (o, c, tap + 1): two tap units
+        const int i = pos - P_W2, o = i >> 8, cc = (i >> 2) & 63, tap = i & 3;
+#pragma unroll
+        for (int h = 0; h < WG_MAX_SPLIT / RW; ++h) {
+            const int sp = wave + RW * h;
+            if (sp >= A.nsplit2) break;
+            r.x += A.part[((int64_t)tap * A.nsplit2 + sp) * WG_BLOCK + o * 64 + cc];
+            r.y += A.part[((int64_t)(tap + 1) * A.nsplit2 + sp) * WG_BLOCK + o * 64 + cc];
+        }
+    } else if (gw_f1) {  // pos even: (j, k), (j, k + 1) in one 64-column block
+        const int i = pos - P_F1, j = i >> 8, k = i & 255;
+#pragma unroll
+        for (int h = 0; h < WG_MAX_SPLIT / RW; ++h) {
+            const int sp = wave + RW * h;
+            if (sp >= A.nsplit1) break;
+            const double2 v = *reinterpret_cast<const double2*>(
+                A.part + ((int64_t)4 * A.nsplit2 + (k >> 6) * A.nsplit1 + sp) * WG_BLOCK +
+                j * 64 + (k & 63));
+            r.x += v.x;
+            r.y += v.y;
+        }
+    } else
 #ifdef G2048_TIMING_NO_WGRAD
     // the timing-only build reads no conv2.weight slab terms (a K = B GEMM leaves a handful of
     // partials for them, not 256 slabs)
@@ -1725,11 +1993,23 @@ static bool train_a_four_waves() {
     return !(e && e[0] == '8');
 }
 
+// GW mode (the weight gradients of conv2 / fc1 as K = B GEMMs, k_conv64_wgrad) when
+// G2048_CONV64_WGRAD=gemm, else the per-workgroup slabs of round 5 (read per call; the workspace
+// holds both forms' buffers).  Measured (B = 8192): 149.6 us per update against 143.4
+// -- k_conv64_wgrad takes 34 us, of which its operand staging alone is 20 -- so the slabs are the
+// default and the GEMM form is kept, parity-tested, for the record and for larger nets.
+static bool wgrad_gemm() {
+    const char* e = getenv("G2048_CONV64_WGRAD");
+    return e && e[0] == 'g';
+}
+
 extern "C" G2048_API int64_t g2048_convnet_update_f64_workspace(int64_t batch) {
     if (batch <= 0) return 0;
     const int64_t tiles = (batch + TB - 1) / TB;
     // the packed operands | the next-step word (+ pad) | slabs | dZ2 rows | train B's slab sums
-    return WS_SLAB + (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + SLAB;
+    // | (GW) H2 rows | dZ3 rows | the GEMMs' partials
+    return WS_SLAB + (int64_t)grid_of(batch) * SLAB + tiles * TB * 256 + SLAB +
+           tiles * TB * (256 + 64) + wgrad_part_doubles(batch);
 }
 
 extern "C" G2048_API int g2048_convnet_update_f64(
@@ -1755,7 +2035,13 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     unsigned long long* step_next = reinterpret_cast<unsigned long long*>(workspace + WS_STEP);
     double* slab = workspace + WS_SLAB;
     double* dz2 = slab + (int64_t)grid * SLAB;
-    double* pre = grid >= SHADOW_MIN_GRID ? dz2 + ((batch + TB - 1) / TB) * TB * 256 : nullptr;
+    const int64_t rows = ((batch + TB - 1) / TB) * TB;
+    const bool gw = wgrad_gemm();
+    double* pre = !gw && grid >= SHADOW_MIN_GRID ? dz2 + rows * 256 : nullptr;
+    double* h2g = dz2 + rows * 256 + SLAB;
+    double* dz3g = h2g + rows * 256;
+    double* part = dz3g + rows * 64;
+    const WgSplit wsp = wgrad_splits(batch);
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 
     // with Adam folded in, the packed operands are current (g2048_convnet_pack_f64 or the
@@ -1809,11 +2095,34 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     A.dz2 = dz2;
     A.slab = slab;
     A.pre = pre;
-    if (train_a_four_waves())
-        hipLaunchKernelGGL(k_conv64_train_a, dim3(grid), dim3(NT), 0, st, FA);
-    else
-        hipLaunchKernelGGL(k_conv64_train_a8, dim3(grid), dim3(NT8), 0, st, FA);
-    hipLaunchKernelGGL(k_conv64_train_b, dim3(grid), dim3(NT), 0, st, A);
+    A.h2g = h2g;
+    A.dz3g = dz3g;
+    if (gw) {
+        hipLaunchKernelGGL(k_conv64_train_a<true>, dim3(grid), dim3(NT), 0, st, FA);
+        hipLaunchKernelGGL(k_conv64_train_b<true>, dim3(grid), dim3(NT), 0, st, A);
+        WgArgs G;
+        G.w1 = online->w1;
+        G.b1 = online->b1;
+        G.s = R.s;
+        G.idx = idx_out;
+        G.dz2 = dz2;
+        G.h2 = h2g;
+        G.dz3 = dz3g;
+        G.batch = batch;
+        G.s1 = wsp.s1;
+        G.s2 = wsp.s2;
+        const int64_t st_f = (batch + 63) / 64, st_w = (batch + 15) / 16;
+        G.chunk1 = (st_f + wsp.s1 - 1) / wsp.s1 * 64;
+        G.chunk2 = (st_w + wsp.s2 - 1) / wsp.s2 * 16;
+        G.part = part;
+        hipLaunchKernelGGL(k_conv64_wgrad, dim3(4 * (wsp.s1 + wsp.s2)), dim3(NTW), 0, st, G);
+    } else {
+        if (train_a_four_waves())
+            hipLaunchKernelGGL(k_conv64_train_a<false>, dim3(grid), dim3(NT), 0, st, FA);
+        else
+            hipLaunchKernelGGL(k_conv64_train_a8, dim3(grid), dim3(NT8), 0, st, FA);
+        hipLaunchKernelGGL(k_conv64_train_b<false>, dim3(grid), dim3(NT), 0, st, A);
+    }
 
     RedArgs D;
     D.slab = slab;
@@ -1840,6 +2149,9 @@ extern "C" G2048_API int g2048_convnet_update_f64(
     D.eps = eps;
     D.adam = adam ? 1 : 0;
     D.pk = adam ? pk : nullptr;
+    D.part = gw ? part : nullptr;
+    D.nsplit1 = wsp.s1;
+    D.nsplit2 = wsp.s2;
     hipLaunchKernelGGL(k_conv64_reduce, dim3((P_N + 1 + 127) / 128), dim3(64 * RW), 0, st, D);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? G2048_OK

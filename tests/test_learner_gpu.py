@@ -206,14 +206,21 @@ def test_fused_target_sync_on_device(G, net, graph):
     assert int(L.step_dev) == 4 == L.updates
 
 
-@pytest.mark.parametrize("net", ["dense64", "conv"])
-def test_fused_f64_matches_reference(G, golden_dir, net):
+@pytest.mark.parametrize("net", ["dense64", "conv", "conv-gemm"])
+def test_fused_f64_matches_reference(G, golden_dir, net, monkeypatch):
     """The fused float64 updates (g2048_dense64_update_f64 / g2048_convnet_update_f64,
     DQNLearner(dtype=float64)) against the reference train_step fixture: loss within 1e-6
     absolute, y, the gradient and the parameters after one Adam step (src/dqn_lib.py:119-164,
-    intended order) to 1e-10 relative (gradient: 1e-10 of its largest element)."""
+    intended order) to 1e-10 relative (gradient: 1e-10 of its largest element).  conv-gemm: the
+    conv update with its conv2 / fc1 weight gradients as K = B GEMMs (G2048_CONV64_WGRAD=gemm)."""
     from g2048.learner import DQNLearner
     from g2048.nets import det_init, make_net
+
+    if net == "conv-gemm":
+        monkeypatch.setenv("G2048_CONV64_WGRAD", "gemm")
+        net = "conv"
+    else:
+        monkeypatch.delenv("G2048_CONV64_WGRAD", raising=False)
 
     g = fixture(golden_dir, net)
     rb = loaded_replay(G, g)
@@ -507,7 +514,9 @@ def test_conv64_train_a8_equals_four_wave(G, batch, double_dqn):
     """The eight-wave train A (k_conv64_train_a8, two waves per SIMD) keeps every sum of the
     four-wave k_conv64_train_a in the same order: three float64 conv updates with each (the
     eight-wave one selected by G2048_CONV64_TRAIN_A=8) agree bit for bit -- y, loss, the summed
-    gradient (the reduce writes it beside the folded Adam) and both nets' weights."""
+    gradient (the reduce writes it beside the folded Adam) and both nets' weights.  Both in the
+    slab form of the weight gradients (G2048_CONV64_WGRAD=slab), the only one with an eight-wave
+    train A."""
     from g2048.learner import DQNLearner
 
     n = 2048
@@ -515,6 +524,7 @@ def test_conv64_train_a8_equals_four_wave(G, batch, double_dqn):
     rb = G.ReplayBuffer(16 * n, device=DEV)
     env.rollout(16, replay=rb)
     outs = []
+    os.environ["G2048_CONV64_WGRAD"] = "slab"
     for eight in (False, True):
         if eight:
             os.environ["G2048_CONV64_TRAIN_A"] = "8"
@@ -532,4 +542,57 @@ def test_conv64_train_a8_equals_four_wave(G, batch, double_dqn):
             outs.append(torch.cat(res))
         finally:
             os.environ.pop("G2048_CONV64_TRAIN_A", None)
+    os.environ.pop("G2048_CONV64_WGRAD", None)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("double_dqn", [True, False])
+@pytest.mark.parametrize("batch", [1, 33, 700, 4096, 8192, 20000])
+def test_conv64_wgrad_gemm_equals_slabs(G, batch, double_dqn, monkeypatch):
+    """The float64 conv update's two forms of the conv2 / fc1 weight gradients -- K = B GEMMs
+    over stored operands (k_conv64_wgrad, direct form per conv2 tap; G2048_CONV64_WGRAD=gemm)
+    and the per-workgroup slabs (the default) -- from the same state (weights, Adam
+    moments, update counter copied before every update): y bitwise, the loss to 1e-14 relative
+    (the slab form may run the eight-wave train A, whose loss sums in another order), every
+    gradient tensor to 1e-12 relative (float64 summation order), three updates; the GEMM form
+    run to run bitwise."""
+    from g2048.learner import DQNLearner
+
+    n = 2048
+    env = G.VecEnv2048(n, seed=37, device=DEV)
+    rb = G.ReplayBuffer(16 * n, device=DEV)
+    env.rollout(16, replay=rb)
+    Ls = [DQNLearner(rb, net="conv", dtype=torch.float64, batch_size=batch, seed=6,
+                     target_sync_every=2, graph=False, use_double_dqn=double_dqn,
+                     data_parallel=True)  # gradient-only updates: grad_flat is the summed gradient
+          for _ in range(3)]
+    modes = ("gemm", "slab", "gemm")
+
+    def state(L):
+        return (list(L.model.parameters()) + list(L.target.parameters())
+                + [L._adam.exp_avg, L._adam.exp_avg_sq, L.step_dev])
+
+    for it in range(3):
+        with torch.no_grad():
+            for L in (Ls[0], Ls[2]):
+                for x, y in zip(state(L), state(Ls[1])):
+                    x.copy_(y)
+        got = []
+        for L, mode in zip(Ls, modes):
+            if mode == "gemm":
+                monkeypatch.setenv("G2048_CONV64_WGRAD", "gemm")
+            else:
+                monkeypatch.delenv("G2048_CONV64_WGRAD", raising=False)
+            L.update()
+            torch.cuda.synchronize()
+            got.append((L._y.clone(), L.last_loss.clone(), L.grad_flat.clone()))
+        (ya, la, ga), (yb, lb, gb), (yc, lc, gc) = got
+        assert torch.equal(ya, yb), it
+        assert abs(float(la) - float(lb)) <= 1e-14 * abs(float(lb)), (it, float(la), float(lb))
+        assert torch.equal(ga, gc) and torch.equal(la, lc), it  # run to run
+        off = 0
+        for i, p in enumerate(Ls[0].model.parameters()):
+            sz = p.numel()
+            x, y = ga[off:off + sz], gb[off:off + sz]
+            assert float((x - y).norm()) <= 1e-12 * float(y.norm()) + 1e-300, (it, i, batch)
+            off += sz

@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6 (m): GEMM-form parity subset, then the wgrad probe timings (r06l)
+set -o pipefail
+export PYTHONUNBUFFERED=1
+mkdir -p gpurun_out/r06m
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread \
+  tests/test_learner_gpu.py -k "wgrad or fused_f64 or conv64" > gpurun_out/r06m/tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/r06m/tests.log
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_r06l.sh

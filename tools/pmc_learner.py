@@ -21,7 +21,7 @@ import statistics
 import sys
 from collections import defaultdict
 
-KERNELS = {"k_conv64_train_a8", "k_conv64_train_a", "k_conv64_train_b", "k_conv64_reduce", "k_pack",
+KERNELS = {"k_conv64_train_a8", "k_conv64_train_a", "k_conv64_train_b", "k_conv64_wgrad", "k_conv64_reduce", "k_pack",
            "k_conv_targets_persist", "k_conv_train_fwd", "k_conv_train_bwd", "k_reduce_pre",
            "k_reduce_slabs", "k_dense_sample", "k_dense_forward", "k_dense_rows", "k_dense_wgrad",
            "k_dense_reduce", "k_mlp_update1", "k_mlp_update", "k_mlp_reduce",
