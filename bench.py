@@ -44,9 +44,10 @@ FP64_PEAK_TF = 78.6    # dense f64 peak
 #   board / meta / episode counters are read and written once per launch (not per step)
 ROLLOUT_BYTES = 38
 #   one launch per step, random mode: board 16 R + 16 W + reward 4 + done 1 = 37 B;
-#   with the bookkeeping the kernel moves as well (meta 8 R + 8 W, legal 1): 54 B
+#   with the bookkeeping the kernel moves as well (the score row 4 R + 4 W, legal 1): 46 B --
+#   54 B up to ABI v4, whose meta held {score, moves} per board (8 R + 8 W every step)
 STEP_BYTES = 37
-STEP_BYTES_BOOKKEEPING = 54
+STEP_BYTES_BOOKKEEPING = 46
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r06")
 PMC_FILE = os.path.join(PROFILE_DIR, "pmc.json")
 # the learner kernels' PMC passes (tools/gpu_pmc_learner.sh -> tools/pmc_learner.py)
@@ -455,8 +456,8 @@ def bench_step(args, world, rank, dev):
 
     wall, ev = timed(world, dev, run_all, 1)
     env.check_errors()
-    # the launch floor here: a graph-replayed device copy of the kernel's board + meta bytes
-    src = torch.zeros((n, 24), dtype=torch.uint8, device=dev)
+    # the launch floor here: a graph-replayed device copy of the kernel's board + score bytes
+    src = torch.zeros((n, 20), dtype=torch.uint8, device=dev)
     dst = torch.empty_like(src)
     gf = capture(lambda: dst.copy_(src), 100)
     gf.replay()

@@ -6,8 +6,9 @@
  * Usage:  abi_demo [n_boards [steps [rollout_k [out.bin]]]]   (default 65536 1000 0)
  * Runs `steps` random-policy g2048_env_step calls and one g2048_env_rollout of rollout_k steps
  * on device 0 with a replay ring of 16 rows per board, samples one B = 8192 f32 minibatch, and
- * (with out.bin) writes the final boards u8[n][16] then meta u32[n][2] to out.bin, so a test can
- * compare them with the CPU oracle (tests/test_abi_gpu.py).  Needs an MI355X at run time. */
+ * (with out.bin) writes the final boards u8[n][16] then {score, moves} u32[n][2]
+ * (g2048_env_score_moves) to out.bin, so a test can compare them with the CPU oracle
+ * (tests/test_abi_gpu.py).  Needs an MI355X at run time. */
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -57,14 +58,17 @@ int main(int argc, char** argv) {
     int64_t bad = 0;
     CHECK(g2048_env_error_count(env, &bad, NULL));  /* synchronises the stream */
     uint8_t* board = NULL;
-    uint32_t* meta = NULL;
-    CHECK(g2048_env_views(env, &board, &meta, NULL, NULL));
+    CHECK(g2048_env_views(env, &board, NULL, NULL, NULL));
     if (out) {
         uint8_t* hb = (uint8_t*)malloc((size_t)n * 16);
         uint32_t* hm = (uint32_t*)malloc((size_t)n * 8);
+        uint32_t* sm = NULL;  /* {score, moves} per board, derived from meta and the clock */
         if (!hb || !hm) return 1;
+        HCHECK(hipMalloc((void**)&sm, (size_t)n * 8));
+        CHECK(g2048_env_score_moves(env, sm, NULL));
         HCHECK(hipMemcpy(hb, board, (size_t)n * 16, hipMemcpyDeviceToHost));
-        HCHECK(hipMemcpy(hm, meta, (size_t)n * 8, hipMemcpyDeviceToHost));
+        HCHECK(hipMemcpy(hm, sm, (size_t)n * 8, hipMemcpyDeviceToHost));
+        hipFree(sm);
         FILE* f = fopen(out, "wb");
         if (!f || fwrite(hb, 1, (size_t)n * 16, f) != (size_t)n * 16 ||
             fwrite(hm, 1, (size_t)n * 8, f) != (size_t)n * 8 || fclose(f) != 0)

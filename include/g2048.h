@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define G2048_ABI_VERSION 4
+#define G2048_ABI_VERSION 5
 
 #ifndef G2048_API
 #define G2048_API __attribute__((visibility("default")))
@@ -87,10 +87,12 @@ typedef struct {
 } g2048_episode;
 
 /* ---- environment -------------------------------------------------------------------------
- * State per board i: board u8[16]; meta u32[2] = {score, moves} (score = Board2048._mergescore,
- * moves = len(_action_history) of the running episode); ep u32[4] = {episodes finished, last
- * score, last moves, last max exponent} (the Experiment.add_episode fields,
- * src/experiments.py:112-122).  Per group of 64 boards (boards 64g .. 64g+63): clock u64[g] =
+ * State per board i: board u8[16]; meta u32[2][n] (two rows): meta[0][i] = score
+ * (Board2048._mergescore), meta[1][i] = start = the step clock (low 32 bits) at which the running
+ * episode began, so moves = len(_action_history) = (uint32_t)(clock - start) is derived, not
+ * stored (ABI v5; v4 held {score, moves} per board, a read-modify-write of both every step --
+ * g2048_env_score_moves writes that pair layout); ep u32[4] = {episodes finished, last score,
+ * last moves, last max exponent} (the Experiment.add_episode fields, src/experiments.py:112-122).  Per group of 64 boards (boards 64g .. 64g+63): clock u64[g] =
  * the number of steps taken, i.e. the Philox counter of the next step and the replay row it
  * appends to.  Every step call advances every board, so all clocks of an env hold the same
  * value; each group is read and advanced only by the wavefront that steps its boards, so no
@@ -105,7 +107,7 @@ typedef struct {
 /* Replaces `Board2048()` x n_boards (src/board.py:10-20): allocates and resets n boards. */
 G2048_API int g2048_env_create(g2048_env** out, int64_t n_boards, uint64_t seed, uint64_t board_offset,
                      int device_id, uint32_t flags, void* stream);
-/* Same, over caller-owned device buffers board u8[n][16], meta u32[n][2], ep u32[n][4],
+/* Same, over caller-owned device buffers board u8[n][16], meta u32[2][n], ep u32[n][4],
  * clock u64[G2048_CLOCK_WORDS(n)] (board/ep 16-byte, meta/clock 8-byte aligned).  If reset != 0
  * the boards are reset (2 spawns each), else left as given; the clock is used as given (all
  * words equal: zero for a fresh env). */
@@ -117,6 +119,11 @@ G2048_API void g2048_env_destroy(g2048_env* env);
 G2048_API int g2048_env_views(g2048_env* env, uint8_t** board_dev, uint32_t** meta_dev,
                               uint32_t** ep_dev, uint64_t** clock_dev);
 G2048_API int64_t g2048_env_size(const g2048_env* env);
+
+/* {score, moves} of every board as u32[n][2] (out_dev 8-byte aligned): Board2048.merge_score()
+ * (src/board.py:207) and len(_action_history) (src/experiments.py:112-122 number_moves), from meta
+ * and the clock -- the v4 meta layout, for hosts that read it. */
+G2048_API int g2048_env_score_moves(g2048_env* env, uint32_t* out_dev, void* stream);
 
 /* Re-deal fresh boards (2 spawns, src/board.py:18-20) where reset_mask_dev[i] != 0 (all if NULL). */
 G2048_API int g2048_env_reset(g2048_env* env, const uint8_t* reset_mask_dev, void* stream);

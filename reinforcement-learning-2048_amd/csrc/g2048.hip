@@ -3,7 +3,11 @@
 //
 // HBM layout (one env = one shard of boards, SoA):
 //   board u8[N][16]   exponents                       (one uint4 per board)
-//   meta  u32[N][2]   {score, moves}                  (one uint2 per board)
+//   meta  u32[2][N]   row 0: score; row 1: start = the step clock (low word) at which the running
+//                     episode began, so moves = clock - start (mod 2^32) is derived, never
+//                     stored: a one-launch step reads and writes 4 B of meta per board, and the
+//                     start row is written only when an episode ends (ABI v5; v4 held {score,
+//                     moves} per board and moved 16 B per step)
 //   ep    u32[N][4]   {episodes, last score, last moves, last max exponent} (read with the board
 //                     only where the step needs it; written on done)
 //   clock u64[N/64]   the step counter of each 64-board group (all equal: every call steps every
@@ -76,7 +80,8 @@ struct ReplayDev {
 
 struct StepArgs {
     uint4* board;
-    uint2* meta;
+    uint32_t* score;  // meta row 0
+    uint32_t* start;  // meta row 1
     uint4* ep;
     uint64_t* clock;
     int64_t n;
@@ -106,6 +111,18 @@ struct StepArgs {
 };
 
 __device__ __forceinline__ Board load_board(const uint4 v) { return Board{v.x, v.y, v.z, v.w}; }
+
+// {score, moves} of board i at clock t (the rollouts carry both in registers)
+__device__ __forceinline__ uint2 load_meta(const StepArgs& A, int64_t i, uint64_t t) {
+    return make_uint2(A.score[i], (uint32_t)t - A.start[i]);
+}
+// ... and back at clock t1: the start row only if an episode ended in the launch (otherwise
+// t1 - moves is the start it was loaded with)
+__device__ __forceinline__ void store_meta(const StepArgs& A, int64_t i, uint64_t t1, uint2 m,
+                                           bool ended) {
+    A.score[i] = m.x;
+    if (ended) A.start[i] = (uint32_t)t1 - m.y;
+}
 
 // The step counter of board i's 64-board group as a wave-uniform (SGPR) value.  Every lane of the
 // wave loads the same word; the wave's first lane is always live (groups start at 64-aligned
@@ -168,6 +185,8 @@ __device__ __forceinline__ void end_episode(const StepArgs& A, int64_t i, uint64
 
 // One transition of board i (global id gid) at step t (the group clock).  Mirrors o2048_env_step
 // (oracle/oracle2048.c), which restates src/dqn_lib.py:91-107 + src/board.py.
+// m.x is the score; the episode's moves are read (clock - start) only on a terminal step, and a
+// re-dealt board's start row is written there -- a one-launch step moves 4 B of meta, not 16.
 // kPre: the caller loaded ep (and qs, when a q-sum buffer is attached) together with the board.
 // Otherwise they are loaded here on done only -- 16 B less traffic per board, at the price of a
 // dependent memory round trip for every wave that holds a terminal board.
@@ -242,7 +261,6 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
         }
     }
     m.x += r;
-    m.y += 1u;
 
     if (A.rb.rows) {
         const int64_t slot = (int64_t)ring_row(t, A.rb.rows) * A.n + i;
@@ -260,6 +278,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
                 if (A.qsum) qs = A.qsum[i];
             }
         }
+        m.y = (uint32_t)(t + 1u) - A.start[i];  // this terminal step included
         end_episode<kGreedy>(A, i, gid, t, b, m, ep, qs);
         if (!(A.flags & G2048_NO_AUTORESET)) {
             if constexpr (MODE == MODE_RANDOM)
@@ -268,6 +287,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
             else
                 b = fresh_board(u, A.p4_thresh);  // the step's own block (see fresh_board)
             m = make_uint2(0u, 0u);
+            A.start[i] = (uint32_t)(t + 1u);
         }
     }
     rew_out = (int32_t)r;
@@ -290,7 +310,7 @@ __device__ __forceinline__ void bump_count(const StepArgs& A, uint64_t t_next) {
 // kernel-argument preloading (16 SGPRs), so they arrive in SGPRs and neither the board loads nor
 // the draw wait for a scalar load of the argument block.
 template <int MODE, bool kFull, bool kPre, int BS>
-__global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2* __restrict__ meta_p,
+__global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint32_t* __restrict__ score_p,
                                              uint4* ep_p, uint64_t* clock_p, uint64_t board_offset,
                                              uint32_t seed_lo, uint32_t seed_hi,
                                              uint32_t p4_thresh, uint32_t flags, StepArgs A) {
@@ -303,7 +323,7 @@ __global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2*
     A.flags = flags;
     const uint64_t t = load_clock_s<BS>(clock_p);
     Board b = load_board(board_p[i]);
-    uint2 m = meta_p[i];
+    uint2 m = make_uint2(score_p[i], 0u);
     uint4 ep = kPre ? ep_p[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
@@ -320,7 +340,7 @@ __global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint2*
     step_one<MODE, kPre>(A, i, board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
                          act, ep);
     board_p[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    meta_p[i] = m;
+    score_p[i] = m.x;
     if ((i & 63) == 0) clock_p[i >> 6] = t + 1u;
     if (kGreedy && A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
@@ -361,7 +381,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     if (live) {
         b = load_board(A.board[i]);
         if (half == 0 || !q_out) {
-            m = A.meta[i];
+            m = make_uint2(A.score[i], 0u);
             ep = A.ep[i];
         }
     }
@@ -417,7 +437,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     step_one<MODE_EG_REG>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done, legal,
                           act, ep, q);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    A.score[i] = m.x;
     if (lane == 0) A.clock[blockIdx.x] = t + 1u;  // wave 1 read it before the barrier
     if (A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
@@ -447,7 +467,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const 
     if (live) {
         b = load_board(A.board[i]);
         if (half == 0 || !q_out) {
-            m = A.meta[i];
+            m = make_uint2(A.score[i], 0u);
             ep = A.ep[i];
         }
     }
@@ -499,7 +519,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const 
     step_one<MODE_EG_REG64>(A, i, A.board_offset + (uint64_t)i, t, b, m, eps, qs, rew, done,
                             legal, act, ep, float4{0, 0, 0, 0}, q);
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    A.score[i] = m.x;
     if (lane == 0) A.clock[blockIdx.x] = t + 1u;  // wave 1 read it before the barrier
     if (A.qsum) A.qsum[i] = qs;
     if (A.reward) A.reward[i] = rew;
@@ -556,7 +576,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     G2048_ROLL_MARK(0);
     const uint64_t t0 = load_clock(A.clock, i);
     Board b = load_board(A.board[i]);
-    uint2 m = A.meta[i];
+    uint2 m = load_meta(A, i, t0);
     uint4 ep = A.ep[i];
     const uint64_t gid = A.board_offset + (uint64_t)i;
     const bool autoreset = !(A.flags & G2048_NO_AUTORESET);
@@ -658,7 +678,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kSum ? 5
     G2048_ROLL_MARK(2);
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    store_meta(A, i, t1, m, ep.x != ep0);
     if (ep.x != ep0) {
         ep.w = max_exp(last);
         A.ep[i] = ep;
@@ -695,11 +715,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
     // latencies overlap (the prologue is a few steps' worth of a 64-step launch)
     uint64_t c0 = 0;
     uint4 bv = make_uint4(0, 0, 0, 0), ep = bv;
-    uint2 m = make_uint2(0, 0);
+    uint2 m = make_uint2(0, 0);  // {score, start} until t0 is known, then {score, moves}
     if (live) {
         c0 = A.clock[i >> 6];
         bv = A.board[i];
-        m = A.meta[i];
+        m = make_uint2(A.score[i], A.start[i]);
         ep = A.ep[i];
     }
     if (threadIdx.x < 16)
@@ -710,6 +730,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
     __syncthreads();
     if (!live) return;
     const uint64_t t0 = first_lane_u64(c0);
+    m.y = (uint32_t)t0 - m.y;
     Board b = load_board(bv);
     const uint64_t gid = A.board_offset + (uint64_t)i;
     const uint32_t p4 = A.p4_thresh;
@@ -861,7 +882,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
     }
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    store_meta(A, i, t1, m, ep.x != ep0);
     if (ep.x != ep0) {
         ep.w = max_exp(last);
         A.ep[i] = ep;
@@ -872,8 +893,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves))
     if (i == 0) bump_count(A, t1);
 }
 
-__global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint2* meta, int64_t n,
-                                                  uint64_t board_offset, uint32_t seed_lo,
+__global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint32_t* meta, const uint64_t* clock,
+                                                  int64_t n, uint64_t board_offset, uint32_t seed_lo,
                                                   uint32_t seed_hi, uint32_t p4_thresh,
                                                   uint32_t epoch, const uint8_t* mask) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -882,7 +903,16 @@ __global__ __launch_bounds__(kBlock) void k_reset(uint4* board, uint2* meta, int
     const Board b = fresh_board(
         draw(seed_lo, seed_hi, board_offset + (uint64_t)i, DOMAIN_RESET, epoch), p4_thresh);
     board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    meta[i] = make_uint2(0u, 0u);  // score, moves; the step clock keeps running
+    meta[i] = 0u;                           // score
+    meta[n + i] = (uint32_t)clock[i >> 6];  // a new episode starts at the running clock: 0 moves
+}
+
+// The {score, moves} pairs of ABI v4 (g2048_env_score_moves): out[i] = {score, clock - start}.
+__global__ __launch_bounds__(kBlock) void k_score_moves(const uint32_t* meta, const uint64_t* clock,
+                                                        int64_t n, uint2* out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    out[i] = make_uint2(meta[i], (uint32_t)clock[i >> 6] - meta[n + i]);
 }
 
 // available_moves_as_torch_unit_vector (src/board.py:128-135) of every board, as a bit mask.
@@ -1122,7 +1152,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
     uint4 ep = make_uint4(0, 0, 0, 0);
     if (live) {
         b = load_board(A.board[i]);
-        m = A.meta[i];
+        m = load_meta(A, i, t0);
         ep = A.ep[i];
     }
     const uint64_t gid = A.board_offset + (uint64_t)i;
@@ -1185,7 +1215,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws(StepArgs A) {
     if (!live || !ok) return;
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    store_meta(A, i, t1, m, ep.x != ep0);
     if (ep.x != ep0) {
         ep.w = max_exp(last);
         A.ep[i] = ep;
@@ -1201,7 +1231,7 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBloc
 int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
     DeviceGuard g(e->device);
     hipLaunchKernelGGL(k_reset, dim3(grid_for(e->n)), dim3(kBlock), 0, st,
-                       reinterpret_cast<uint4*>(e->board), reinterpret_cast<uint2*>(e->meta), e->n,
+                       reinterpret_cast<uint4*>(e->board), e->meta, e->clock, e->n,
                        e->board_offset, (uint32_t)e->seed, (uint32_t)(e->seed >> 32),
                        p4_thresh(e->flags), e->epoch, mask);
     G_HIP(hipGetLastError());
@@ -1212,7 +1242,8 @@ int launch_reset(g2048_env* e, const uint8_t* mask, hipStream_t st) {
 int make_args(g2048_env* e, g2048_replay* rb, StepArgs& A) {
     std::memset(&A, 0, sizeof(A));
     A.board = reinterpret_cast<uint4*>(e->board);
-    A.meta = reinterpret_cast<uint2*>(e->meta);
+    A.score = e->meta;
+    A.start = e->meta + e->n;
     A.ep = reinterpret_cast<uint4*>(e->ep);
     A.clock = e->clock;
     A.n = e->n;
@@ -1276,19 +1307,19 @@ void launch_step_k(g2048_env* e, const StepArgs& A, hipStream_t st) {
         const unsigned grid = (unsigned)((e->n + BS - 1) / BS);
         if (e->n % BS == 0)
             hipLaunchKernelGGL((k_step<MODE, true, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
-                               A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                               A.score, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
                                A.p4_thresh, A.flags, A);
         else
             hipLaunchKernelGGL((k_step<MODE, false, kPre, BS>), dim3(grid), dim3(BS), 0, st, A.board,
-                               A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                               A.score, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
                                A.p4_thresh, A.flags, A);
     } else if (e->n % kBlock == 0) {
         hipLaunchKernelGGL((k_step<MODE, true, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock), 0,
-                           st, A.board, A.meta, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
+                           st, A.board, A.score, A.ep, A.clock, A.board_offset, A.seed_lo, A.seed_hi,
                            A.p4_thresh, A.flags, A);
     } else {
         hipLaunchKernelGGL((k_step<MODE, false, kPre, kBlock>), dim3(grid_for(e->n)), dim3(kBlock),
-                           0, st, A.board, A.meta, A.ep, A.clock, A.board_offset, A.seed_lo,
+                           0, st, A.board, A.score, A.ep, A.clock, A.board_offset, A.seed_lo,
                            A.seed_hi, A.p4_thresh, A.flags, A);
     }
 }
@@ -1462,6 +1493,17 @@ int g2048_env_set_episode_log(g2048_env* e, g2048_episode* log, int64_t slots_pe
     e->log = log;
     e->log_slots = log ? slots_per_board : 0;
     e->qsum = log ? qsum : nullptr;
+    return G2048_OK;
+}
+
+int g2048_env_score_moves(g2048_env* e, uint32_t* out, void* stream) {
+    if (!e || !out) return fail(G2048_EINVAL, "env_score_moves: NULL argument");
+    if ((uintptr_t)out & 7u) return fail(G2048_EINVAL, "env_score_moves: out must be 8-byte aligned");
+    DeviceGuard g(e->device);
+    hipLaunchKernelGGL(k_score_moves, dim3(grid_for(e->n)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), e->meta, e->clock, e->n,
+                       reinterpret_cast<uint2*>(out));
+    G_HIP(hipGetLastError());
     return G2048_OK;
 }
 

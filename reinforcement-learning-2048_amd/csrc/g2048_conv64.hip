@@ -1227,6 +1227,10 @@ __global__ __launch_bounds__(NT) void k_conv64_train_b(TrainArgs A) {
             }
         }
         CPHASE(14);
+        // every wave's conv1 reads all 16 rows of M.x, which wave 0 wrote above (until round 6
+        // there was no barrier here: the other waves' dM stores usually outlasted wave 0's row
+        // stores, and a run where they did not produced a wrong conv1 gradient block)
+        __syncthreads();
         const uint64_t mask = conv1_mfma<false>(M.x, M.d, M.sw);
         __syncthreads();
         // the next tile's row and dZ2 (HBM), issued at the start of dW2, whose operands all come

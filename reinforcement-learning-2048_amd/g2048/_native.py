@@ -18,7 +18,7 @@ G2048_OK, G2048_EINVAL, G2048_EHIP, G2048_ENOMEM, G2048_EBADINPUT = 0, -1, -2, -
 P4_10, EGREEDY_FIXED, NO_AUTORESET = 1, 2, 4
 F32, F64 = 0, 1
 ASTAR_SPAWN_PHILOX, ASTAR_SPAWN_FIRST_EMPTY = 0, 1
-ABI_VERSION = 4  # include/g2048.h G2048_ABI_VERSION
+ABI_VERSION = 5  # include/g2048.h G2048_ABI_VERSION
 MAX_BOARDS = (1 << 31) - 256  # include/g2048.h G2048_MAX_BOARDS
 REPLAY_SECTION_PAD = 4352  # include/g2048.h G2048_REPLAY_SECTION_PAD
 
@@ -44,6 +44,7 @@ SIGNATURES = {
     "g2048_env_set_epoch": (_int, [_vp, _u32]),
     "g2048_env_set_episode_log": (_int, [_vp, _vp, _i64, _vp]),
     "g2048_env_legal_mask": (_int, [_vp, _vp, _vp]),
+    "g2048_env_score_moves": (_int, [_vp, _vp, _vp]),
     "g2048_env_step_egreedy_dense64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp, _vp,
                                               _vp, _vp]),
     "g2048_env_step_egreedy_dense64_f64": (_int, [_vp, _vp, _vp, _dbl, _dbl, _dbl, _vp, _vp, _vp, _vp,

@@ -148,7 +148,7 @@ def play_one_step(env: VecEnv2048, epsilon, model: torch.nn.Module, replay_buffe
     else:
         q = q_values(env, model, board_to_tensor_function)
     s = env.board.clone() if custom else None
-    score0 = (env.meta[:, 0].to(torch.int64) & 0xFFFFFFFF) if custom else None  # u32 in int32
+    score0 = (env.score.to(torch.int64) & 0xFFFFFFFF) if custom else None  # u32 in int32
     row0 = int(env.clock[0]) % (replay_buffer.capacity // env.n) * env.n if custom else 0
     action, reward, done = env.step_egreedy(q, epsilon, replay=replay_buffer)
     if custom:

@@ -89,7 +89,10 @@ class VecEnv2048:
     """N independent 2048 boards on one GPU, stepped by the HIP kernels in csrc/g2048.hip.
 
     board  uint8 [N, 16]  log2 exponents (== Board2048.log_scale().state, src/board.py:224-231)
-    meta   int32 [N, 2]   {score (= merge_score()), moves (= len(_action_history))}
+    meta   int32 [2, N]   row 0: score (= merge_score()); row 1: the step clock (low 32 bits) at
+                          which the running episode began -- moves (= len(_action_history)) is
+                          clock - start, derived (ABI v5: a one-launch step moves 4 B of meta);
+                          score_moves() gives the [N, 2] {score, moves} pairs
     ep     int32 [N, 4]   {episodes finished, last score, last moves, last max exponent}
     clock  int64 [ceil(N/64)]  steps taken by each 64-board group (all equal; the Philox counter)
     """
@@ -112,7 +115,7 @@ class VecEnv2048:
         lib = N.load()
         kw = dict(device=self.device)
         self.board = torch.zeros((self.n, 16), dtype=torch.uint8, **kw)
-        self.meta = torch.zeros((self.n, 2), dtype=torch.int32, **kw)
+        self.meta = torch.zeros((2, self.n), dtype=torch.int32, **kw)
         self.ep = torch.zeros((self.n, 4), dtype=torch.int32, **kw)
         self.clock = torch.zeros(((self.n + 63) // 64,), dtype=torch.int64, **kw)
         self._h = C.c_void_p()
@@ -302,11 +305,19 @@ class VecEnv2048:
     # ------------------------------------------------------------------ views
     @property
     def score(self):          # Board2048.merge_score(), src/board.py:207
-        return self.meta[:, 0]
+        return self.meta[0]
 
     @property
-    def moves(self):          # len(Board2048._action_history)
-        return self.meta[:, 1]
+    def moves(self):          # len(Board2048._action_history): clock - episode start (mod 2^32)
+        return self.score_moves()[:, 1]
+
+    def score_moves(self) -> torch.Tensor:
+        """int32 [N, 2] {score, moves} of every board (g2048_env_score_moves; the u32 values in
+        int32, as the v4 meta layout held them)."""
+        out = torch.empty((self.n, 2), dtype=torch.int32, device=self.device)
+        N.check(N.load().g2048_env_score_moves(self._h, N.ptr(out), self._stream()),
+                "g2048_env_score_moves")
+        return out
 
     @property
     def steps(self):

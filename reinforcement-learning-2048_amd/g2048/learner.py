@@ -30,11 +30,25 @@ from .optim import FusedAdam
 #   1 (round 1): env meta [N, 4], no clock;
 #   2 (round 2): meta [N, 2] + a per-wave clock, ABI-v2 random-policy draws (no version key was
 #                written then; load_state_dict infers 1 / 2 from the meta shape);
-#   3: the layout of 2 with the ABI-v3 random policy (include/g2048.h), whose draws differ.
-TRAINER_STATE_VERSION = 3
+#   3: the layout of 2 with the ABI-v3 random policy (include/g2048.h), whose draws differ;
+#   4 (ABI v5): env meta [2, N] = {score row, episode-start clock row}; a version-3 state is read
+#     by converting its {score, moves} pairs (start = clock - moves).
+TRAINER_STATE_VERSION = 4
 _STATE_LAYOUTS = {1: "env meta [N, 4], no step clock", 2: "env meta [N, 2] + per-wave clock, ABI-v2 "
                   "random-policy draws", 3: "env meta [N, 2] + per-wave clock, ABI-v3 random-policy "
-                  "draws"}
+                  "draws", 4: "env meta [2, N] {score, episode start} + per-wave clock, ABI-v3 "
+                  "random-policy draws"}
+_READABLE = (3, 4)
+
+
+def meta_from_score_moves(sm: torch.Tensor, clock: torch.Tensor) -> torch.Tensor:
+    """A version-3 env meta ([N, 2] {score, moves}, int32) as the v4 rows [2, N] {score, start}:
+    start = (the board's group clock - moves) mod 2^32, stored as int32."""
+    n = sm.shape[0]
+    lo = clock.to(torch.int64).repeat_interleave(64)[:n] & 0xFFFFFFFF
+    start = (lo - (sm[:, 1].to(torch.int64) & 0xFFFFFFFF)) & 0xFFFFFFFF
+    start = torch.where(start >= 1 << 31, start - (1 << 32), start).to(torch.int32)
+    return torch.stack([sm[:, 0].to(torch.int32), start])
 
 
 def _state_version(st: dict) -> int:
@@ -444,7 +458,7 @@ class Trainer:
             self.h_d = torch.zeros((self.history_len, self.track), dtype=torch.uint8, **kw)
             self.h_t0 = self.steps  # first trainer step the ring holds
             # per tracked board: its running episode starts inside the window (no moves yet)
-            self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
+            self._clean = (env.moves[:self.track] == 0).cpu().numpy()
         self._action = torch.empty(env.n, dtype=torch.uint8, device=env.device)
         self._reward = torch.empty(env.n, dtype=torch.int32, device=env.device)
         self._done = torch.empty(env.n, dtype=torch.uint8, device=env.device)
@@ -660,7 +674,7 @@ class Trainer:
     def load_state_dict(self, st: dict) -> None:
         self._loop_graph = None  # host-side env state (the reset epoch) is baked into a capture
         fmt = _state_version(st)
-        if fmt != TRAINER_STATE_VERSION:
+        if fmt not in _READABLE:
             raise ValueError(
                 f"trainer state version {fmt} ({_STATE_LAYOUTS.get(fmt, 'unknown layout')}) is not "
                 f"readable by this build (version {TRAINER_STATE_VERSION}: "
@@ -673,7 +687,8 @@ class Trainer:
         if st["replay"]["capacity"] != rb.capacity:
             raise ValueError("checkpoint replay capacity differs")
         env.board.copy_(e["board"])
-        env.meta.copy_(e["meta"])
+        env.meta.copy_(e["meta"] if fmt == TRAINER_STATE_VERSION
+                       else meta_from_score_moves(e["meta"], e["clock"]))
         env.ep.copy_(e["ep"])
         env.clock.copy_(e["clock"])
         env.epoch = e["epoch"]
@@ -694,7 +709,7 @@ class Trainer:
         self.learner.load_state_dict(st["learner"])
         if self.track:
             self.h_t0 = self.steps
-            self._clean = (env.meta[:self.track, 1] == 0).cpu().numpy()
+            self._clean = (env.moves[:self.track] == 0).cpu().numpy()
 
 
 def _flat_adam_state(per_param: list, params) -> dict:

@@ -172,7 +172,7 @@ class BatchedPlayer:
         t = 0
         while True:
             before = env.board[:k].clone() if k else None
-            score_before = env.meta[:k, 0].clone() if k else None
+            score_before = env.score[:k].clone() if k else None
             if policy == "random":
                 act, reward, done = env.step_egreedy(q0, 1.0)
                 ended = done.bool()
@@ -193,8 +193,9 @@ class BatchedPlayer:
                 newly_stuck = illegal & ~ended & ~fin
                 ended = ended | newly_stuck
             new = ended & ~fin
-            f_score = torch.where(new, env.meta[:, 0].to(torch.int64), f_score)
-            f_moves = torch.where(new, env.meta[:, 1].to(torch.int64), f_moves)
+            sm = env.score_moves().to(torch.int64)
+            f_score = torch.where(new, sm[:, 0], f_score)
+            f_moves = torch.where(new, sm[:, 1], f_moves)
             f_max = torch.where(new, env.board.amax(dim=1).to(torch.int64), f_max)
             if newly_stuck is not None:
                 stuck |= newly_stuck

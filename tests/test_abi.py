@@ -18,7 +18,7 @@ def _declared():
 def test_header_declares_abi():
     names = _declared()
     assert "g2048_env_step" in names and "g2048_replay_sample_encode" in names
-    assert len(names) == 55
+    assert len(names) == 56
 
 
 def test_library_exports_every_declared_symbol():
@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in _declared():
         assert hasattr(lib, name), name
     assert set(_declared()) == set(N.SIGNATURES)
-    assert lib.g2048_abi_version() == 4
+    assert lib.g2048_abi_version() == 5
     out = subprocess.run(["nm", "-D", "--defined-only", N.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     exported = sorted(set(re.findall(r" T (g2048_\w+)", out)))

@@ -46,12 +46,12 @@ def test_custom_reward_function(g2048):
 
     for t in range(5):
         row0 = (6 + t) % 4 * n
-        before = env.meta[:, 0].clone().long()
+        before = env.score.clone().long()
         _, a, r, d, _ = dqn_lib.play_one_step(env, 1.0, None, rb, reward_function=ref_style)
         gain = rb.r[row0:row0 + n].long()
         assert torch.equal(r.long(), gain) and int(gain.sum()) > 0, t
         live = d == 0  # the env re-deals terminal boards (score 0), the ring keeps the transition
-        assert torch.equal((before + gain)[live], env.meta[:, 0].long()[live]), t
+        assert torch.equal((before + gain)[live], env.score.long()[live]), t
 
     def halves(board, next_board, action, done):
         return torch.full((board.n,), 0.5, device=board.device)

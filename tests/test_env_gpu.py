@@ -178,7 +178,7 @@ def test_random_steps_with_replay_vs_oracle(g2048, n, flags):
             assert np.array_equal(_np(r), o["reward"]), step
             assert np.array_equal(_np(d), o["done"]), step
             assert np.array_equal(_np(lg), o["legal"]), step
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
     assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
     assert (ref.clock == 120).all()
@@ -202,7 +202,7 @@ def test_steps_across_clock_moves(g2048):
     def check(tag):
         torch.cuda.synchronize()
         assert np.array_equal(_np(env.board), ref.board), tag
-        assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta), tag
+        assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta), tag
         assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock), tag
 
     def steps(k, tag):
@@ -244,7 +244,7 @@ def test_actions_in_vs_oracle(g2048):
         o = ref.step(O.MODE_ACTIONS, actions=a)
         assert np.array_equal(_np(r), o["reward"]), step
     assert np.array_equal(_np(env.board), ref.board)
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
 
 
 @pytest.mark.parametrize("qdtype", [np.float32, np.float64])
@@ -428,7 +428,7 @@ def test_empty_board_is_terminal(g2048, autoreset):
         outs = [ref.step(O.MODE_RANDOM, replay=ref_rb) for _ in range(5)]
         assert outs[0]["done"][::3].all() and outs[0]["legal"][::3].max() == 0
         assert np.array_equal(_np(env.board), ref.board), use_rollout
-        assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta), use_rollout
+        assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta), use_rollout
         assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep), use_rollout
         for name in ["s", "s2", "a", "r", "d", "count"]:
             assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), (name, use_rollout)
@@ -455,7 +455,7 @@ def test_rollout_vs_oracle(g2048):
     for _ in range(50):
         ref.step(O.MODE_RANDOM, replay=ref_rb)
     assert np.array_equal(_np(env.board), ref.board)
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
     assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
     for name in ["s", "s2", "a", "r", "d", "count"]:
@@ -477,7 +477,7 @@ def test_large_random_steps_vs_oracle(g2048):
         assert np.array_equal(_np(r), o["reward"]), step
         assert np.array_equal(_np(d), o["done"]), step
     assert np.array_equal(_np(env.board), ref.board)
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     assert np.array_equal(_np(env.clock).view(np.uint64), ref.clock)
     for name in ["s", "s2", "a", "r", "d", "count"]:
         assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
@@ -533,7 +533,7 @@ def test_reset_mask_and_episode_stats(g2048):
     env.reset(torch.from_numpy(mask).to(DEV))
     ref.reset(mask)
     assert np.array_equal(_np(env.board), ref.board)
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
 
 
@@ -792,6 +792,9 @@ def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     ref_rb = O.OracleReplay(rows * n)
     t0 = (1 << 32) - 5
     env.clock.fill_(t0)
+    # the episodes start at t0 too: meta's start row holds the clock's low word (ABI v5), so
+    # moving the clock without it would count t0 moves
+    env.meta[1].fill_(t0 - (1 << 32))  # (uint32) t0 as int32
     ref.clock[:] = t0
     for step in range(4):
         r, d, lg = env.step(None, replay=rb)
@@ -810,6 +813,6 @@ def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     assert int(ref.clock[0]) == t0 + 12 and t0 + 12 > (1 << 32)
     assert int(_np(rb.count)[0]) == int(ref_rb.count[0]) == rows * n
     assert np.array_equal(_np(env.board), ref.board)
-    assert np.array_equal(_np(env.meta).view(np.uint32), ref.meta)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     for name in ["s", "s2", "a", "r", "d"]:
         assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name

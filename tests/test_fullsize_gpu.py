@@ -40,7 +40,7 @@ def test_bench_rollout_full_size_vs_oracle(g2048):
     rb = g2048.ReplayBuffer(N * K, device=DEV)
     env.rollout(K, replay=rb)
     torch.cuda.synchronize()
-    board, meta, ep = _np(env.board), _np(env.meta).view(np.uint32), _np(env.ep).view(np.uint32)
+    board, meta, ep = _np(env.board), _np(env.score_moves()).view(np.uint32), _np(env.ep).view(np.uint32)
     ring = {name: _np(getattr(rb, name)) for name in ["s", "s2", "a", "r", "d"]}
     assert int(rb.count) == N * K
     assert (_np(env.clock).view(np.uint64) == K).all()
@@ -247,7 +247,7 @@ def test_max_boards_vs_oracle(g2048):
             ref.step(O.MODE_RANDOM)
         sl = slice(i0, i0 + n)
         assert np.array_equal(_np(env.board[sl]), ref.board), i0
-        assert np.array_equal(_np(env.meta[sl]).view(np.uint32), ref.meta), i0
+        assert np.array_equal(_np(env.score_moves()[sl]).view(np.uint32), ref.meta), i0
         assert np.array_equal(_np(env.ep[sl]).view(np.uint32), ref.ep), i0
     clock = env.clock[-1:]
     assert int(clock) == 6

@@ -187,9 +187,31 @@ def test_trainer_state_version_inference():
     """States written before the version key existed: round 1 (meta [N, 4]) and round 2
     (meta [N, 2] + clock) are told apart by the meta shape."""
     from g2048.learner import _state_version, TRAINER_STATE_VERSION
-    assert _state_version({"trainer_state_version": 3}) == TRAINER_STATE_VERSION == 3
+    assert _state_version({"trainer_state_version": 4}) == TRAINER_STATE_VERSION == 4
+    assert _state_version({"trainer_state_version": 3}) == 3
     assert _state_version({"env": {"meta": torch.zeros((5, 4))}}) == 1
     assert _state_version({"env": {"meta": torch.zeros((5, 2))}}) == 2
+
+
+def test_meta_from_score_moves():
+    """A version-3 env meta ({score, moves} per board) as the ABI-v5 rows {score, start}:
+    start = group clock - moves (mod 2^32), so clock - start gives the moves back -- also
+    across a clock past 2^32 and moves past the clock's low word."""
+    from g2048.learner import meta_from_score_moves
+    n = 130
+    g = torch.Generator().manual_seed(5)
+    score = torch.randint(0, 1 << 20, (n,), generator=g, dtype=torch.int64)
+    moves = torch.randint(0, 1 << 31, (n,), generator=g, dtype=torch.int64)
+    moves[:3] = torch.tensor([0, 1, (1 << 31) + 5])  # a u32 count held in int32
+    clock = torch.tensor([7, (1 << 32) + 3, 1 << 40], dtype=torch.int64)
+    sm = torch.stack([score, moves], 1)
+    sm = torch.where(sm >= 1 << 31, sm - (1 << 32), sm).to(torch.int32)
+    m = meta_from_score_moves(sm, clock)
+    assert m.shape == (2, n) and m.dtype == torch.int32
+    assert torch.equal(m[0], sm[:, 0])
+    lo = clock.repeat_interleave(64)[:n] & 0xFFFFFFFF
+    back = (lo - (m[1].to(torch.int64) & 0xFFFFFFFF)) & 0xFFFFFFFF
+    assert torch.equal(back, sm[:, 1].to(torch.int64) & 0xFFFFFFFF)
 
 
 def test_board_batch_accessors():

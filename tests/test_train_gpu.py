@@ -112,6 +112,32 @@ def test_resume_round4_dense_checkpoint(G):
                                                             fused=False, kind="")))
 
 
+def test_resume_version3_trainer_state(G):
+    """A trainer state of rounds 3-5 (version 3: env meta [N, 2] {score, moves}, ABI v4) resumes
+    on the ABI-v5 env (meta rows {score, episode start}): its pairs become rows with start =
+    clock - moves, and the run continues bit for bit -- boards, score / moves, episode counters,
+    the ring, the episode log and the learner."""
+    a = _small(G, "conv")
+    for _ in range(12):
+        a.step()
+    st = a.state_dict()
+    assert st["trainer_state_version"] == 4 and tuple(st["env"]["meta"].shape) == (2, a.env.n)
+    old = dict(st, trainer_state_version=3,
+               env=dict(st["env"], meta=a.env.score_moves().cpu().clone()))
+    for _ in range(9):
+        a.step()
+    want = _fingerprint(a)
+    b = _small(G, "conv")
+    b.load_state_dict(old)
+    assert torch.equal(b.env.meta.cpu(), st["env"]["meta"])
+    for _ in range(9):
+        b.step()
+    got = _fingerprint(b)
+    for k in ("board", "meta", "clock", "ep", "replay_s", "count", "log", "loss"):
+        assert torch.equal(got[k], want[k]), k
+    assert torch.equal(b.env.score_moves(), a.env.score_moves())
+
+
 def test_load_rejects_mismatch(G):
     a = _small(G, "conv")
     st = a.state_dict()

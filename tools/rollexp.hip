@@ -126,7 +126,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws_barrier(StepArgs A) {
     uint4 ep = make_uint4(0, 0, 0, 0);
     if (live) {
         b = load_board(A.board[i]);
-        m = A.meta[i];
+        m = load_meta(A, i, t0);
         ep = A.ep[i];
     }
     const uint64_t gid = A.board_offset + (uint64_t)i;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(2 * kBlock) void k_rollout_ws_barrier(StepArgs A) {
     if (!live) return;
     const uint64_t t1 = t0 + (uint64_t)K;
     A.board[i] = make_uint4(b.r0, b.r1, b.r2, b.r3);
-    A.meta[i] = m;
+    store_meta(A, i, t1, m, ep.x != ep0);
     if (ep.x != ep0) {
         ep.w = max_exp(last);
         A.ep[i] = ep;

@@ -36,7 +36,7 @@ def soak(n_all, k, launches, seed):
             ref.step(O.MODE_RANDOM, replay=ref_rb)
         sl = slice(i0, i0 + n)
         ok = (np.array_equal(env.board[sl].cpu().numpy(), ref.board) and
-              np.array_equal(env.meta[sl].cpu().numpy().view(np.uint32), ref.meta) and
+              np.array_equal(env.score_moves()[sl].cpu().numpy().view(np.uint32), ref.meta) and
               np.array_equal(env.ep[sl].cpu().numpy().view(np.uint32), ref.ep))
         # ring rows (row r of board i at r * n_all + i) vs the slice ring (r * n + (i - i0))
         ridx = (np.arange(rows)[:, None] * n_all + np.arange(i0, i0 + n)[None, :]).reshape(-1)

@@ -44,7 +44,7 @@ for i0 in (0, n // 2 - 500, n - 1000):
         o = ref.step(O.MODE_RANDOM, replay=ref_rb)
     sl = slice(i0, i0 + k)
     ok = (np.array_equal(env.board[sl].cpu().numpy(), ref.board) and
-          np.array_equal(env.meta[sl].cpu().numpy().view(np.uint32), ref.meta) and
+          np.array_equal(env.score_moves()[sl].cpu().numpy().view(np.uint32), ref.meta) and
           np.array_equal(env.ep[sl].cpu().numpy().view(np.uint32), ref.ep) and
           np.array_equal(r[sl].cpu().numpy(), o["reward"]) and
           np.array_equal(lg[sl].cpu().numpy(), o["legal"]))
