@@ -3,5 +3,5 @@
 # (the train-B conv1 staging race), then the learner timing of both forms
 set -o pipefail
 export PYTHONUNBUFFERED=1
-for b in 700 33 4096 8192; do timeout -k 10 120 python tools/scratch/gw_det.py $b slab || exit 1; done
+for b in 700 33 4096 8192; do timeout -k 10 120 python tools/conv64_wgrad_det.py $b slab || exit 1; done
 timeout -k 10 300 python tools/learner_ab.py "" conv
