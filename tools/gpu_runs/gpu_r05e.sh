@@ -4,5 +4,5 @@
 mkdir -p gpurun_out
 set -o pipefail
 export TMPDIR=/tmp
-bash tools/gpu_r05d.sh || exit 1
-bash tools/gpu_r05c.sh
+bash tools/gpu_runs/gpu_r05d.sh || exit 1
+bash tools/gpu_runs/gpu_r05c.sh

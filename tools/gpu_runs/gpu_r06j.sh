@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?
 tail -3 gpurun_out/r06j/tests.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/gpu_r06i.sh
+bash tools/gpu_runs/gpu_r06i.sh

@@ -8,4 +8,4 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 rc=$?
 tail -3 gpurun_out/r06m/tests.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/gpu_r06l.sh
+bash tools/gpu_runs/gpu_r06l.sh
