@@ -185,9 +185,10 @@ __device__ __forceinline__ void end_episode(const StepArgs& A, int64_t i, uint64
 
 // One transition of board i (global id gid) at step t (the group clock).  Mirrors o2048_env_step
 // (oracle/oracle2048.c), which restates src/dqn_lib.py:91-107 + src/board.py.
-// m.x is the score; the episode's moves are read (clock - start) only on a terminal step, and a
+// m.x is the score; the episode's moves (clock - start) are needed only on a terminal step, and a
 // re-dealt board's start row is written there -- a one-launch step moves 4 B of meta, not 16.
-// kPre: the caller loaded ep (and qs, when a q-sum buffer is attached) together with the board.
+// kPre: the caller loaded ep, the start row (in m.y) and qs (when a q-sum buffer is attached)
+// together with the board; otherwise ep and start are read on a terminal step only.
 // Otherwise they are loaded here on done only -- 16 B less traffic per board, at the price of a
 // dependent memory round trip for every wave that holds a terminal board.
 template <int MODE, bool kPre = true>
@@ -278,7 +279,7 @@ __device__ __forceinline__ void step_one(const StepArgs& A, int64_t i, uint64_t 
                 if (A.qsum) qs = A.qsum[i];
             }
         }
-        m.y = (uint32_t)(t + 1u) - A.start[i];  // this terminal step included
+        m.y = (uint32_t)(t + 1u) - (kPre ? m.y : A.start[i]);  // this terminal step included
         end_episode<kGreedy>(A, i, gid, t, b, m, ep, qs);
         if (!(A.flags & G2048_NO_AUTORESET)) {
             if constexpr (MODE == MODE_RANDOM)
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(BS) void k_step(uint4* __restrict__ board_p, uint32
     A.flags = flags;
     const uint64_t t = load_clock_s<BS>(clock_p);
     Board b = load_board(board_p[i]);
-    uint2 m = make_uint2(score_p[i], 0u);
+    uint2 m = make_uint2(score_p[i], kPre ? A.start[i] : 0u);
     uint4 ep = kPre ? ep_p[i] : make_uint4(0u, 0u, 0u, 0u);
     double eps = 0.0;
     if constexpr (MODE == MODE_EG_F32 || MODE == MODE_EG_F64) {
@@ -381,7 +382,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split(StepArgs A, const fl
     if (live) {
         b = load_board(A.board[i]);
         if (half == 0 || !q_out) {
-            m = make_uint2(A.score[i], 0u);
+            m = make_uint2(A.score[i], A.start[i]);  // step_one's kPre form
             ep = A.ep[i];
         }
     }
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(128) void k_step_dense64_split64(StepArgs A, const 
     if (live) {
         b = load_board(A.board[i]);
         if (half == 0 || !q_out) {
-            m = make_uint2(A.score[i], 0u);
+            m = make_uint2(A.score[i], A.start[i]);  // step_one's kPre form
             ep = A.ep[i];
         }
     }
