@@ -816,3 +816,59 @@ def test_clock_past_2_32_vs_oracle(g2048, n, rows):
     assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
     for name in ["s", "s2", "a", "r", "d"]:
         assert np.array_equal(_np(getattr(rb, name)), getattr(ref_rb, name)), name
+
+
+def test_meta_start_row_mid_episode_vs_oracle(g2048):
+    """ABI v5 meta: a caller-set state mid-episode -- clock C, scores, and moves m given as start
+    rows C - m (mod 2^32, so some starts wrap below zero) -- steps like the oracle holding
+    {score, m}: single steps, a rollout and an explicit reset, with score_moves() equal to the
+    oracle's pairs after each, and the start rows of boards that did not finish unchanged."""
+    n, seed = 1000, 0x5EED
+    rng = np.random.default_rng(3)
+    env = g2048.VecEnv2048(n, seed=seed, device=DEV)
+    ref = O.OracleEnv(n, seed=seed)
+    clock = 123_456
+    score = rng.integers(0, 1 << 20, n).astype(np.uint32)
+    moves = rng.integers(0, 1 << 31, n).astype(np.uint32)  # many moves > clock: starts wrap
+    moves[:5] = [0, 1, clock, clock + 1, (1 << 32) - 1]
+    start = (np.uint64(clock) - moves.astype(np.uint64)) & np.uint64(0xFFFFFFFF)
+    env.clock.fill_(clock)
+    env.meta[0].copy_(torch.from_numpy(score.view(np.int32)))
+    env.meta[1].copy_(torch.from_numpy(start.astype(np.uint32).view(np.int32)))
+    ref.clock[:] = clock
+    ref.meta[:, 0] = score
+    ref.meta[:, 1] = moves
+    ref.board[:] = _np(env.board)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
+    before = _np(env.meta[1]).copy()
+    for _ in range(3):
+        env.step(None)
+        ref.step(O.MODE_RANDOM)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
+    ended = _np(env.ep)[:, 0] > 0
+    assert np.array_equal(_np(env.meta[1])[~ended], before[~ended])
+    env.rollout(9)
+    for _ in range(9):
+        ref.step(O.MODE_RANDOM)
+    assert np.array_equal(_np(env.score_moves()).view(np.uint32), ref.meta)
+    mask = (np.arange(n) % 4 == 1).astype(np.uint8)
+    env.reset(torch.from_numpy(mask).to(DEV))
+    ref.reset(mask)
+    sm = _np(env.score_moves()).view(np.uint32)
+    assert np.array_equal(sm, ref.meta) and not sm[mask == 1].any()
+    assert np.array_equal(_np(env.board), ref.board)
+    assert np.array_equal(_np(env.ep).view(np.uint32), ref.ep)
+
+
+def test_score_moves_errors(g2048):
+    """g2048_env_score_moves: NULL arguments and a misaligned output are G2048_EINVAL."""
+    import ctypes as C
+    from g2048 import _native as N
+    env = g2048.VecEnv2048(64, device=DEV)
+    lib = N.load()
+    out = torch.zeros(64 * 2 + 2, dtype=torch.int32, device=DEV)
+    s = N.stream_of(env.device)
+    assert lib.g2048_env_score_moves(None, N.ptr(out), s) == N.G2048_EINVAL
+    assert lib.g2048_env_score_moves(env._h, None, s) == N.G2048_EINVAL
+    assert lib.g2048_env_score_moves(env._h, C.c_void_p(N.ptr(out) + 4), s) == N.G2048_EINVAL
+    assert lib.g2048_env_score_moves(env._h, N.ptr(out), s) == N.G2048_OK
