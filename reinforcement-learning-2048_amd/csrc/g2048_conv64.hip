@@ -9,6 +9,10 @@
 //                (+ the target sync on the device update counter), and the updated weights
 //                re-packed into f64-MFMA operand order (B fragments) for the next update: the
 //                online net's every update, the target net's when the sync fires
+// With G2048_CONV64_WGRAD=gemm (opt-in, measured slower: 149.6 against 143.7 us per update at
+// B = 8192) conv2.weight's and fc1.weight's gradients leave the train launches for a
+// fourth launch, k_conv64_wgrad: K = B GEMMs over H2 / dZ3 / dZ2 stored by train A, partials
+// summed by the reduce.
 // The packed operands live at the start of the workspace; g2048_convnet_pack_f64 (k_pack) writes
 // them from the weights as given.  Without Adam (grad_out only: a data-parallel learner applies
 // Adam after the all-reduce) the update packs at its start instead.
